@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: oblivious CRUD requests/s of the gvstore engine (BASELINE.json metric).
+
+One "step" = one batch of B synthetic requests through the whole pipeline
+(mailbox pass, allocation, message-table pass, mailbox write pass) with the
+requests already resident in HBM.  Default workload = BASELINE config 3:
+2^24 stored-message capacity prefilled to 75 %, 64K-request batches, a
+25/25/25/25 CREATE/READ/UPDATE/DELETE mix with half of the READ/DELETE asking
+for the next message (zero id), as SURVEY.md §8(d) specifies.
+
+Multi-GPU (`torch.distributed.run`): one process per GPU, each owning an
+independent store shard serving its own batches (weak scaling, no data-path
+collective in this round).  Rank 0 prints one JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md:36
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--log2n", type=int, default=24, help="log2 message capacity per GPU")
+    p.add_argument("--batch", type=int, default=65536)
+    p.add_argument("--fill", type=float, default=0.75)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return p.parse_args()
+
+
+def gen_batches(torch, dev, B, count, known, pool, g, ts0):
+    """Synthetic request slabs (B x 1040 bytes, gvs_request layout) on `dev`."""
+    out = []
+    nk = known.shape[0]
+    for b in range(count):
+        r = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
+        r[:, :1024] = torch.randint(0, 256, (B, 1024), dtype=torch.uint8, device=dev, generator=g)
+        r[:, 1024:] = 0
+        roll = torch.randint(0, 100, (B,), device=dev, generator=g)
+        typ = torch.where(roll < 25, 1, torch.where(roll < 50, 2, torch.where(roll < 75, 3, 4)))
+        nxt = (torch.randint(0, 100, (B,), device=dev, generator=g) < 50) & ((typ == 2) | (typ == 4))
+        byid = (typ != 1) & ~nxt
+        k = torch.randint(0, nk, (B,), device=dev, generator=g)
+        kn = known[k]  # (B, 80): id, sender, recipient
+        coin = torch.randint(0, 2, (B, 1), device=dev, generator=g).bool()
+        auth_byid = torch.where(coin, kn[:, 16:48], kn[:, 48:80])
+        pi = torch.randint(0, pool.shape[0], (B, 2), device=dev, generator=g)
+        auth = torch.where(byid[:, None], auth_byid, pool[pi[:, 0]])
+        auth = torch.where(nxt[:, None], kn[:, 48:80], auth)
+        rcpt = torch.where(byid[:, None], kn[:, 48:80], pool[pi[:, 1]])
+        mid = torch.where(byid[:, None], kn[:, 0:16], r[:, 0:16])
+        mid = torch.where(nxt[:, None], torch.zeros_like(mid), mid)
+        r[:, 0:16] = mid
+        r[:, 16:48] = auth
+        r[:, 48:80] = rcpt
+        ts = torch.arange(B, device=dev, dtype=torch.int64) + ts0 + b * B + 1
+        r[:, 80:88] = ts.view(torch.uint8).reshape(B, 8)
+        r[:, 1024:1028] = typ.to(torch.int32).view(torch.uint8).reshape(B, 4)
+        out.append(r)
+    return out
+
+
+def prefill(torch, store, dev, B, target, pool, g, ts0):
+    """Fill the store with `target` creates through the normal pipeline; returns
+    (id, sender, recipient) of every created message (device tensor n x 80)."""
+    known = []
+    done = 0
+    d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
+    while done < target:
+        n = min(B, target - done)
+        r = torch.empty((n, 1040), dtype=torch.uint8, device=dev)
+        r[:, :1024] = torch.randint(0, 256, (n, 1024), dtype=torch.uint8, device=dev, generator=g)
+        r[:, 1024:] = 0
+        pi = torch.randint(0, pool.shape[0], (n, 2), device=dev, generator=g)
+        r[:, 16:48] = pool[pi[:, 0]]
+        r[:, 48:80] = pool[pi[:, 1]]
+        ts = torch.arange(n, device=dev, dtype=torch.int64) + ts0 + done + 1
+        r[:, 80:88] = ts.view(torch.uint8).reshape(n, 8)
+        r[:, 1024] = 1
+        torch.cuda.synchronize(dev)
+        store.process_batch_device(r.data_ptr(), n, d_out.data_ptr())
+        ok = d_out[:n, 1024] == 1
+        known.append(d_out[:n][ok][:, 0:80].clone())
+        done += n
+    return torch.cat(known)
+
+
+def cpu_baseline(budget_s):
+    """The CPU oracle (sequential model, one core) on a bounded sample of the
+    same mix: 2^20 capacity prefilled to 75 %, C3 mix, timed for ~budget_s."""
+    from grapevine_amd import abi
+    from oracle import ffi
+    cfg = abi.make_config(1 << 20, max_batch=65536)
+    m = ffi.Model(cfg)
+    m.seed(0x6772617065 + 3)
+    fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=1 << 15)
+    for _ in range((3 << 18) // 65536):
+        m.process_batch(m.gen_batch(65536, fill))
+    mix = ffi.gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=0, bad_auth=0,
+                         bad_recipient=0, hard_error=0, zero_recipient=0, n_identities=1 << 15)
+    ops, t = 0, 0.0
+    while t < budget_s:
+        reqs = m.gen_batch(8192, mix)
+        t0 = time.perf_counter()
+        m.process_batch(reqs)
+        t += time.perf_counter() - t0
+        ops += len(reqs)
+    return {"value": ops / t, "unit": "req/s", "cores": 1, "kind": "port",
+            "sample": f"oracle seqmodel (plain sequential CPU handler), 2^20 capacity prefilled to 75%, "
+                      f"C3 mix, {ops} requests timed over {t:.1f}s on 1 core"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from grapevine_amd import abi
+    from grapevine_amd.store import ObliviousStore
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    N, B = 1 << a.log2n, a.batch
+    cfg = abi.make_config(N, max_batch=B, device=local)
+    store = ObliviousStore(cfg)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x6772617065 + 3 + 7919 * rank)
+    pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
+    pool[:, 0] |= 1
+    known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000)
+    batches = gen_batches(torch, dev, B, a.warmup + a.steps, known, pool, g, 1_800_000_000)
+    d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
+    store.set_timing(True)
+    torch.cuda.synchronize(dev)
+    for i in range(a.warmup):
+        store.process_batch_device(batches[i].data_ptr(), B, d_out.data_ptr())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stage = {}
+    for i in range(a.steps):
+        store.process_batch_device(batches[a.warmup + i].data_ptr(), B, d_out.data_ptr())
+        for k, v in store.last_timings().items():
+            stage[k] = stage.get(k, 0.0) + v
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stage_ms = {k: v / a.steps for k, v in stage.items()}
+    st = store.stats()
+    statuses = torch.bincount(d_out[:, 1024].to(torch.int64), minlength=9)[:9].tolist()
+
+    if rank == 0:
+        total = world * B * a.steps
+        rpass_ms = stage_ms.get("rpass", float("nan"))
+        # algorithmic bytes of one message-table pass: every row
+        # read + written, every request image read, every response written
+        alg_bytes = 2 * N * 1024 + B * (1024 + 1040)
+        achieved = alg_bytes / (rpass_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(a.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("log2n") == a.log2n and tj.get("batch") == B:
+                traffic = tj.get("rpass_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        cpu = None if a.no_cpu or world > 1 else cpu_baseline(a.cpu_seconds)
+        line = {
+            "metric": "oblivious CRUD req/s (node) at 2^24 msgs, 64K batch; % HBM peak",
+            "value": total / elapsed,
+            "unit": "req/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded on device): 75% prefill, 25/25/25/25 CRUD mix, 50% next-message reads/deletes",
+            "config": {"workload": f"C3: 2^{a.log2n} message capacity per GPU, {B}-request batches",
+                       "msg_capacity": N, "batch": B,
+                       "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,
+                       "parallelism": f"shards{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_rpass (message-table pass)",
+                         "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms},
+            "cpu_baseline": cpu,
+            "stage_ms": stage_ms,
+            "store": {"messages": st["messages"], "mailboxes": st["mailboxes"],
+                      "last_batch_status_hist": statuses},
+        }
+        print(json.dumps(line), flush=True)
+    store.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

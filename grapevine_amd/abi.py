@@ -1,0 +1,102 @@
+"""numpy / ctypes mirrors of the POD types in include/gvstore.h.
+
+The request layout puts the Record a CREATE would store first (README.md:132-136:
+16 B id, 32 B sender, 32 B recipient, 8 B timestamp, 936 B payload) with the
+request's auth_identity in the sender position; see include/gvstore.h.
+"""
+import ctypes
+
+import numpy as np
+
+MSG_ID_BYTES = 16
+KEY_BYTES = 32
+PAYLOAD_BYTES = 936
+RECORD_BYTES = 1024
+MAILBOX_SLOTS = 62
+
+# RequestType, types/src/lib.rs:16-22
+REQUEST_TYPE_CREATE = 1
+REQUEST_TYPE_READ = 2
+REQUEST_TYPE_UPDATE = 3
+REQUEST_TYPE_DELETE = 4
+
+# StatusCode, types/src/lib.rs:122-137 (0 = hard error, see gvstore.h)
+STATUS_HARD_ERROR = 0
+STATUS_CODE_SUCCESS = 1
+STATUS_CODE_NOT_FOUND = 2
+STATUS_CODE_MESSAGE_ID_ALREADY_IN_USE = 3
+STATUS_CODE_INVALID_RECIPIENT = 4
+STATUS_CODE_TOO_MANY_MESSAGES_FOR_RECIPIENT = 5
+STATUS_CODE_TOO_MANY_RECIPIENTS = 6
+STATUS_CODE_TOO_MANY_MESSAGES = 7
+STATUS_CODE_INTERNAL_ERROR = 8
+
+GVS_OK = 0
+GVS_ERR_INVALID_ARG = -1
+GVS_ERR_DEVICE = -2
+GVS_ERR_OUT_OF_MEMORY = -3
+GVS_ERR_BATCH_OVERFLOW = -4
+GVS_ERR_NO_DEVICE = -5
+GVS_ERR_INTERNAL = -6
+
+RECORD_DTYPE = np.dtype([
+    ("msg_id", "u1", 16),
+    ("sender", "u1", 32),
+    ("recipient", "u1", 32),
+    ("timestamp", "<u8"),
+    ("payload", "u1", PAYLOAD_BYTES),
+])
+REQUEST_DTYPE = np.dtype([
+    ("msg_id", "u1", 16),
+    ("auth_identity", "u1", 32),
+    ("recipient", "u1", 32),
+    ("timestamp", "<u8"),
+    ("payload", "u1", PAYLOAD_BYTES),
+    ("request_type", "<u4"),
+    ("reserved", "<u4", 3),
+])
+RESPONSE_DTYPE = np.dtype([
+    ("record", RECORD_DTYPE),
+    ("status_code", "<u4"),
+    ("reserved", "<u4", 3),
+])
+assert RECORD_DTYPE.itemsize == 1024
+assert REQUEST_DTYPE.itemsize == 1040
+assert RESPONSE_DTYPE.itemsize == 1040
+
+
+class GvsConfig(ctypes.Structure):
+    _fields_ = [
+        ("msg_capacity", ctypes.c_uint64),
+        ("mailbox_partitions", ctypes.c_uint32),
+        ("mailbox_partition_slots", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
+        ("device", ctypes.c_uint32),
+        ("secret_key", ctypes.c_uint8 * 32),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 7),
+    ]
+
+
+class GvsStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "messages", "mailboxes", "batches", "creation_counter", "free_ring_head",
+        "free_ring_tail", "msg_partitions", "msg_partition_slots")]
+
+
+def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,
+                max_batch=None, device=0, secret_key=None):
+    """Config mirroring gvs_config_init's defaults (R = N/16 mailboxes)."""
+    cfg = GvsConfig()
+    cfg.msg_capacity = msg_capacity
+    if mailbox_partitions is None:
+        r = max(msg_capacity // 16, 256)
+        mailbox_partitions = max(r // mailbox_partition_slots, 1)
+    cfg.mailbox_partitions = mailbox_partitions
+    cfg.mailbox_partition_slots = mailbox_partition_slots
+    cfg.max_batch = max_batch if max_batch is not None else (4096 if msg_capacity < 65536 else 65536)
+    cfg.device = device
+    key = secret_key if secret_key is not None else bytes((0x67 + 31 * i) & 0xFF for i in range(32))
+    for i in range(32):
+        cfg.secret_key[i] = key[i]
+    return cfg

@@ -1,0 +1,201 @@
+// gvs_device.h — device-side definitions shared by the gvstore kernels.
+//
+// Layouts:
+//   * message table: N rows of 1024 B (gvs_record layout, README.md:132-136),
+//     partition-major: slot s lives in partition w = s % W at offset o = s / W,
+//     row index w*S + o (S = N/W).  An all-zero msg_id marks an empty row
+//     (README.md:159-160: the zero id is invalid).
+//   * mailbox table: R = Q*S_r rows of 1024 B = recipient[32] + 62 ids x 16 B
+//     (README.md:78-80); lane l>=2 of a wave holds id l-2.  Side array of 16 B
+//     per row holds the recipient hash and the mailbox length.
+//   * request image: the first 1024 B of gvs_request are the Record a CREATE
+//     stores (sender = auth_identity), so images and rows share lane mapping.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gvs {
+
+constexpr uint32_t kIdTag = 0x47565331u;  // "GVS1", must match oracle
+constexpr uint32_t kPending = 0xFFu;      // internal status: decided later
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kGroupMax = 512;            // distinct recipients per mailbox partition per batch
+constexpr int kSrMax = 1024;              // mailbox rows per partition
+constexpr int kTile = 256;                // message rows per R-pass tile
+constexpr int kSeqBits = 20;              // B <= 2^20
+constexpr uint32_t kSeqMask = (1u << kSeqBits) - 1;
+
+enum Kind : uint32_t {
+  KIND_PAD = 0,
+  KIND_HARD = 1,
+  KIND_NEXT_READ = 2,
+  KIND_NEXT_DEL = 3,
+  KIND_CREATE = 4,
+  KIND_READ = 5,
+  KIND_UPDATE = 6,
+  KIND_DELETE = 7,
+};
+
+// cflag bits written by M1 (one u32 per op)
+constexpr uint32_t CF_POP = 1u;     // delete-next that pops a message
+constexpr uint32_t CF_MBOX_OK = 2u; // create passes the mailbox checks
+
+struct alignas(16) OpState {  // 64 B, seq-indexed, written by k_meta
+  uint32_t kind, pre_status, slot, q;
+  uint64_t ts, h_hi, h_lo;
+  uint32_t id[4];
+  uint32_t pad[2];
+};
+static_assert(sizeof(OpState) == 64, "OpState");
+
+struct alignas(16) M1Out {  // 32 B, seq-indexed, written by the M1 pass
+  uint32_t status, slot, flags, pad;
+  uint32_t id[4];
+};
+
+struct alignas(16) ROp {  // 64 B, seq-indexed: everything the R and M2 passes need
+  uint32_t status, slot, kind, flags;
+  uint32_t id[4];
+  uint32_t x[8];  // mailbox key (recipient / auth) for mailbox-touching ops
+};
+static_assert(sizeof(ROp) == 64, "ROp");
+
+struct alignas(16) Key128 {
+  uint64_t hi, lo;
+};
+
+struct Scal {  // persistent device scalars + per-batch temporaries
+  uint64_t count, ctr, head, tail, n_mailboxes, batches;
+  uint32_t error, pad0;
+  // per batch
+  uint64_t pops, scnt, m, count1, head0, tail0, nd;
+  uint64_t pad1[4];
+};
+
+struct KeyCtx {
+  uint64_t pk0, pk1, hk0, hk1;
+};
+
+// ------------------------------------------------------------- SipHash-2-4
+
+__host__ __device__ inline uint64_t rotl64(uint64_t x, int b) {
+  return (x << b) | (x >> (64 - b));
+}
+
+#define GVS_SIPROUND                                                          \
+  do {                                                                        \
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);             \
+    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                                  \
+    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                                  \
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);             \
+  } while (0)
+
+// SipHash-2-4 over full 8-byte blocks m[0..nb) followed by a final block
+// carrying `tail` (already packed little-endian) and total length `len`.
+__host__ __device__ inline uint64_t siphash24_blocks(uint64_t k0, uint64_t k1,
+                                                      const uint64_t* m, int nb,
+                                                      uint64_t tail, uint64_t len) {
+  uint64_t v0 = 0x736f6d6570736575ULL ^ k0;
+  uint64_t v1 = 0x646f72616e646f6dULL ^ k1;
+  uint64_t v2 = 0x6c7967656e657261ULL ^ k0;
+  uint64_t v3 = 0x7465646279746573ULL ^ k1;
+  for (int i = 0; i < nb; ++i) {
+    v3 ^= m[i];
+    GVS_SIPROUND;
+    GVS_SIPROUND;
+    v0 ^= m[i];
+  }
+  uint64_t b = (len << 56) | tail;
+  v3 ^= b;
+  GVS_SIPROUND;
+  GVS_SIPROUND;
+  v0 ^= b;
+  v2 ^= 0xff;
+  GVS_SIPROUND;
+  GVS_SIPROUND;
+  GVS_SIPROUND;
+  GVS_SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
+__host__ __device__ inline uint64_t feistel_f(const KeyCtx& k, int r, uint64_t x) {
+  uint64_t m[2] = {x, (uint64_t)r};
+  return siphash24_blocks(k.pk0, k.pk1, m, 2, 0, 16);
+}
+
+// id = PRP(slot | TAG<<32, ctr); bytes [0:8) = L, [8:16) = R little-endian
+__host__ __device__ inline void id_encode(const KeyCtx& k, uint32_t slot, uint64_t ctr,
+                                          uint64_t& L, uint64_t& R) {
+  L = (uint64_t)slot | ((uint64_t)kIdTag << 32);
+  R = ctr;
+  for (int r = 0; r < 4; ++r) {
+    uint64_t nl = R, nr = L ^ feistel_f(k, r, R);
+    L = nl;
+    R = nr;
+  }
+}
+
+// returns the slot, or kNone when the id does not decode to a valid slot
+__host__ __device__ inline uint32_t id_decode(const KeyCtx& k, uint64_t L, uint64_t R,
+                                              uint64_t n_slots) {
+  for (int r = 3; r >= 0; --r) {
+    uint64_t nl = R ^ feistel_f(k, r, L), nr = L;
+    L = nl;
+    R = nr;
+  }
+  if ((uint32_t)(L >> 32) != kIdTag) return kNone;
+  if ((uint64_t)(uint32_t)L >= n_slots) return kNone;
+  return (uint32_t)L;
+}
+
+// recipient PRF over the 32-byte key given as 4 little-endian words
+__host__ __device__ inline void recipient_hash(const KeyCtx& k, const uint64_t x[4],
+                                               uint64_t& hi, uint64_t& lo) {
+  hi = siphash24_blocks(k.hk0, k.hk1, x, 4, 1, 33);
+  lo = siphash24_blocks(k.hk0, k.hk1, x, 4, 2, 33);
+}
+
+// S1 (mailbox) sort key: hi = h_hi; lo = h_lo[63:23] | class<<21 | seq<<1 | sub
+__host__ __device__ inline uint64_t s1_lo(uint64_t h_lo, uint32_t cls, uint32_t seq,
+                                          uint32_t sub) {
+  return (h_lo & ~((1ull << 23) - 1)) | ((uint64_t)cls << 21) | ((uint64_t)seq << 1) |
+         (uint64_t)sub;
+}
+__host__ __device__ inline uint64_t s1_group(uint64_t lo) { return lo >> 23; }
+__host__ __device__ inline uint32_t s1_class(uint64_t lo) { return (uint32_t)(lo >> 21) & 3u; }
+__host__ __device__ inline uint32_t s1_seq(uint64_t lo) { return (uint32_t)(lo >> 1) & kSeqMask; }
+__host__ __device__ inline uint32_t s1_sub(uint64_t lo) { return (uint32_t)lo & 1u; }
+
+// R-pass sort key: slot' (partition-major row) << 22 | class << 20 | seq
+constexpr uint64_t kRNullRow = (1ull << 42) - 1;
+__host__ __device__ inline uint64_t r_key(uint64_t row, uint32_t cls, uint32_t seq) {
+  return (row << 22) | ((uint64_t)cls << 20) | (uint64_t)seq;
+}
+
+// ------------------------------------------------------------- wave helpers
+
+__device__ inline uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ inline uint32_t mbcnt64(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ inline uint4 shfl4(uint4 v, int src) {
+  uint4 r;
+  r.x = __shfl(v.x, src);
+  r.y = __shfl(v.y, src);
+  r.z = __shfl(v.z, src);
+  r.w = __shfl(v.w, src);
+  return r;
+}
+
+__device__ inline bool eq4(uint4 a, uint4 b) {
+  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+__device__ inline bool nz4(uint4 a) { return (a.x | a.y | a.z | a.w) != 0u; }
+
+__device__ inline uint64_t u4lo(uint4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
+__device__ inline uint64_t u4hi(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
+
+}  // namespace gvs

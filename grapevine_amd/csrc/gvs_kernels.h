@@ -1,0 +1,1045 @@
+// gvs_kernels.h — gfx950 HIP kernels of the batched oblivious store pipeline.
+//
+// Per batch (DESIGN.md §3 has the full pipeline and the obliviousness rules):
+//   k_copy      request AoS (ABI layout) -> 1 KiB request images + type array
+//   k_meta      classify, recipient PRF, id decode, mailbox sort keys, histogram
+//   sort128     LDS-staged bitonic sort of the mailbox keys (S1)
+//   k_m1        mailbox read pass: resolve next-message ops, create admission
+//   k_alloc_a   seq-order scan: pops, mailbox-ok creates, free-ring appends
+//   k_alloc_b   capacity cutoff, slot allocation, id PRP, message-pass keys
+//   sort64      bitonic sort of the message-pass keys
+//   k_rpass     message table pass: stream every row, cmov-apply ops, emit responses
+//   k_post      seq-order scan: by-id deletes -> free ring, scalar commit
+//   k_m2        mailbox write pass: pops, appends, removals, new mailboxes
+//
+// Rule used by every kernel: each table row is read and written exactly once
+// per pass, and each op's per-kernel reads/writes have a fixed size, so launch
+// sequence, grid sizes and HBM byte counts depend only on (N, R, B, n).
+#pragma once
+#include "gvs_device.h"
+
+namespace gvs {
+
+// ------------------------------------------------------------ sort (bitonic)
+
+template <typename K>
+__device__ inline bool key_lt(const K& a, const K& b);
+template <>
+__device__ inline bool key_lt<uint64_t>(const uint64_t& a, const uint64_t& b) {
+  return a < b;
+}
+template <>
+__device__ inline bool key_lt<Key128>(const Key128& a, const Key128& b) {
+  return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo);
+}
+
+// Sorts (full=1) or finishes a merge level k (full=0) inside tiles of L keys.
+template <typename K, int LMAX>
+__global__ __launch_bounds__(1024) void k_bitonic_local(K* data, uint32_t L, uint32_t kmerge,
+                                                        int full) {
+  __shared__ K s[LMAX];
+  const uint32_t base = blockIdx.x * L;
+  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) s[i] = data[base + i];
+  __syncthreads();
+  uint32_t k_begin = full ? 2u : kmerge, k_end = full ? L : kmerge;
+  for (uint32_t k = k_begin; k <= k_end; k <<= 1) {
+    uint32_t j0 = full ? (k >> 1) : (L >> 1);
+    for (uint32_t j = j0; j > 0; j >>= 1) {
+      for (uint32_t p = threadIdx.x; p < (L >> 1); p += blockDim.x) {
+        uint32_t i = ((p / j) * 2u * j) + (p % j);
+        uint32_t pj = i + j;
+        bool asc = (((base + i) & k) == 0u);
+        K a = s[i], b = s[pj];
+        bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+        if (sw) {
+          s[i] = b;
+          s[pj] = a;
+        }
+      }
+      __syncthreads();
+    }
+    if (!full) break;
+  }
+  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) data[base + i] = s[i];
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_bitonic_global(K* data, uint32_t n, uint32_t k,
+                                                        uint32_t j) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (n >> 1)) return;
+  uint32_t i = ((p / j) * 2u * j) + (p % j);
+  uint32_t pj = i + j;
+  bool asc = ((i & k) == 0u);
+  K a = data[i], b = data[pj];
+  bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+  if (sw) {
+    data[i] = b;
+    data[pj] = a;
+  }
+}
+
+// ------------------------------------------------------ single-block scans
+
+// out[i] = sum(in[0..i)), out[n] = total.  One block of 1024 threads.
+__global__ __launch_bounds__(1024) void k_scan_excl(const uint32_t* in, uint32_t* out,
+                                                    uint32_t n) {
+  __shared__ uint32_t s[1024];
+  const uint32_t T = blockDim.x, t = threadIdx.x;
+  const uint32_t per = (n + T - 1) / T;
+  const uint32_t lo = t * per, hi = min(n, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += in[i];
+  s[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < T; off <<= 1) {
+    uint32_t v = t >= off ? s[t - off] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = s[t] - sum;
+  for (uint32_t i = lo; i < hi; ++i) {
+    uint32_t v = in[i];
+    out[i] = run;
+    run += v;
+  }
+  if (t == T - 1) out[n] = s[T - 1];
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint32_t v, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// ------------------------------------------------------------------ k_copy
+
+// One wave per request: 64 x 16 B of image + the type word.  Rows >= n are
+// padding (zero image, type 0).
+__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint32_t n,
+                                              uint32_t B, uint4* __restrict__ img,
+                                              uint32_t* __restrict__ types) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = lane_id();
+  if (i >= B) return;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (i < n) v = in[(uint64_t)i * 65 + lane];
+  img[(uint64_t)i * 64 + lane] = v;
+  if (lane == 0) {
+    uint32_t t = 0;
+    if (i < n) t = in[(uint64_t)i * 65 + 64].x;
+    types[i] = t;
+  }
+}
+
+// ------------------------------------------------------------------ k_meta
+
+struct MetaArgs {
+  const uint4* img;
+  const uint32_t* types;
+  OpState* ops;
+  uint32_t* kinds;
+  Key128* s1keys;
+  uint32_t* qcount;  // Q+1 counters
+  uint32_t n, B, Q, logQ;
+  uint64_t N;
+  KeyCtx kc;
+};
+
+__global__ __launch_bounds__(256) void k_meta(MetaArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.B) return;
+  const uint4* row = a.img + (uint64_t)i * 64;
+  uint4 c0 = row[0], c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4], c5 = row[5];
+  const uint32_t type = a.types[i];
+  OpState o;
+  o.id[0] = c0.x; o.id[1] = c0.y; o.id[2] = c0.z; o.id[3] = c0.w;
+  o.ts = u4lo(c5);
+  o.slot = kNone;
+  o.h_hi = 0;
+  o.h_lo = 0;
+  o.pad[0] = o.pad[1] = 0;
+  const bool id_zero = !nz4(c0);
+  const bool auth_zero = !nz4(c1) && !nz4(c2);
+  const bool rcpt_zero = !nz4(c3) && !nz4(c4);
+  uint32_t kind, pre = kPending, cls = 3, sub = 0;
+  uint64_t x[4] = {0, 0, 0, 0};
+  if (i >= a.n) {
+    kind = KIND_PAD;
+    pre = 0;
+  } else if (type < 1u || type > 4u || auth_zero || (type == 3u && id_zero)) {
+    kind = KIND_HARD;  // grapevine.proto:57-64, :95 fail-fast
+    pre = 0;
+  } else if (type == 1u) {
+    kind = KIND_CREATE;
+    if (rcpt_zero) {
+      pre = 4;  // INVALID_RECIPIENT, grapevine.proto:72
+    } else {
+      cls = 1;
+      x[0] = u4lo(c3); x[1] = u4hi(c3); x[2] = u4lo(c4); x[3] = u4hi(c4);
+    }
+  } else if ((type == 2u || type == 4u) && id_zero) {
+    kind = type == 2u ? KIND_NEXT_READ : KIND_NEXT_DEL;
+    cls = 0;
+    sub = type == 4u ? 1u : 0u;
+    x[0] = u4lo(c1); x[1] = u4hi(c1); x[2] = u4lo(c2); x[3] = u4hi(c2);
+  } else {
+    kind = type == 2u ? KIND_READ : (type == 3u ? KIND_UPDATE : KIND_DELETE);
+    uint32_t s = id_decode(a.kc, u4lo(c0), u4hi(c0), a.N);
+    o.slot = s;
+    if (s == kNone) pre = 2;  // NOT_FOUND: the id names no slot
+    else if (kind == KIND_DELETE && !rcpt_zero) {
+      cls = 2;
+      x[0] = u4lo(c3); x[1] = u4hi(c3); x[2] = u4lo(c4); x[3] = u4hi(c4);
+    }
+  }
+  Key128 key;
+  uint32_t q = a.Q;
+  if (cls < 3) {
+    uint64_t hi, lo;
+    recipient_hash(a.kc, x, hi, lo);
+    o.h_hi = hi;
+    o.h_lo = lo;
+    q = a.logQ ? (uint32_t)(hi >> (64 - a.logQ)) : 0u;
+    key.hi = hi;
+    key.lo = s1_lo(lo, cls, i, sub);
+  } else {
+    key.hi = ~0ull;
+    key.lo = (~0ull << 21) | ((uint64_t)i << 1);
+  }
+  o.kind = kind;
+  o.pre_status = pre;
+  o.q = q;
+  a.ops[i] = o;
+  a.kinds[i] = kind;
+  a.s1keys[i] = key;
+  atomicAdd(&a.qcount[q], 1u);
+}
+
+// ------------------------------------------------------ mailbox passes M1/M2
+
+struct GroupL {  // 64 B LDS descriptor of one recipient group
+  uint64_t hi, glo;
+  uint32_t first, n_next, n_del, n_create;
+  uint32_t n_x, fcs, len, flags;
+  int32_t slot;
+  uint32_t n_succ, n_delok, fl;
+};
+
+struct MArgs {
+  const Key128* keys;
+  const uint32_t* qstart;  // Q+2 entries
+  uint4* mbox;             // R rows x 64 uint4
+  uint4* side;             // R entries
+  M1Out* m1out;
+  uint32_t* cflag;
+  uint32_t* m1slot;
+  const ROp* rop;          // M2
+  const uint32_t* fstatus; // M2
+  Scal* scal;
+  uint32_t Q, Sr, B, dummy_blocks;
+  uint64_t N;
+  KeyCtx kc;
+};
+
+// Phase A shared by M1 and M2: discover groups of the sorted key range
+// [start, end) of this partition into LDS.  Returns the group count, or
+// kGroupMax+1 on overflow.
+template <bool kM2>
+__device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end,
+                                    GroupL* g, uint32_t* s_w, uint32_t* s_ng) {
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  if (tid == 0) *s_ng = 0;
+  __syncthreads();
+  for (uint32_t base = start; base < end; base += 256) {
+    const uint32_t i = base + tid;
+    const bool valid = i < end;
+    Key128 key = {~0ull, ~0ull}, prev = {~0ull, ~0ull};
+    uint32_t fst = 0;
+    if (valid) {
+      key = a.keys[i];
+      if (i > 0) prev = a.keys[i - 1];
+      if (kM2) fst = a.fstatus[s1_seq(key.lo)];
+    }
+    const bool head = valid && (i == start || key.hi != prev.hi ||
+                                s1_group(key.lo) != s1_group(prev.lo));
+    const uint64_t bm = __ballot(head);
+    const uint32_t pre = mbcnt64(bm);
+    if (lane == 0) s_w[wave] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+      woff += w < wave ? s_w[w] : 0u;
+      tot += s_w[w];
+    }
+    const uint32_t ng0 = *s_ng;
+    const uint32_t incl = ng0 + woff + pre + (head ? 1u : 0u);
+    if (head && incl - 1 < (uint32_t)kGroupMax) {
+      GroupL& G = g[incl - 1];
+      G.hi = key.hi;
+      G.glo = s1_group(key.lo);
+      G.first = i;
+      G.n_next = G.n_del = G.n_create = G.n_x = 0;
+      G.fcs = 0xFFFFFFFFu;
+      G.len = 0;
+      G.flags = 0;
+      G.slot = -1;
+      G.n_succ = G.n_delok = G.fl = 0;
+    }
+    __syncthreads();
+    if (valid && incl >= 1 && incl - 1 < (uint32_t)kGroupMax) {
+      GroupL& G = g[incl - 1];
+      const uint32_t cls = s1_class(key.lo), seq = s1_seq(key.lo);
+      if (cls == 0) {
+        atomicAdd(&G.n_next, 1u);
+        if (s1_sub(key.lo)) atomicAdd(&G.n_del, 1u);
+      } else if (cls == 1) {
+        atomicAdd(&G.n_create, 1u);
+        atomicMin(&G.fcs, seq);
+        if (kM2 && fst == 1u) atomicAdd(&G.n_succ, 1u);
+      } else {
+        atomicAdd(&G.n_x, 1u);
+        if (kM2 && fst == 1u) atomicAdd(&G.n_delok, 1u);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) *s_ng = ng0 + tot;
+    __syncthreads();
+  }
+  uint32_t ng = *s_ng;
+  return ng > (uint32_t)kGroupMax ? (uint32_t)kGroupMax + 1 : ng;
+}
+
+__device__ inline int find_group(const GroupL* g, uint32_t ng, uint64_t hi, uint64_t glo) {
+  int lo = 0, hi_i = (int)ng - 1;
+  while (lo <= hi_i) {
+    int mid = (lo + hi_i) >> 1;
+    const GroupL& G = g[mid];
+    if (G.hi == hi && G.glo == glo) return mid;
+    bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
+    if (less) lo = mid + 1;
+    else hi_i = mid - 1;
+  }
+  return -1;
+}
+
+// Phase B shared: map occupied mailbox rows of the partition to groups.
+__device__ inline void side_prepass(const MArgs& a, uint32_t q, GroupL* g, uint32_t ng,
+                                    int16_t* s_sg, uint32_t* s_occ) {
+  for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
+    uint4 sd = a.side[(uint64_t)q * a.Sr + j];
+    uint64_t hi = u4lo(sd), w1 = u4hi(sd);
+    int16_t sg = -1;
+    if (w1 & 1u) {
+      atomicAdd(s_occ, 1u);
+      int k = find_group(g, ng, hi, w1 >> 23);
+      if (k >= 0) {
+        g[k].slot = (int32_t)j;
+        g[k].len = (uint32_t)(w1 >> 1) & 63u;
+        sg = (int16_t)k;
+      }
+    }
+    s_sg[j] = sg;
+  }
+}
+
+__device__ inline void m1_write(const MArgs& a, uint32_t seq, uint32_t status, uint32_t slot,
+                                uint32_t flags, uint4 id) {
+  M1Out o;
+  o.status = status;
+  o.slot = slot;
+  o.flags = flags;
+  o.pad = 0;
+  o.id[0] = id.x; o.id[1] = id.y; o.id[2] = id.z; o.id[3] = id.w;
+  a.m1out[seq] = o;
+  a.cflag[seq] = flags;
+  a.m1slot[seq] = slot;
+}
+
+// Resolve the next-message ops (class 0) of group G against its mailbox row v
+// (lane 2+k holds id k): the op that has d delete-nexts before it reads id d.
+__device__ void m1_resolve_next(const MArgs& a, const GroupL& G, uint4 v) {
+  const uint32_t lane = lane_id();
+  const uint32_t len = G.len;
+  uint32_t carry = 0;
+  for (uint32_t c = 0; c < G.n_next; c += 64) {
+    const bool valid = c + lane < G.n_next;
+    Key128 key = {0, 0};
+    if (valid) key = a.keys[G.first + c + lane];
+    const uint32_t seq = s1_seq(key.lo), sub = s1_sub(key.lo);
+    const uint64_t dm = __ballot(valid && sub);
+    const uint32_t d = carry + mbcnt64(dm);
+    carry += (uint32_t)__popcll(dm);
+    const uint4 id = shfl4(v, 2 + (int)min(d, 61u));
+    if (valid) {
+      if (d < len) {
+        uint32_t slot = id_decode(a.kc, u4lo(id), u4hi(id), a.N);
+        m1_write(a, seq, kPending, slot, sub ? CF_POP : 0u, id);
+      } else {
+        m1_write(a, seq, 2u, kNone, 0u, make_uint4(0, 0, 0, 0));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_m1(MArgs a) {
+  __shared__ GroupL g[kGroupMax];
+  __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t q = blockIdx.x;
+  if (q >= a.Q) {
+    // dummy partition: ops that touch no mailbox; same per-op reads/writes
+    const uint32_t start = a.qstart[a.Q], end = a.qstart[a.Q + 1];
+    const uint32_t nb = a.dummy_blocks, b = q - a.Q;
+    const uint32_t len = end - start, per = (len + nb - 1) / nb;
+    const uint32_t lo = start + b * per, hi = min(end, lo + per);
+    for (uint32_t i = lo + tid; i < hi; i += 256) {
+      Key128 key = a.keys[i];
+      if (i > 0) (void)a.keys[i - 1];
+      m1_write(a, s1_seq(key.lo), kPending, kNone, 0u, make_uint4(0, 0, 0, 0));
+    }
+    return;
+  }
+  const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
+  const uint32_t ng = discover_groups<false>(a, start, end, g, s_w, &s_ng);
+  if (ng > (uint32_t)kGroupMax) {
+    if (tid == 0) atomicOr(&a.scal->error, 1u);
+    return;
+  }
+  if (tid == 0) {
+    s_occ = 0;
+    s_empt = 0;
+  }
+  __syncthreads();
+  side_prepass(a, q, g, ng, s_sg, &s_occ);
+  __syncthreads();
+
+  // Phase C: stream every mailbox row of the partition (read-only pass).
+  const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = s_sg[j0 + u];
+      if (k >= 0) m1_resolve_next(a, g[k], v[u]);
+    }
+  }
+  __syncthreads();
+
+  // Phase D: free rows after pops, admission of new recipients by the seq of
+  // their first create (grapevine.proto:74 TOO_MANY_RECIPIENTS).
+  for (uint32_t k = tid; k < ng; k += 256) {
+    const GroupL& G = g[k];
+    if (G.slot >= 0 && G.len == min(G.n_del, G.len)) atomicAdd(&s_empt, 1u);
+  }
+  __syncthreads();
+  const uint32_t freeq = (a.Sr - s_occ) + s_empt;
+  for (uint32_t k = tid; k < ng; k += 256) {
+    GroupL& G = g[k];
+    const uint32_t len1 = G.slot >= 0 ? G.len - min(G.n_del, G.len) : 0u;
+    const bool exists1 = len1 > 0;
+    const bool isnew = !exists1 && G.n_create > 0;
+    uint32_t rank = 0;
+    if (isnew) {
+      for (uint32_t k2 = 0; k2 < ng; ++k2) {
+        const GroupL& H = g[k2];
+        const uint32_t hl = H.slot >= 0 ? H.len - min(H.n_del, H.len) : 0u;
+        if (hl == 0 && H.n_create > 0 && H.fcs < G.fcs) ++rank;
+      }
+    }
+    G.fl = len1;
+    G.flags = (exists1 ? 1u : 0u) | ((isnew && rank < freeq) ? 2u : 0u);
+  }
+  __syncthreads();
+
+  // Phase E: creates get their mailbox verdict; every remaining op is visited once.
+  for (uint32_t k = wave; k < ng; k += 4) {
+    const GroupL& G = g[k];
+    if (G.slot < 0) {
+      for (uint32_t c = lane; c < G.n_next; c += 64) {
+        Key128 key = a.keys[G.first + c];
+        m1_write(a, s1_seq(key.lo), 2u, kNone, 0u, make_uint4(0, 0, 0, 0));
+      }
+    }
+    const bool exists1 = G.flags & 1u, admitted = G.flags & 2u;
+    for (uint32_t r = lane; r < G.n_create; r += 64) {
+      Key128 key = a.keys[G.first + G.n_next + r];
+      const bool ok = exists1 ? (G.fl + r < GVS_MAILBOX_SLOTS) : (admitted && r < GVS_MAILBOX_SLOTS);
+      const uint32_t st = ok ? kPending : ((exists1 || admitted) ? 5u : 6u);
+      m1_write(a, s1_seq(key.lo), st, kNone, ok ? CF_MBOX_OK : 0u, make_uint4(0, 0, 0, 0));
+    }
+    for (uint32_t r = lane; r < G.n_x; r += 64) {
+      Key128 key = a.keys[G.first + G.n_next + G.n_create + r];
+      m1_write(a, s1_seq(key.lo), kPending, kNone, 0u, make_uint4(0, 0, 0, 0));
+    }
+  }
+}
+
+// ---------------------------------------------------------- allocation scans
+
+struct AllocArgs {
+  const uint32_t* kinds;
+  const uint32_t* cflag;
+  const uint32_t* m1slot;
+  uint32_t* pfx_pop;   // B: exclusive prefix of pops
+  uint32_t* pfx_s;     // B: exclusive prefix of mailbox-ok creates
+  uint32_t* ring;
+  Scal* scal;
+  uint32_t B;
+  uint64_t N, ring_size;
+};
+
+// One block of 1024 threads: two flag scans in seq order and the free-ring
+// window write for delete-next pops (a permutation of [tail, tail+B)).
+__global__ __launch_bounds__(1024) void k_alloc_a(AllocArgs a) {
+  __shared__ uint32_t s_w[2][16];
+  __shared__ uint32_t s_carry[2];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  if (a.scal->error) return;
+  if (tid == 0) {
+    s_carry[0] = 0;
+    s_carry[1] = 0;
+  }
+  __syncthreads();
+  for (uint32_t base = 0; base < a.B; base += 1024) {
+    const uint32_t i = base + tid;
+    const uint32_t cf = a.cflag[i];
+    const bool pop = cf & CF_POP;
+    const bool s = (cf & CF_MBOX_OK) && a.kinds[i] == KIND_CREATE;
+    const uint64_t mp = __ballot(pop), ms = __ballot(s);
+    if (lane == 0) {
+      s_w[0][wave] = (uint32_t)__popcll(mp);
+      s_w[1][wave] = (uint32_t)__popcll(ms);
+    }
+    __syncthreads();
+    uint32_t op = 0, os = 0, tp = 0, ts = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      op += w < wave ? s_w[0][w] : 0u;
+      os += w < wave ? s_w[1][w] : 0u;
+      tp += s_w[0][w];
+      ts += s_w[1][w];
+    }
+    a.pfx_pop[i] = s_carry[0] + op + mbcnt64(mp);
+    a.pfx_s[i] = s_carry[1] + os + mbcnt64(ms);
+    __syncthreads();
+    if (tid == 0) {
+      s_carry[0] += tp;
+      s_carry[1] += ts;
+    }
+    __syncthreads();
+  }
+  const uint32_t pops = s_carry[0], scnt = s_carry[1];
+  const uint64_t tail = a.scal->tail;
+  for (uint32_t i = tid; i < a.B; i += 1024) {
+    const uint32_t P = a.pfx_pop[i];
+    const bool pop = a.cflag[i] & CF_POP;
+    const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
+    const uint32_t val = pop ? a.m1slot[i] : kNone;
+    a.ring[(tail + pos) % a.ring_size] = val;
+  }
+  if (tid == 0) {
+    Scal* s = a.scal;
+    s->pops = pops;
+    s->scnt = scnt;
+    s->count1 = s->count - pops;
+    const uint64_t room = a.N - s->count1;
+    s->m = scnt < room ? scnt : room;
+    s->head0 = s->head;
+    s->tail0 = tail;
+  }
+}
+
+struct AllocBArgs {
+  const uint4* img;
+  const OpState* ops;
+  const uint32_t* kinds;
+  const uint32_t* cflag;
+  const M1Out* m1out;
+  const uint32_t* pfx_s;
+  const uint32_t* ring;
+  ROp* rop;
+  uint64_t* rkeys;
+  uint32_t* tcount;  // NT+1 tile counters
+  const Scal* scal;
+  uint32_t B, W, S, NT;
+  uint64_t N, ring_size;
+  KeyCtx kc;
+};
+
+// Per op: capacity cutoff (TOO_MANY_MESSAGES before the mailbox checks), slot
+// allocation from the free ring, id PRP, and the message-pass routing key.
+__global__ __launch_bounds__(256) void k_alloc_b(AllocBArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.B) return;
+  if (a.scal->error) return;
+  const uint32_t kind = a.kinds[i];
+  const OpState os = a.ops[i];
+  const M1Out m1 = a.m1out[i];
+  const uint32_t cf = a.cflag[i];
+  const uint32_t S_i = a.pfx_s[i];
+  const uint4* row = a.img + (uint64_t)i * 64;
+  const uint4 c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4];
+  const uint64_t count1 = a.scal->count1, m = a.scal->m, head0 = a.scal->head0;
+  const uint64_t ctr0 = a.scal->ctr;
+
+  ROp r;
+  r.kind = kind;
+  r.flags = 0;
+  r.status = os.pre_status;
+  r.slot = kNone;
+  r.id[0] = os.id[0]; r.id[1] = os.id[1]; r.id[2] = os.id[2]; r.id[3] = os.id[3];
+  uint4 xa = c3, xb = c4;  // recipient
+  uint32_t cls = 3;
+
+  const bool s = (cf & CF_MBOX_OK) && kind == KIND_CREATE;
+  const uint64_t succ_before = S_i < m ? S_i : m;
+  bool success = false;
+  if (kind == KIND_CREATE && os.pre_status == kPending) {
+    if (count1 + S_i >= a.N) r.status = 7;  // TOO_MANY_MESSAGES
+    else if (!s) r.status = m1.status;      // 5 or 6 from the mailbox pass
+    else success = true;
+  }
+  // free-ring gather: successes read [head0, head0+m), others the rest of the window
+  const uint64_t rpos = success ? (uint64_t)S_i : m + (i - succ_before);
+  const uint32_t ring_slot = a.ring[(head0 + rpos) % a.ring_size];
+  if (success) {
+    uint64_t L, R;
+    id_encode(a.kc, ring_slot, ctr0 + S_i, L, R);
+    r.slot = ring_slot;
+    r.status = kPending;
+    r.id[0] = (uint32_t)L; r.id[1] = (uint32_t)(L >> 32);
+    r.id[2] = (uint32_t)R; r.id[3] = (uint32_t)(R >> 32);
+    cls = 1;
+  } else if (kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL) {
+    xa = c1;
+    xb = c2;  // auth identity
+    r.status = m1.status;
+    if (m1.status == kPending) {
+      r.slot = m1.slot;
+      r.id[0] = m1.id[0]; r.id[1] = m1.id[1]; r.id[2] = m1.id[2]; r.id[3] = m1.id[3];
+      cls = 0;
+    }
+  } else if (kind == KIND_READ || kind == KIND_UPDATE || kind == KIND_DELETE) {
+    r.slot = os.slot;
+    if (os.slot != kNone) cls = 2;
+  }
+  r.x[0] = xa.x; r.x[1] = xa.y; r.x[2] = xa.z; r.x[3] = xa.w;
+  r.x[4] = xb.x; r.x[5] = xb.y; r.x[6] = xb.z; r.x[7] = xb.w;
+  a.rop[i] = r;
+  uint64_t rowp = kRNullRow;
+  uint32_t tile = a.NT;
+  if (cls < 3) {
+    const uint32_t sl = r.slot;
+    rowp = (uint64_t)(sl % a.W) * a.S + sl / a.W;
+    tile = (uint32_t)(rowp / kTile);
+  } else {
+    cls = 0;
+  }
+  a.rkeys[i] = r_key(rowp, cls, i);
+  atomicAdd(&a.tcount[tile], 1u);
+}
+
+// ---------------------------------------------------------------- R pass
+
+struct RArgs {
+  uint4* table;             // N rows x 64 uint4, partition-major
+  const uint64_t* rkeys;    // sorted
+  const uint32_t* tstart;   // NT+2
+  const ROp* rop;
+  const uint4* img;
+  uint4* out;               // user responses (65 uint4 each) for seq < n
+  uint4* out_scratch;       // responses for padding rows seq >= n
+  uint32_t* fstatus;
+  const Scal* scal;
+  uint32_t n, B, W, S, NT, null_blocks;
+};
+
+__device__ inline void write_response(const RArgs& a, uint32_t seq, uint4 rec, uint32_t status) {
+  const uint32_t lane = lane_id();
+  uint4* dst = seq < a.n ? a.out + (uint64_t)seq * 65 : a.out_scratch + (uint64_t)(seq - a.n) * 65;
+  dst[lane] = rec;
+  if (lane == 0) {
+    dst[64] = make_uint4(status, 0, 0, 0);
+    a.fstatus[seq] = status;
+  }
+}
+
+// failure record: all zero but the request's server timestamp (lane 5 low 8 B)
+__device__ inline uint4 fail_record(uint4 q, uint32_t status) {
+  const uint32_t lane = lane_id();
+  const uint4 ts = shfl4(q, 5);
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (lane == 5 && status != 0u) {
+    r.x = ts.x;
+    r.y = ts.y;
+  }
+  return r;
+}
+
+// Apply the ops routed to one row, in (class, seq) order, to the row held in v
+// (16 B per lane).  Wave-uniform control flow; data moves by lane-wise select.
+__device__ void r_apply(const RArgs& a, uint4& v, uint32_t first, uint32_t cnt) {
+  const uint32_t lane = lane_id();
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint64_t key = a.rkeys[first + k];
+    const uint32_t seq = (uint32_t)key & kSeqMask;
+    const ROp r = a.rop[seq];
+    const uint4 q = a.img[(uint64_t)seq * 64 + lane];
+    const uint32_t kind = __builtin_amdgcn_readfirstlane(r.kind);
+    const uint4 vr = shfl4(v, (int)lane + 2);  // lanes 1,2 see the row's recipient
+    const uint64_t m_eq = __ballot(eq4(q, v));
+    const uint64_t m_eqr = __ballot(eq4(q, vr));
+    const bool exists = (__ballot(nz4(v)) & 1ull) != 0;
+    const uint4 rid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    const bool rid_match = (__ballot(lane == 0 && eq4(v, rid)) & 1ull) != 0;
+    const bool id_match = (m_eq & 1ull) != 0;
+    const bool auth_ok = ((m_eq & 6ull) == 6ull) || ((m_eqr & 6ull) == 6ull);
+    const bool rcpt_ok = (m_eq & 0x18ull) == 0x18ull;
+    uint32_t status;
+    uint4 resp = v;
+    if (kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL) {
+      status = (exists && rid_match) ? 1u : 8u;  // resolved by M1; mismatch = internal error
+      if (status == 1u && kind == KIND_NEXT_DEL) v = make_uint4(0, 0, 0, 0);
+    } else if (kind == KIND_CREATE) {
+      status = exists ? 8u : 1u;  // the allocator only hands out free rows
+      if (status == 1u) {
+        v = lane == 0 ? rid : q;  // sender = auth, recipient, ts, payload from the image
+        resp = v;
+      }
+    } else {
+      const bool found = exists && id_match && auth_ok;
+      if (!found) status = 2u;                               // NOT_FOUND
+      else if (kind != KIND_READ && !rcpt_ok) status = 4u;   // INVALID_RECIPIENT
+      else status = 1u;
+      if (status == 1u && kind == KIND_UPDATE) {
+        if (lane >= 5) v = q;  // timestamp (lane 5 low half) + payload
+        resp = v;
+      } else if (status == 1u && kind == KIND_DELETE) {
+        v = make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (status != 1u) resp = fail_record(q, status);
+    write_response(a, seq, resp, status);
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_rpass(RArgs a) {
+  __shared__ uint32_t s_first[kTile], s_cnt[kTile];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t w = blockIdx.x;
+  if (a.scal->error) return;
+  if (w >= a.W) {
+    // ops that touch no row: write their (failure) responses
+    const uint32_t start = a.tstart[a.NT], end = a.B;
+    const uint32_t nb = a.null_blocks, b = w - a.W;
+    const uint32_t len = end - start, per = (len + nb - 1) / nb;
+    const uint32_t lo = start + b * per, hi = min(end, lo + per);
+    for (uint32_t i = lo + wave; i < hi; i += 4) {
+      const uint32_t seq = (uint32_t)a.rkeys[i] & kSeqMask;
+      const uint32_t st = __builtin_amdgcn_readfirstlane(a.rop[seq].status);
+      const uint4 q = a.img[(uint64_t)seq * 64 + lane];
+      write_response(a, seq, fail_record(q, st), st);
+    }
+    return;
+  }
+  uint4* part = a.table + (uint64_t)w * a.S * 64;
+  const uint32_t tiles = a.S / kTile;
+  for (uint32_t t = 0; t < tiles; ++t) {
+    const uint32_t tile = w * tiles + t;
+    const uint32_t lo = a.tstart[tile], hi = a.tstart[tile + 1];
+    s_cnt[tid] = 0;
+    s_first[tid] = 0xFFFFFFFFu;
+    __syncthreads();
+    const uint64_t rowbase = (uint64_t)tile * kTile;
+    for (uint32_t i = lo + tid; i < hi; i += 256) {
+      const uint32_t o = (uint32_t)((a.rkeys[i] >> 22) - rowbase);
+      atomicAdd(&s_cnt[o], 1u);
+      atomicMin(&s_first[o], i);
+    }
+    __syncthreads();
+    const uint32_t rb = t * kTile + wave * 64;
+    for (uint32_t j = 0; j < 64; j += U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = part[(uint64_t)(rb + j + u) * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t o = wave * 64 + j + u;
+        const uint32_t c = s_cnt[o];
+        if (c) r_apply(a, v[u], s_first[o], c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) part[(uint64_t)(rb + j + u) * 64 + lane] = v[u];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ post-R commit
+
+struct PostArgs {
+  const uint32_t* kinds;
+  const uint32_t* fstatus;
+  const ROp* rop;
+  uint32_t* pfx;  // scratch B
+  uint32_t* ring;
+  Scal* scal;
+  uint32_t B;
+  uint64_t ring_size;
+};
+
+// by-id deletes append their slots to the free ring in seq order; commit scalars
+__global__ __launch_bounds__(1024) void k_post(PostArgs a) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_carry;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  if (a.scal->error) return;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < a.B; base += 1024) {
+    const uint32_t i = base + tid;
+    const bool d = a.kinds[i] == KIND_DELETE && a.fstatus[i] == 1u;
+    const uint64_t md = __ballot(d);
+    if (lane == 0) s_w[wave] = (uint32_t)__popcll(md);
+    __syncthreads();
+    uint32_t o = 0, t = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      o += w < wave ? s_w[w] : 0u;
+      t += s_w[w];
+    }
+    a.pfx[i] = s_carry + o + mbcnt64(md);
+    __syncthreads();
+    if (tid == 0) s_carry += t;
+    __syncthreads();
+  }
+  const uint32_t nd = s_carry;
+  const uint64_t tail = a.scal->tail0 + a.scal->pops;
+  for (uint32_t i = tid; i < a.B; i += 1024) {
+    const bool d = a.kinds[i] == KIND_DELETE && a.fstatus[i] == 1u;
+    const uint32_t P = a.pfx[i];
+    const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
+    const uint32_t val = d ? a.rop[i].slot : kNone;
+    a.ring[(tail + pos) % a.ring_size] = val;
+  }
+  if (tid == 0) {
+    Scal* s = a.scal;
+    s->nd = nd;
+    s->count = s->count1 + s->m - nd;
+    s->head = s->head0 + s->m;
+    s->tail = s->tail0 + s->pops + nd;
+    s->ctr += s->m;
+    s->batches += 1;
+  }
+}
+
+// ----------------------------------------------------------------- M2 pass
+
+__device__ inline void m2_visit(const MArgs& a, uint32_t sorted_idx, Key128& key, ROp& r,
+                                uint32_t& st) {
+  key = a.keys[sorted_idx];
+  const uint32_t seq = s1_seq(key.lo);
+  r = a.rop[seq];
+  st = a.fstatus[seq];
+}
+
+// Build the new state of one mailbox row: pop D' ids, append the ids of the
+// successful creates (a prefix of the class-1 members), remove ids of
+// successful by-id deletes, clear the row if it ends empty.
+__device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched) {
+  const uint32_t lane = lane_id();
+  const uint32_t len = matched ? G.len : 0u;
+  const uint32_t dp = min(G.n_del, len);
+  for (uint32_t c = 0; c < G.n_next; c += 64) {  // visit pops (state needs only the count)
+    if (c + lane < G.n_next) {
+      Key128 key; ROp r; uint32_t st;
+      m2_visit(a, G.first + c + lane, key, r, st);
+    }
+  }
+  if (dp) {
+    const uint32_t src = lane + dp;
+    const uint4 s = shfl4(v, (int)min(src, 63u));
+    if (lane >= 2) v = src < 64 ? s : make_uint4(0, 0, 0, 0);
+  }
+  uint32_t cur = len - dp;
+  for (uint32_t c = 0; c < G.n_create; c += 64) {
+    const bool valid = c + lane < G.n_create;
+    Key128 key = {0, 0}; ROp r = {}; uint32_t st = 0;
+    if (valid) m2_visit(a, G.first + G.n_next + c + lane, key, r, st);
+    const uint64_t ms = __ballot(valid && st == 1u);
+    const uint32_t ns = (uint32_t)__popcll(ms);
+    if (!matched && c == 0) {
+      const uint4 x0 = shfl4(make_uint4(r.x[0], r.x[1], r.x[2], r.x[3]), 0);
+      const uint4 x1 = shfl4(make_uint4(r.x[4], r.x[5], r.x[6], r.x[7]), 0);
+      if (lane == 0) v = x0;
+      if (lane == 1) v = x1;
+    }
+    const int rel = (int)lane - 2 - (int)cur;
+    const uint4 nid = shfl4(make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]),
+                            rel < 0 ? 0 : (rel > 63 ? 63 : rel));
+    if (lane >= 2 && rel >= 0 && rel < (int)ns) v = nid;
+    cur += ns;
+  }
+  for (uint32_t c = 0; c < G.n_x; c += 64) {
+    const bool valid = c + lane < G.n_x;
+    Key128 key = {0, 0}; ROp r = {}; uint32_t st = 0;
+    if (valid) m2_visit(a, G.first + G.n_next + G.n_create + c + lane, key, r, st);
+    uint64_t md = __ballot(valid && st == 1u);
+    const uint4 myid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    while (md) {
+      const int b = __builtin_ctzll(md);
+      md &= md - 1;
+      const uint4 did = shfl4(myid, b);
+      const uint64_t hit = __ballot(lane >= 2 && eq4(v, did));
+      if (hit) {
+        const uint32_t p = (uint32_t)__builtin_ctzll(hit);
+        const uint4 nxt = shfl4(v, (int)min(lane + 1, 63u));
+        if (lane >= p) v = lane < 63 ? nxt : make_uint4(0, 0, 0, 0);
+        cur -= 1;
+      }
+    }
+  }
+  if (cur == 0) v = make_uint4(0, 0, 0, 0);
+}
+
+// block-wide exclusive prefix of a per-index flag over [0, n) (n <= 1024),
+// result in out[0..n], out[n] = total.  All 256 threads must call.
+__device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t* out,
+                                       uint32_t* s_w) {
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n; base += 256) {
+    const uint32_t i = base + tid;
+    const bool f = i < n && flag[i];
+    const uint64_t m = __ballot(f);
+    if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+      off += w < wave ? s_w[w] : 0u;
+      tot += s_w[w];
+    }
+    if (i < n) out[i] = (uint16_t)(carry + off + mbcnt64(m));
+    carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) out[n] = (uint16_t)carry;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_m2(MArgs a) {
+  __shared__ GroupL g[kGroupMax];
+  __shared__ int16_t s_sg[kSrMax];
+  __shared__ int16_t s_place[kSrMax];
+  __shared__ uint8_t s_flag[kSrMax];
+  __shared__ uint16_t s_pfx[kSrMax + 1];
+  __shared__ uint16_t s_gpfx[kGroupMax + 1];
+  __shared__ uint8_t s_gflag[kGroupMax];
+  __shared__ int16_t s_pend[kGroupMax];
+  __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t q = blockIdx.x;
+  if (a.scal->error) return;
+  if (q >= a.Q) {
+    const uint32_t start = a.qstart[a.Q], end = a.qstart[a.Q + 1];
+    const uint32_t nb = a.dummy_blocks, b = q - a.Q;
+    const uint32_t len = end - start, per = (len + nb - 1) / nb;
+    const uint32_t lo = start + b * per, hi = min(end, lo + per);
+    for (uint32_t i = lo + tid; i < hi; i += 256) {
+      Key128 key; ROp r; uint32_t st;
+      m2_visit(a, i, key, r, st);
+      if (i > 0) (void)a.keys[i - 1];
+    }
+    return;
+  }
+  const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
+  const uint32_t ng = discover_groups<true>(a, start, end, g, s_w, &s_ng);
+  if (ng > (uint32_t)kGroupMax) return;  // M1 already flagged the batch
+  if (tid == 0) {
+    s_occ = 0;
+    s_delta = 0;
+  }
+  __syncthreads();
+  side_prepass(a, q, g, ng, s_sg, &s_occ);
+  __syncthreads();
+  // final lengths; pending = groups with no row that end non-empty
+  for (uint32_t k = tid; k < ng; k += 256) {
+    GroupL& G = g[k];
+    const uint32_t len = G.slot >= 0 ? G.len : 0u;
+    const uint32_t dp = min(G.n_del, len);
+    G.fl = len - dp + G.n_succ - G.n_delok;
+    s_gflag[k] = (G.slot < 0 && G.fl > 0) ? 1 : 0;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j];
+    const uint4 sd = a.side[(uint64_t)q * a.Sr + j];
+    const bool occ = u4hi(sd) & 1u;
+    s_flag[j] = (!occ || (k >= 0 && g[k].fl == 0)) ? 1 : 0;
+  }
+  __syncthreads();
+  block_flag_scan(s_flag, a.Sr, s_pfx, s_w);
+  block_flag_scan(s_gflag, ng, s_gpfx, s_w);
+  for (uint32_t k = tid; k < ng; k += 256)
+    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t npend = s_gpfx[ng];
+  if (tid == 0 && npend > s_pfx[a.Sr]) atomicOr(&a.scal->error, 2u);
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    int16_t p = -1;
+    if (s_flag[j] && s_pfx[j] < npend) p = s_pend[s_pfx[j]];
+    s_place[j] = p;
+    const int k = s_sg[j];
+    if (k >= 0 && g[k].fl == 0) atomicSub(&s_delta, 1u);
+  }
+  if (tid == 0) atomicAdd(&s_delta, npend);
+  __syncthreads();
+
+  // Phase C: rewrite every row of the partition exactly once.
+  uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j = j0 + u;
+      const int k = s_sg[j], p = s_place[j];
+      uint4 sd = a.side[(uint64_t)q * a.Sr + j];
+      if (k >= 0) m2_apply(a, g[k], v[u], true);
+      if (p >= 0) {  // a new mailbox takes a row that is (or became) empty
+        v[u] = make_uint4(0, 0, 0, 0);
+        m2_apply(a, g[p], v[u], false);
+      }
+      if (k >= 0 || p >= 0) {
+        const GroupL& G = g[p >= 0 ? p : k];
+        if (G.fl > 0) {
+          const uint64_t w1 = (G.glo << 23) | ((uint64_t)G.fl << 1) | 1ull;
+          sd = make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                          (uint32_t)(w1 >> 32));
+        } else {
+          sd = make_uint4(0, 0, 0, 0);
+        }
+      }
+      part[(uint64_t)j * 64 + lane] = v[u];
+      if (lane == 0) a.side[(uint64_t)q * a.Sr + j] = sd;
+    }
+  }
+  // Phase D: members of groups that own no row (misses, failed creates) are visited too.
+  for (uint32_t k = wave; k < ng; k += 4) {
+    const GroupL& G = g[k];
+    if (G.slot >= 0 || s_gflag[k]) continue;
+    const uint32_t cnt = G.n_next + G.n_create + G.n_x;
+    for (uint32_t c = lane; c < cnt; c += 64) {
+      Key128 key; ROp r; uint32_t st;
+      m2_visit(a, G.first + c, key, r, st);
+    }
+  }
+  if (tid == 0 && s_delta) atomicAdd((unsigned long long*)&a.scal->n_mailboxes,
+                                     (unsigned long long)(int64_t)(int32_t)s_delta);
+}
+
+}  // namespace gvs

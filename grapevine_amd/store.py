@@ -1,0 +1,129 @@
+"""Host-side mirror of the store surface over libgvstore.so (ctypes).
+
+`ObliviousStore.process_batch` is the batched form of the enclave handler's
+QueryRequest -> QueryResponse dispatch (types/src/lib.rs:27-120,
+api/proto/grapevine.proto:57-122); `access` is the single-op shim in the shape
+of mc-oblivious-traits' ObliviousHashMap::access_and_insert.
+There is no CPU fallback: if the HIP library or a GPU is missing, construction
+fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import abi
+
+_LIB = None
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgvstore.so")
+
+EXPORTED = (
+    "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
+    "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
+    "gvs_synchronize", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
+)
+
+
+class GvsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gvstore error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path=None):
+    """Load libgvstore.so and declare the C ABI signatures."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or _LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libgvstore.so not built at {p}; run `make` (HIP extension missing)")
+    lib = ctypes.CDLL(p)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    lib.gvs_config_init.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.c_uint64]
+    lib.gvs_create.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.POINTER(vp)]
+    lib.gvs_destroy.argtypes = [vp]
+    lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
+    lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
+    lib.gvs_access.argtypes = [vp, vp, vp]
+    lib.gvs_get_stats.argtypes = [vp, ctypes.POINTER(abi.GvsStats)]
+    lib.gvs_dump_messages.argtypes = [vp, vp, ctypes.c_uint64]
+    lib.gvs_synchronize.argtypes = [vp]
+    lib.gvs_set_timing.argtypes = [vp, i32]
+    lib.gvs_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
+                                     ctypes.POINTER(ctypes.c_float), i32]
+    lib.gvs_last_error.argtypes = [vp]
+    lib.gvs_last_error.restype = ctypes.c_char_p
+    lib.gvs_version.restype = ctypes.c_char_p
+    for name in EXPORTED:
+        if name not in ("gvs_last_error", "gvs_version"):
+            getattr(lib, name).restype = i32
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+class ObliviousStore:
+    """One store on one GPU (one handle; not thread-safe, like `&mut self`)."""
+
+    def __init__(self, config):
+        self.lib = load_library()
+        self.config = config
+        h = ctypes.c_void_p()
+        rc = self.lib.gvs_create(ctypes.byref(config), ctypes.byref(h))
+        if rc != 0:
+            raise GvsError(rc, "gvs_create failed (no GPU, bad config or out of memory)")
+        self.h = h
+        self.B = config.max_batch
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gvs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise GvsError(rc, self.lib.gvs_last_error(self.h).decode())
+
+    def process_batch(self, reqs):
+        """reqs: np.ndarray of abi.REQUEST_DTYPE -> responses (abi.RESPONSE_DTYPE)."""
+        reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+        out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
+        self._check(self.lib.gvs_process_batch(self.h, reqs.ctypes.data, len(reqs), out.ctypes.data))
+        return out
+
+    def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
+        self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))
+
+    def access(self, req):
+        out = self.process_batch(np.asarray([req], dtype=abi.REQUEST_DTYPE) if not isinstance(req, np.ndarray) else req.reshape(1))
+        return out[0]
+
+    def stats(self):
+        s = abi.GvsStats()
+        self._check(self.lib.gvs_get_stats(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in abi.GvsStats._fields_}
+
+    def dump_messages(self):
+        n = self.config.msg_capacity
+        out = np.zeros(n, dtype=abi.RECORD_DTYPE)
+        self._check(self.lib.gvs_dump_messages(self.h, out.ctypes.data, n * 1024))
+        return out
+
+    def synchronize(self):
+        self._check(self.lib.gvs_synchronize(self.h))
+
+    def set_timing(self, on=True):
+        self._check(self.lib.gvs_set_timing(self.h, 1 if on else 0))
+
+    def last_timings(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        c = self.lib.gvs_last_timings(self.h, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(max(c, 0))}

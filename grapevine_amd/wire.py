@@ -1,0 +1,177 @@
+"""Batched constant-size protobuf codec for QueryRequest / QueryResponse.
+
+Encodes/decodes the wire form of api/proto/grapevine.proto:123-176 (prost
+structs types/src/lib.rs:27-120) directly to/from the engine's POD slabs
+(include/gvstore.h), vectorised over a whole batch with numpy.
+
+Every field of these messages has a fixed size (README.md:148: payloads are
+exactly 936 bytes), so a fully populated QueryRequest is 1099 bytes and a
+QueryResponse with nonzero timestamp and status is 1042 bytes: the
+constant-size property pinned by api/tests/grapevine_types.rs:22-31,46-55.
+Messages in that canonical form are handled by slicing; anything else goes
+through a small generic protobuf reader.
+"""
+import numpy as np
+
+from . import abi
+
+REQUEST_WIRE_BYTES = 1099
+RESPONSE_WIRE_BYTES = 1042
+
+# canonical QueryRequest: (offset, tag bytes) of each field header
+_REQ_HDR = [
+    (0, b"\x0d"),                 # 1: request_type fixed32
+    (5, b"\x12\x20"),             # 2: auth_identity, 32 B
+    (39, b"\x1a\x40"),            # 3: auth_signature, 64 B
+    (105, b"\x22\xdf\x07"),       # 4: record (RequestRecord, 991 B)
+    (108, b"\x0a\x10"),           #    1: msg_id, 16 B
+    (126, b"\x12\x20"),           #    2: recipient, 32 B
+    (160, b"\x1a\xa8\x07"),       #    3: payload, 936 B
+]
+_RESP_HDR = [
+    (0, b"\x0a\x8a\x08"),         # 1: record (Record, 1034 B)
+    (3, b"\x0a\x10"),             #    1: msg_id
+    (21, b"\x12\x20"),            #    2: sender
+    (55, b"\x1a\x20"),            #    3: recipient
+    (89, b"\x21"),                #    4: timestamp fixed64
+    (98, b"\x2a\xa8\x07"),        #    5: payload
+    (1037, b"\x15"),              # 2: status_code fixed32
+]
+
+
+def _put_headers(buf, hdrs):
+    for off, tag in hdrs:
+        buf[:, off:off + len(tag)] = np.frombuffer(tag, np.uint8)
+
+
+def encode_responses(resps):
+    """gvs_response slab -> (n, 1042) uint8 wire messages.
+
+    Requires nonzero timestamp and status (what the engine emits for every
+    non-hard-error response); raises otherwise, since proto3 would then omit
+    the field and the message would not be constant-size."""
+    r = np.asarray(resps, dtype=abi.RESPONSE_DTYPE)
+    if (r["record"]["timestamp"] == 0).any() or (r["status_code"] == 0).any():
+        raise ValueError("zero timestamp/status is not constant-size on the wire")
+    n = len(r)
+    out = np.zeros((n, RESPONSE_WIRE_BYTES), np.uint8)
+    _put_headers(out, _RESP_HDR)
+    rec = r["record"]
+    out[:, 5:21] = rec["msg_id"]
+    out[:, 23:55] = rec["sender"]
+    out[:, 57:89] = rec["recipient"]
+    out[:, 90:98] = rec["timestamp"].astype("<u8").view(np.uint8).reshape(n, 8)
+    out[:, 101:1037] = rec["payload"]
+    out[:, 1038:1042] = r["status_code"].astype("<u4").view(np.uint8).reshape(n, 4)
+    return out
+
+
+def encode_requests(reqs, signatures=None):
+    """gvs_request slab (+ optional (n, 64) signatures) -> (n, 1099) wire messages."""
+    q = np.asarray(reqs, dtype=abi.REQUEST_DTYPE)
+    if (q["request_type"] == 0).any():
+        raise ValueError("request_type 0 is not constant-size on the wire")
+    n = len(q)
+    out = np.zeros((n, REQUEST_WIRE_BYTES), np.uint8)
+    _put_headers(out, _REQ_HDR)
+    out[:, 1:5] = q["request_type"].astype("<u4").view(np.uint8).reshape(n, 4)
+    out[:, 7:39] = q["auth_identity"]
+    if signatures is not None:
+        out[:, 41:105] = signatures
+    out[:, 110:126] = q["msg_id"]
+    out[:, 128:160] = q["recipient"]
+    out[:, 163:1099] = q["payload"]
+    return out
+
+
+def _read_varint(b, i):
+    v, s = 0, 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << s
+        s += 7
+        if not c & 0x80:
+            return v, i
+
+
+def _fields(b):
+    i, out = 0, {}
+    while i < len(b):
+        key, i = _read_varint(b, i)
+        f, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _read_varint(b, i)
+        elif wt == 1:
+            v, i = int.from_bytes(b[i:i + 8], "little"), i + 8
+        elif wt == 5:
+            v, i = int.from_bytes(b[i:i + 4], "little"), i + 4
+        elif wt == 2:
+            ln, i = _read_varint(b, i)
+            v, i = bytes(b[i:i + ln]), i + ln
+        else:
+            raise ValueError(f"unsupported wire type {wt}")
+        out[f] = v  # proto3: last one wins
+    return out
+
+
+def _fixed(v, size, name):
+    v = v if v is not None else b""
+    if len(v) != size:
+        raise ValueError(f"{name} must be exactly {size} bytes, got {len(v)}")
+    return np.frombuffer(v, np.uint8)
+
+
+def decode_requests(msgs, timestamps=None):
+    """Wire QueryRequests -> (gvs_request slab, (n, 64) signatures).
+
+    `msgs` is a list of bytes or an (n, 1099) uint8 array; `timestamps` is the
+    server time to stamp on each request (README.md:143-144)."""
+    canon = isinstance(msgs, np.ndarray) and msgs.ndim == 2 and msgs.shape[1] == REQUEST_WIRE_BYTES
+    if canon:
+        for off, tag in _REQ_HDR:
+            if not (msgs[:, off:off + len(tag)] == np.frombuffer(tag, np.uint8)).all():
+                canon = False
+                break
+    if canon:
+        n = len(msgs)
+        q = np.zeros(n, abi.REQUEST_DTYPE)
+        q["request_type"] = msgs[:, 1:5].copy().view("<u4").reshape(n)
+        q["auth_identity"] = msgs[:, 7:39]
+        sig = msgs[:, 41:105].copy()
+        q["msg_id"] = msgs[:, 110:126]
+        q["recipient"] = msgs[:, 128:160]
+        q["payload"] = msgs[:, 163:1099]
+    else:
+        rows = [bytes(m) for m in msgs]
+        n = len(rows)
+        q = np.zeros(n, abi.REQUEST_DTYPE)
+        sig = np.zeros((n, 64), np.uint8)
+        for k, m in enumerate(rows):
+            f = _fields(m)
+            rec = _fields(f.get(4, b""))
+            q[k]["request_type"] = f.get(1, 0)
+            q[k]["auth_identity"] = _fixed(f.get(2), 32, "auth_identity")
+            sig[k] = _fixed(f.get(3), 64, "auth_signature")
+            q[k]["msg_id"] = _fixed(rec.get(1), 16, "msg_id")
+            q[k]["recipient"] = _fixed(rec.get(2), 32, "recipient")
+            q[k]["payload"] = _fixed(rec.get(3), abi.PAYLOAD_BYTES, "payload")
+    if timestamps is not None:
+        q["timestamp"] = timestamps
+    return q, sig
+
+
+def decode_responses(msgs):
+    """Wire QueryResponses -> gvs_response slab (generic reader)."""
+    n = len(msgs)
+    r = np.zeros(n, abi.RESPONSE_DTYPE)
+    for k, m in enumerate(msgs):
+        f = _fields(bytes(m))
+        rec = _fields(f.get(1, b""))
+        r[k]["record"]["msg_id"] = _fixed(rec.get(1), 16, "msg_id")
+        r[k]["record"]["sender"] = _fixed(rec.get(2), 32, "sender")
+        r[k]["record"]["recipient"] = _fixed(rec.get(3), 32, "recipient")
+        r[k]["record"]["timestamp"] = rec.get(4, 0)
+        r[k]["record"]["payload"] = _fixed(rec.get(5), abi.PAYLOAD_BYTES, "payload")
+        r[k]["status_code"] = f.get(2, 0)
+    return r

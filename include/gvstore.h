@@ -1,0 +1,188 @@
+/*
+ * gvstore.h — C ABI of the MI355X-native batched oblivious message store for
+ * grapevine's CRUD path.
+ *
+ * This header is the single drop-in boundary between the (Rust) enclave request
+ * handler and the HIP engine.  Every type is a plain-old-data struct; no torch,
+ * HIP or C++ type appears here.  INTEGRATION.md shows the `extern "C"` Rust
+ * binding (gvstore-sys) a maintainer would add next to the reference's
+ * `types/` crate.
+ *
+ * What each entry point replaces in the reference (all hot-path code is absent
+ * from the reference snapshot; the surface below follows the
+ * types the reference does hold):
+ *
+ *   gvs_process_batch   the enclave handler's per-request dispatch over
+ *                       QueryRequest -> QueryResponse
+ *                       (types/src/lib.rs:27-59 request, :111-120 response,
+ *                        semantics api/proto/grapevine.proto:57-122),
+ *                       batched: B requests in, B responses out, request order.
+ *   gvs_access          ObliviousHashMap::access_and_insert-style single-op
+ *                       shim (mc-oblivious-traits, absent),
+ *                       implemented as a batch of one.
+ *   gvs_create/destroy  construction of the ORAM-backed maps (capacity fixed
+ *                       at creation, README.md:73-80).
+ *
+ * Conventions: return 0 on success, a negative GVS_ERR_* on
+ * API misuse or device failure.  Per-request outcomes are reported only in
+ * gvs_response.status_code.  Nothing unwinds across this boundary.  A handle
+ * is owned by one host thread at a time (the reference traits take &mut self);
+ * calls are synchronous.  The caller owns request/response buffers; the library
+ * owns all device memory.
+ */
+#ifndef GVSTORE_H
+#define GVSTORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants (types/src/lib.rs, README.md) ---------------------------- */
+
+#define GVS_MSG_ID_BYTES 16    /* README.md:134 */
+#define GVS_KEY_BYTES 32       /* ristretto public key, README.md:134,141 */
+#define GVS_PAYLOAD_BYTES 936  /* README.md:134-136, 148 */
+#define GVS_RECORD_BYTES 1024  /* README.md:132-136 */
+#define GVS_MAILBOX_SLOTS 62   /* in-flight messages per recipient, README.md:78-80 */
+
+/* RequestType, types/src/lib.rs:16-22 / api/proto/grapevine.proto:44-55 */
+#define GVS_REQUEST_CREATE 1u
+#define GVS_REQUEST_READ 2u
+#define GVS_REQUEST_UPDATE 3u
+#define GVS_REQUEST_DELETE 4u
+
+/* StatusCode, types/src/lib.rs:122-137 / api/proto/grapevine.proto:178-197.
+ * GVS_STATUS_HARD_ERROR (0, the proto's INVALID_STATUS) marks a request the
+ * proto says must fail at the gRPC level instead of with a status
+ * (grapevine.proto:57-64 fail-fast rules, :95 zero-id UPDATE). */
+#define GVS_STATUS_HARD_ERROR 0u
+#define GVS_STATUS_SUCCESS 1u
+#define GVS_STATUS_NOT_FOUND 2u
+#define GVS_STATUS_MESSAGE_ID_ALREADY_IN_USE 3u
+#define GVS_STATUS_INVALID_RECIPIENT 4u
+#define GVS_STATUS_TOO_MANY_MESSAGES_FOR_RECIPIENT 5u
+#define GVS_STATUS_TOO_MANY_RECIPIENTS 6u
+#define GVS_STATUS_TOO_MANY_MESSAGES 7u
+#define GVS_STATUS_INTERNAL_ERROR 8u
+
+/* return codes */
+#define GVS_OK 0
+#define GVS_ERR_INVALID_ARG (-1)
+#define GVS_ERR_DEVICE (-2)      /* HIP / RCCL failure; see gvs_last_error */
+#define GVS_ERR_OUT_OF_MEMORY (-3)
+#define GVS_ERR_BATCH_OVERFLOW (-4) /* a fixed per-partition bound of the batch
+                                       was exceeded; the batch was not applied */
+#define GVS_ERR_NO_DEVICE (-5)
+#define GVS_ERR_INTERNAL (-6)
+
+/* ---- records ------------------------------------------------------------- */
+
+/* Record, types/src/lib.rs:82-106; byte layout README.md:132-136.  This is
+ * also the exact 1 KiB row stored in HBM. */
+typedef struct gvs_record {
+  uint8_t msg_id[GVS_MSG_ID_BYTES];
+  uint8_t sender[GVS_KEY_BYTES];
+  uint8_t recipient[GVS_KEY_BYTES];
+  uint64_t timestamp;
+  uint8_t payload[GVS_PAYLOAD_BYTES];
+} gvs_record;
+
+/* QueryRequest (types/src/lib.rs:27-59) with its RequestRecord (:63-78),
+ * laid out so that its first 1024 bytes are the Record a CREATE would store:
+ * `sender` is the request's auth_identity.  The 64-byte auth_signature is
+ * verified by the caller before the store is reached (grapevine.proto:57-64,
+ * README.md:187-200) and is not passed in.  `timestamp` is the server time the
+ * caller assigns to this request (README.md:143-144: client timestamps are
+ * ignored); it must be nonzero so responses stay constant-size on the wire
+ * (SURVEY.md §4.1). */
+typedef struct gvs_request {
+  uint8_t msg_id[GVS_MSG_ID_BYTES];        /* RequestRecord.msg_id */
+  uint8_t auth_identity[GVS_KEY_BYTES];    /* QueryRequest.auth_identity */
+  uint8_t recipient[GVS_KEY_BYTES];        /* RequestRecord.recipient */
+  uint64_t timestamp;                      /* server time for this request */
+  uint8_t payload[GVS_PAYLOAD_BYTES];      /* RequestRecord.payload */
+  uint32_t request_type;                   /* QueryRequest.request_type */
+  uint32_t reserved[3];                    /* must be zero */
+} gvs_request;
+
+/* QueryResponse, types/src/lib.rs:111-120. */
+typedef struct gvs_response {
+  gvs_record record;
+  uint32_t status_code;
+  uint32_t reserved[3];
+} gvs_response;
+
+/* ---- configuration ------------------------------------------------------- */
+
+typedef struct gvs_config {
+  uint64_t msg_capacity;        /* N message slots; power of two, >= 256 */
+  uint32_t mailbox_partitions;  /* Q; power of two */
+  uint32_t mailbox_partition_slots; /* S_r mailboxes per partition; R = Q*S_r */
+  uint32_t max_batch;           /* B; power of two, 256 .. 2^20 */
+  uint32_t device;              /* HIP device ordinal */
+  uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key */
+  uint32_t flags;               /* reserved, must be 0 */
+  uint32_t reserved[7];
+} gvs_config;
+
+typedef struct gvs_stats {
+  uint64_t messages;            /* live messages */
+  uint64_t mailboxes;           /* live mailboxes (recipients with messages) */
+  uint64_t batches;             /* batches applied */
+  uint64_t creation_counter;    /* next id generation number */
+  uint64_t free_ring_head;
+  uint64_t free_ring_tail;
+  uint64_t msg_partitions;      /* W: workgroups of the message-table pass */
+  uint64_t msg_partition_slots; /* N / W */
+} gvs_stats;
+
+typedef struct gvs_handle gvs_handle;
+
+/* Fill `cfg` with defaults for capacity N (R = N/16 mailboxes, B = 65536). */
+int gvs_config_init(gvs_config *cfg, uint64_t msg_capacity);
+
+int gvs_create(const gvs_config *cfg, gvs_handle **out);
+int gvs_destroy(gvs_handle *h);
+
+/* Process n <= max_batch requests (host memory) and write n responses in
+ * request order.  Requests of one batch are linearised in the order defined
+ * in DESIGN.md §2 (next-message reads/deletes, then creates, then by-id
+ * operations, each in submission order). */
+int gvs_process_batch(gvs_handle *h, const gvs_request *reqs, uint32_t n,
+                      gvs_response *out);
+
+/* Same, with device-resident buffers (n * sizeof(gvs_request) and
+ * n * sizeof(gvs_response) bytes on the handle's device).  Used by the
+ * benchmark so that the timed region excludes PCIe. */
+int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
+                             void *d_out);
+
+/* Single-request shim in the shape of ObliviousHashMap::access_and_insert. */
+int gvs_access(gvs_handle *h, const gvs_request *req, gvs_response *out);
+
+int gvs_get_stats(gvs_handle *h, gvs_stats *out);
+
+/* Copy the raw message table (N * 1024 bytes) to host memory; test use. */
+int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
+
+/* Wait for all work on the handle's stream. */
+int gvs_synchronize(gvs_handle *h);
+
+/* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */
+int gvs_set_timing(gvs_handle *h, int on);
+
+/* Device timing of the last batch, per pipeline stage, from HIP events on the
+ * handle's stream.  names[i] points at static strings. Returns the count. */
+int gvs_last_timings(gvs_handle *h, const char **names, float *ms, int cap);
+
+const char *gvs_last_error(gvs_handle *h);
+const char *gvs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GVSTORE_H */

@@ -1,0 +1,163 @@
+"""ctypes binding of oracle/libgvs_oracle.so (test infrastructure only)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from grapevine_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class GenParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "pct_create", "pct_read", "pct_update", "pct_delete", "pct_next", "pct_miss",
+        "pct_bad_auth", "pct_bad_recipient", "pct_hard_error", "pct_zero_recipient",
+        "pct_hot", "n_identities")] + [("ts_base", ctypes.c_uint64)]
+
+
+def gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=10, bad_auth=5,
+               bad_recipient=5, hard_error=1, zero_recipient=1, hot=0, n_identities=1000,
+               ts_base=1_700_000_000):
+    return GenParams(create, read, update, delete, nxt, miss, bad_auth, bad_recipient,
+                     hard_error, zero_recipient, hot, n_identities, ts_base)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libgvs_oracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.gvo_siphash24.argtypes = [u64, u64, ctypes.c_char_p, ctypes.c_size_t]
+        L.gvo_siphash24.restype = u64
+        L.gvo_id_encode.argtypes = [ctypes.c_char_p, u32, u64, ctypes.c_char_p]
+        L.gvo_id_decode.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64,
+                                    ctypes.POINTER(u32), ctypes.POINTER(u64)]
+        L.gvo_id_decode.restype = ctypes.c_int
+        L.gvo_recipient_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p,
+                                         ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.gvo_create.argtypes = [ctypes.POINTER(abi.GvsConfig)]
+        L.gvo_create.restype = vp
+        L.gvo_destroy.argtypes = [vp]
+        L.gvo_process_batch.argtypes = [vp, vp, u32, vp]
+        L.gvo_process_batch.restype = ctypes.c_int
+        L.gvo_apply_one.argtypes = [vp, vp, vp]
+        for f in ("gvo_messages", "gvo_mailboxes", "gvo_creation_counter", "gvo_state_digest"):
+            getattr(L, f).argtypes = [vp]
+            getattr(L, f).restype = u64
+        L.gvo_dump_messages.argtypes = [vp, vp, u64]
+        L.gvo_dump_messages.restype = ctypes.c_int
+        L.gvo_live_message.argtypes = [vp, u64, vp]
+        L.gvo_live_message.restype = ctypes.c_int
+        L.gvo_identity.argtypes = [u32, ctypes.c_char_p]
+        L.gvo_gen_batch.argtypes = [vp, ctypes.POINTER(GenParams), ctypes.POINTER(u64), vp, u32, u64]
+        _LIB = L
+    return _LIB
+
+
+def siphash24(key16: bytes, msg: bytes) -> int:
+    k0 = int.from_bytes(key16[:8], "little")
+    k1 = int.from_bytes(key16[8:16], "little")
+    return lib().gvo_siphash24(k0, k1, msg, len(msg))
+
+
+def id_encode(key16: bytes, slot: int, ctr: int) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().gvo_id_encode(key16, slot, ctr, out)
+    return out.raw
+
+
+def id_decode(key16: bytes, msg_id: bytes, n_slots: int):
+    s, c = ctypes.c_uint32(), ctypes.c_uint64()
+    ok = lib().gvo_id_decode(key16, msg_id, n_slots, ctypes.byref(s), ctypes.byref(c))
+    return (s.value, c.value) if ok else None
+
+
+def identity(i: int) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().gvo_identity(i, out)
+    return out.raw
+
+
+class Model:
+    """The sequential semantic model (seqmodel)."""
+
+    def __init__(self, config):
+        self.L = lib()
+        self.config = config
+        self.m = self.L.gvo_create(ctypes.byref(config))
+        if not self.m:
+            raise ValueError("invalid oracle config")
+        self.rng = ctypes.c_uint64(0)
+        self.ops = 0
+
+    def close(self):
+        if self.m:
+            self.L.gvo_destroy(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process_batch(self, reqs):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+        out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
+        rc = self.L.gvo_process_batch(self.m, reqs.ctypes.data, len(reqs), out.ctypes.data)
+        if rc != 0:
+            raise ValueError(f"oracle rejected batch: {rc}")
+        return out
+
+    def apply_one(self, req):
+        r = np.ascontiguousarray(np.asarray(req, dtype=abi.REQUEST_DTYPE).reshape(1))
+        out = np.zeros(1, dtype=abi.RESPONSE_DTYPE)
+        self.L.gvo_apply_one(self.m, r.ctypes.data, out.ctypes.data)
+        return out[0]
+
+    def seed(self, s):
+        self.rng = ctypes.c_uint64(s)
+
+    def gen_batch(self, n, params):
+        reqs = np.zeros(n, dtype=abi.REQUEST_DTYPE)
+        self.L.gvo_gen_batch(self.m, ctypes.byref(params), ctypes.byref(self.rng),
+                             reqs.ctypes.data, n, self.ops)
+        self.ops += n
+        return reqs
+
+    @property
+    def messages(self):
+        return self.L.gvo_messages(self.m)
+
+    @property
+    def mailboxes(self):
+        return self.L.gvo_mailboxes(self.m)
+
+    @property
+    def creation_counter(self):
+        return self.L.gvo_creation_counter(self.m)
+
+    def digest(self):
+        return self.L.gvo_state_digest(self.m)
+
+    def dump_messages(self):
+        n = self.config.msg_capacity
+        out = np.zeros(n, dtype=abi.RECORD_DTYPE)
+        assert self.L.gvo_dump_messages(self.m, out.ctypes.data, n) == 0
+        return out
+
+    def live_message(self, i):
+        rec = np.zeros(1, dtype=abi.RECORD_DTYPE)
+        if self.L.gvo_live_message(self.m, i, rec.ctypes.data) != 0:
+            raise IndexError(i)
+        return rec[0]

@@ -1,0 +1,80 @@
+/*
+ * gvs_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of grapevine's CRUD store semantics ("seqmodel"), used by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * checker.  The product path (libgvstore.so) never links or calls this.
+ *
+ * Parity status: the hot-path code of the reference (mc-oblivious and the
+ * grapevine enclave handler) is absent from /root/reference (SURVEY.md §0,
+ * §8(c)); no store-level golden vectors exist.  Store-level parity is
+ * therefore UNPINNED: this model follows the written spec
+ * (api/proto/grapevine.proto:57-122, README.md:73-175, types/src/lib.rs:13-137)
+ * and the precedence/batching decisions of DESIGN.md §2.  Its primitives are
+ * pinned: SipHash-2-4 against the SipHash paper vectors and CPython's built-in
+ * siphash24 (tests/test_oracle_primitives.py); the wire sizes against the
+ * reference's own constant-size tests (api/tests/grapevine_types.rs:22-55).
+ */
+#ifndef GVS_ORACLE_H
+#define GVS_ORACLE_H
+
+#include "../include/gvstore.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gvo_model gvo_model;
+
+typedef struct gvo_gen_params {
+  uint32_t pct_create, pct_read, pct_update, pct_delete; /* sum to 100 */
+  uint32_t pct_next;          /* % of READ/DELETE sent with a zero msg_id */
+  uint32_t pct_miss;          /* % of by-id ops with a random (absent) id */
+  uint32_t pct_bad_auth;      /* % of by-id ops authenticated by a stranger */
+  uint32_t pct_bad_recipient; /* % of UPDATE/DELETE naming a wrong recipient */
+  uint32_t pct_hard_error;    /* % malformed (zero auth / bad type / zero-id update) */
+  uint32_t pct_zero_recipient;/* % of CREATE with an all-zero recipient */
+  uint32_t pct_hot;           /* % of CREATE/next ops aimed at identity 0 */
+  uint32_t n_identities;      /* size of the identity pool */
+  uint64_t ts_base;           /* timestamps are ts_base + running op index */
+} gvo_gen_params;
+
+/* SipHash-2-4 (Aumasson & Bernstein 2012), 64-bit output. */
+uint64_t gvo_siphash24(uint64_t k0, uint64_t k1, const uint8_t *m, size_t len);
+/* 4-round Feistel PRP over 128 bits used for message ids. */
+void gvo_id_encode(const uint8_t key[16], uint32_t slot, uint64_t ctr,
+                   uint8_t out[16]);
+/* returns 1 if the id decodes to (slot < n_slots, tag ok) */
+int gvo_id_decode(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
+                  uint32_t *slot, uint64_t *ctr);
+void gvo_recipient_hash(const uint8_t key[16], const uint8_t x[32],
+                        uint64_t *h_hi, uint64_t *h_lo);
+
+gvo_model *gvo_create(const gvs_config *cfg);
+void gvo_destroy(gvo_model *m);
+/* Apply a batch in the engine's linearisation order; responses in request order. */
+int gvo_process_batch(gvo_model *m, const gvs_request *reqs, uint32_t n,
+                      gvs_response *out);
+/* The plain sequential handler on one request (no batch reordering). */
+void gvo_apply_one(gvo_model *m, const gvs_request *req, gvs_response *out);
+
+uint64_t gvo_messages(const gvo_model *m);
+/* copy the slot-addressed message table (N records) */
+int gvo_dump_messages(const gvo_model *m, gvs_record *dst, uint64_t n);
+uint64_t gvo_mailboxes(const gvo_model *m);
+uint64_t gvo_creation_counter(const gvo_model *m);
+/* copy out a live message by index in the live list (0 <= i < messages) */
+int gvo_live_message(const gvo_model *m, uint64_t i, gvs_record *out);
+/* FNV-1a style digest over the whole logical state (ids, records, mailboxes) */
+uint64_t gvo_state_digest(const gvo_model *m);
+
+/* Seeded synthetic request stream, drawn against the model's current state
+ * (live ids/recipients), SplitMix64 driven.  `rng` is updated in place. */
+void gvo_identity(uint32_t i, uint8_t out[32]);
+void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
+                   gvs_request *reqs, uint32_t n, uint64_t op_base);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
