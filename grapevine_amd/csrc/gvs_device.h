@@ -20,6 +20,9 @@ constexpr uint32_t kIdTag = 0x47565331u;  // "GVS1", must match oracle
 constexpr uint32_t kPending = 0xFFu;      // internal status: decided later
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kGroupMax = 512;            // distinct recipients per mailbox partition per batch
+constexpr int kStash = 2048;              // per-partition ops kept in LDS (beyond: re-read)
+constexpr int kRowsMax = 4096;            // message rows per partition (S)
+constexpr int kBinsMax = 16384;           // histogram bins (Q+1, W+1) kept in LDS
 constexpr int kSrMax = 1024;              // mailbox rows per partition
 constexpr int kTile = 256;                // message rows per R-pass tile
 constexpr int kSeqBits = 20;              // B <= 2^20
@@ -40,25 +43,40 @@ enum Kind : uint32_t {
 constexpr uint32_t CF_POP = 1u;     // delete-next that pops a message
 constexpr uint32_t CF_MBOX_OK = 2u; // create passes the mailbox checks
 
-struct alignas(16) OpState {  // 64 B, seq-indexed, written by k_meta
+// Per-op records are 128 B (one L2 line) and written whole by one thread, so
+// no two ops ever share a line: scattered per-op traffic then touches a fixed
+// set of lines whatever order the data imposes (obliviousness).
+struct alignas(128) OpState {  // seq-indexed, written by k_meta
   uint32_t kind, pre_status, slot, q;
   uint64_t ts, h_hi, h_lo;
   uint32_t id[4];
-  uint32_t pad[2];
+  uint32_t x[8];  // mailbox key (recipient / auth) for mailbox-touching ops
+  uint32_t pad[10];
 };
-static_assert(sizeof(OpState) == 64, "OpState");
+static_assert(sizeof(OpState) == 128, "OpState");
 
-struct alignas(16) M1Out {  // 32 B, seq-indexed, written by the M1 pass
+struct alignas(128) M1Out {  // seq-indexed, written by the M1 pass
   uint32_t status, slot, flags, pad;
   uint32_t id[4];
+  uint32_t pad2[24];
 };
+static_assert(sizeof(M1Out) == 128, "M1Out");
 
-struct alignas(16) ROp {  // 64 B, seq-indexed: everything the R and M2 passes need
+struct alignas(128) ROp {  // seq-indexed: everything the R and M2 passes need
   uint32_t status, slot, kind, flags;
   uint32_t id[4];
-  uint32_t x[8];  // mailbox key (recipient / auth) for mailbox-touching ops
+  uint32_t x[8];
+  uint32_t pad[16];
 };
-static_assert(sizeof(ROp) == 64, "ROp");
+static_assert(sizeof(ROp) == 128, "ROp");
+
+struct alignas(128) RRes {  // seq-indexed result of the message pass
+  uint32_t status, pad0, pad1, pad2;
+  uint32_t pad[28];
+};
+static_assert(sizeof(RRes) == 128, "RRes");
+
+constexpr uint32_t kRespSlot = 1152;  // internal response slot: 9 whole 128-B lines
 
 struct alignas(16) Key128 {
   uint64_t hi, lo;

@@ -56,6 +56,7 @@ struct gvs_handle {
   uint32_t* ring = nullptr;
   Scal* scal = nullptr;
   // per-batch scratch
+  uint32_t nblk = 0;
   uint4* img = nullptr;
   uint32_t* types = nullptr;
   OpState* ops = nullptr;
@@ -64,19 +65,21 @@ struct gvs_handle {
   uint32_t* qcount = nullptr;
   uint32_t* qstart = nullptr;
   M1Out* m1out = nullptr;
-  uint32_t* cflag = nullptr;
-  uint32_t* m1slot = nullptr;
-  uint32_t* pfx_pop = nullptr;
-  uint32_t* pfx_s = nullptr;
+  uint32_t* pflag = nullptr;
+  uint32_t* pslot = nullptr;
+  uint32_t* bsum = nullptr;
+  uint32_t* cslot = nullptr;
   ROp* rop = nullptr;
   uint64_t* rkeys = nullptr;
-  uint32_t* tcount = nullptr;
-  uint32_t* tstart = nullptr;
-  uint32_t* fstatus = nullptr;
-  uint32_t* pfx_post = nullptr;
+  uint32_t* pcount = nullptr;
+  uint32_t* pstart = nullptr;
+  RRes* rres = nullptr;
+  uint4* resp = nullptr;
+  uint32_t* dflag = nullptr;
+  uint32_t* dslot = nullptr;
+  uint32_t* bsum2 = nullptr;
   uint4* in_stage = nullptr;
   uint4* out_stage = nullptr;
-  uint4* out_scratch = nullptr;
   hipEvent_t ev[kMaxStages + 1] = {};
   bool timed = false;
   std::vector<void*> allocs;
@@ -127,7 +130,8 @@ static int validate(const gvs_config* c) {
   if (!c) return GVS_ERR_INVALID_ARG;
   if (!is_pow2(c->msg_capacity) || c->msg_capacity < 256 || c->msg_capacity > (1ull << 32))
     return GVS_ERR_INVALID_ARG;
-  if (!is_pow2(c->mailbox_partitions) || c->mailbox_partitions > (1u << 20)) return GVS_ERR_INVALID_ARG;
+  if (!is_pow2(c->mailbox_partitions) || c->mailbox_partitions + 1 > (uint32_t)kBinsMax)
+    return GVS_ERR_INVALID_ARG;
   if (c->mailbox_partition_slots == 0 || c->mailbox_partition_slots > (uint32_t)kSrMax ||
       (c->mailbox_partition_slots % 16) != 0)
     return GVS_ERR_INVALID_ARG;
@@ -174,7 +178,12 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   h->S = (uint32_t)S;
   h->W = (uint32_t)(h->N / S);
   h->NT = (uint32_t)(h->N / kTile);
+  h->nblk = h->B / 1024;
   h->ring_size = h->N + h->B;
+  if (h->W + 1 > (uint32_t)kBinsMax || h->S > (uint32_t)kRowsMax) {
+    delete h;
+    return GVS_ERR_INVALID_ARG;
+  }
   h->kc.pk0 = ld64(cfg->secret_key);
   h->kc.pk1 = ld64(cfg->secret_key + 8);
   h->kc.hk0 = ld64(cfg->secret_key + 16);
@@ -214,19 +223,21 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   A(qcount, h->Q + 1);
   A(qstart, h->Q + 2);
   A(m1out, B);
-  A(cflag, B);
-  A(m1slot, B);
-  A(pfx_pop, B);
-  A(pfx_s, B);
+  A(pflag, B);
+  A(pslot, B);
+  A(bsum, 2 * h->nblk);
+  A(cslot, B);
   A(rop, B);
   A(rkeys, B);
-  A(tcount, h->NT + 1);
-  A(tstart, h->NT + 2);
-  A(fstatus, B);
-  A(pfx_post, B);
+  A(pcount, h->W + 1);
+  A(pstart, h->W + 2);
+  A(rres, B);
+  A(resp, B * (kRespSlot / 16));
+  A(dflag, B);
+  A(dslot, B);
+  A(bsum2, h->nblk);
   A(in_stage, B * 65);
   A(out_stage, B * 65);
-  A(out_scratch, B * 65);
 #undef A
   hipStream_t s = h->stream;
   if (hipMemsetAsync(h->table, 0, h->N * 1024, s) != hipSuccess ||
@@ -272,10 +283,8 @@ static MArgs margs(gvs_handle* h) {
   a.mbox = h->mbox;
   a.side = h->side;
   a.m1out = h->m1out;
-  a.cflag = h->cflag;
-  a.m1slot = h->m1slot;
   a.rop = h->rop;
-  a.fstatus = h->fstatus;
+  a.rres = h->rres;
   a.scal = h->scal;
   a.Q = h->Q;
   a.Sr = h->Sr;
@@ -286,24 +295,49 @@ static MArgs margs(gvs_handle* h) {
   return a;
 }
 
-// Enqueue the whole pipeline for one batch on h->stream.
+static AllocArgs aargs(gvs_handle* h) {
+  AllocArgs a{};
+  a.kinds = h->kinds;
+  a.m1out = h->m1out;
+  a.ops = h->ops;
+  a.pflag = h->pflag;
+  a.pslot = h->pslot;
+  a.bsum = h->bsum;
+  a.cslot = h->cslot;
+  a.ring = h->ring;
+  a.rop = h->rop;
+  a.rkeys = h->rkeys;
+  a.pcount = h->pcount;
+  a.scal = h->scal;
+  a.B = h->B;
+  a.nblk = h->nblk;
+  a.W = h->W;
+  a.S = h->S;
+  a.N = h->N;
+  a.ring_size = h->ring_size;
+  a.kc = h->kc;
+  return a;
+}
+
+// Enqueue the whole pipeline for one batch on h->stream; responses for the
+// first n requests are written to d_out (caller layout).
 static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out) {
   hipStream_t s = h->stream;
-  const uint32_t B = h->B;
+  const uint32_t B = h->B, nblk = h->nblk;
   int st = 0;
   auto mark = [&](int i) {
     if (h->timed) (void)hipEventRecord(h->ev[i], s);
   };
   GVS_HIP(h, hipMemsetAsync(&h->scal->error, 0, sizeof(uint32_t), s));
   GVS_HIP(h, hipMemsetAsync(h->qcount, 0, (h->Q + 1) * sizeof(uint32_t), s));
-  GVS_HIP(h, hipMemsetAsync(h->tcount, 0, (h->NT + 1) * sizeof(uint32_t), s));
+  GVS_HIP(h, hipMemsetAsync(h->pcount, 0, (h->W + 1) * sizeof(uint32_t), s));
   mark(st++);
   hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, n, B, h->img, h->types);
   mark(st++);
   {
     MetaArgs a{h->img, h->types, h->ops, h->kinds, h->s1keys, h->qcount,
                n, B, h->Q, h->logQ, h->N, h->kc};
-    hipLaunchKernelGGL(k_meta, dim3(B / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_meta, dim3(nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, h->qcount, h->qstart, h->Q + 1);
   }
   mark(st++);
@@ -312,30 +346,11 @@ static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_o
   hipLaunchKernelGGL(k_m1, dim3(h->Q + kDummyBlocks), dim3(256), 0, s, margs(h));
   mark(st++);
   {
-    AllocArgs a{h->kinds, h->cflag, h->m1slot, h->pfx_pop, h->pfx_s, h->ring, h->scal, B,
-                h->N, h->ring_size};
-    hipLaunchKernelGGL(k_alloc_a, dim3(1), dim3(1024), 0, s, a);
-    AllocBArgs b{};
-    b.img = h->img;
-    b.ops = h->ops;
-    b.kinds = h->kinds;
-    b.cflag = h->cflag;
-    b.m1out = h->m1out;
-    b.pfx_s = h->pfx_s;
-    b.ring = h->ring;
-    b.rop = h->rop;
-    b.rkeys = h->rkeys;
-    b.tcount = h->tcount;
-    b.scal = h->scal;
-    b.B = B;
-    b.W = h->W;
-    b.S = h->S;
-    b.NT = h->NT;
-    b.N = h->N;
-    b.ring_size = h->ring_size;
-    b.kc = h->kc;
-    hipLaunchKernelGGL(k_alloc_b, dim3(B / 256), dim3(256), 0, s, b);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, h->tcount, h->tstart, h->NT + 1);
+    AllocArgs a = aargs(h);
+    hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, h->pcount, h->pstart, h->W + 1);
   }
   mark(st++);
   if (int r = sort_keys<uint64_t, 8192>(h, h->rkeys, B)) return r;
@@ -344,28 +359,29 @@ static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_o
     RArgs a{};
     a.table = h->table;
     a.rkeys = h->rkeys;
-    a.tstart = h->tstart;
+    a.pstart = h->pstart;
     a.rop = h->rop;
     a.img = h->img;
-    a.out = d_out;
-    a.out_scratch = h->out_scratch;
-    a.fstatus = h->fstatus;
+    a.resp = h->resp;
+    a.rres = h->rres;
     a.scal = h->scal;
     a.n = n;
     a.B = B;
     a.W = h->W;
     a.S = h->S;
-    a.NT = h->NT;
     a.null_blocks = kNullBlocks;
     hipLaunchKernelGGL(k_rpass<4>, dim3(h->W + kNullBlocks), dim3(256), 0, s, a);
   }
   mark(st++);
   {
-    PostArgs a{h->kinds, h->fstatus, h->rop, h->pfx_post, h->ring, h->scal, B, h->ring_size};
-    hipLaunchKernelGGL(k_post, dim3(1), dim3(1024), 0, s, a);
+    PostArgs a{h->kinds, h->rres, h->rop, h->dflag, h->dslot, h->bsum2, h->ring, h->scal,
+               B, nblk, h->ring_size};
+    hipLaunchKernelGGL(k_post_sum, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
   }
   mark(st++);
   hipLaunchKernelGGL(k_m2, dim3(h->Q + kDummyBlocks), dim3(256), 0, s, margs(h));
+  if (n) hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)h->resp, n, d_out);
   mark(st++);
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;

@@ -1,20 +1,23 @@
 // gvs_kernels.h — gfx950 HIP kernels of the batched oblivious store pipeline.
 //
-// Per batch (DESIGN.md §3 has the full pipeline and the obliviousness rules):
-//   k_copy      request AoS (ABI layout) -> 1 KiB request images + type array
-//   k_meta      classify, recipient PRF, id decode, mailbox sort keys, histogram
-//   sort128     LDS-staged bitonic sort of the mailbox keys (S1)
-//   k_m1        mailbox read pass: resolve next-message ops, create admission
-//   k_alloc_a   seq-order scan: pops, mailbox-ok creates, free-ring appends
-//   k_alloc_b   capacity cutoff, slot allocation, id PRP, message-pass keys
-//   sort64      bitonic sort of the message-pass keys
-//   k_rpass     message table pass: stream every row, cmov-apply ops, emit responses
-//   k_post      seq-order scan: by-id deletes -> free ring, scalar commit
-//   k_m2        mailbox write pass: pops, appends, removals, new mailboxes
+// Per batch (DESIGN.md §3 has the pipeline, §3 "Obliviousness" the rules):
+//   k_copy        request AoS (ABI layout) -> 1 KiB request images + type words
+//   k_meta        classify, recipient PRF, id decode, mailbox sort keys, histogram
+//   sort128       LDS-staged bitonic sort of the mailbox keys (S1)
+//   k_m1          mailbox read pass: resolve next-message ops, create admission
+//   k_alloc_sum   seq-order flags + block sums (pops, mailbox-ok creates)
+//   k_alloc_ring  one workgroup: pops -> free ring; allocation window -> creates
+//   k_alloc_b     capacity cutoff, id PRP, message-pass keys + histogram
+//   sort64        bitonic sort of the message-pass keys
+//   k_rpass       message table pass: stream every row, apply ops, emit responses
+//   k_post_sum / k_post_ring   by-id deletes -> free ring, scalar commit
+//   k_m2          mailbox write pass: pops, appends, removals, new mailboxes
+//   k_out         internal 1152-B response slots -> caller's 1040-B responses
 //
-// Rule used by every kernel: each table row is read and written exactly once
-// per pass, and each op's per-kernel reads/writes have a fixed size, so launch
-// sequence, grid sizes and HBM byte counts depend only on (N, R, B, n).
+// Every kernel keeps a fixed per-op footprint (same reads and writes for an op
+// whatever its kind or outcome), reads/writes every table row exactly once,
+// uses 128-B per-op records, and does data-dependent permutations of sub-line
+// data only inside a single workgroup.
 #pragma once
 #include "gvs_device.h"
 
@@ -79,9 +82,27 @@ __global__ __launch_bounds__(256) void k_bitonic_global(K* data, uint32_t n, uin
   }
 }
 
-// ------------------------------------------------------ single-block scans
+// ------------------------------------------------------------ block helpers
 
-// out[i] = sum(in[0..i)), out[n] = total.  One block of 1024 threads.
+// Exclusive prefix of a per-thread flag over a 1024-thread block.  Returns the
+// prefix; *total gets the block count.  Uses s_w[16].
+__device__ inline uint32_t block1024_prefix(bool f, uint32_t* s_w, uint32_t* total) {
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint64_t m = __ballot(f);
+  if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (uint32_t w = 0; w < 16; ++w) {
+    off += w < wave ? s_w[w] : 0u;
+    tot += s_w[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + mbcnt64(m);
+}
+
+// out[i] = sum(in[0..i)), out[n] = total.  One block of 1024 threads; n is
+// small (histogram bins).
 __global__ __launch_bounds__(1024) void k_scan_excl(const uint32_t* in, uint32_t* out,
                                                     uint32_t n) {
   __shared__ uint32_t s[1024];
@@ -107,9 +128,11 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const uint32_t* in, uint32_t
   if (t == T - 1) out[n] = s[T - 1];
 }
 
-__global__ void k_fill_u32(uint32_t* p, uint32_t v, uint32_t n) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = v;
+// LDS histogram of one 1024-op block, then every bin (zeros included) added to
+// the global histogram: a fixed set of atomics whatever the bins' contents.
+__device__ inline void hist_flush(uint32_t* s_hist, uint32_t nbins, uint32_t* g_hist) {
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) atomicAdd(&g_hist[b], s_hist[b]);
 }
 
 // ------------------------------------------------------------------ k_copy
@@ -146,24 +169,23 @@ struct MetaArgs {
   KeyCtx kc;
 };
 
-__global__ __launch_bounds__(256) void k_meta(MetaArgs a) {
+__global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
+  __shared__ uint32_t s_hist[kBinsMax];
+  for (uint32_t b = threadIdx.x; b <= a.Q; b += blockDim.x) s_hist[b] = 0;
+  __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.B) return;
   const uint4* row = a.img + (uint64_t)i * 64;
   uint4 c0 = row[0], c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4], c5 = row[5];
   const uint32_t type = a.types[i];
-  OpState o;
+  OpState o = {};
   o.id[0] = c0.x; o.id[1] = c0.y; o.id[2] = c0.z; o.id[3] = c0.w;
   o.ts = u4lo(c5);
   o.slot = kNone;
-  o.h_hi = 0;
-  o.h_lo = 0;
-  o.pad[0] = o.pad[1] = 0;
   const bool id_zero = !nz4(c0);
   const bool auth_zero = !nz4(c1) && !nz4(c2);
   const bool rcpt_zero = !nz4(c3) && !nz4(c4);
   uint32_t kind, pre = kPending, cls = 3, sub = 0;
-  uint64_t x[4] = {0, 0, 0, 0};
+  uint4 xa = c3, xb = c4;  // mailbox key: recipient, or auth for next ops
   if (i >= a.n) {
     kind = KIND_PAD;
     pre = 0;
@@ -172,40 +194,40 @@ __global__ __launch_bounds__(256) void k_meta(MetaArgs a) {
     pre = 0;
   } else if (type == 1u) {
     kind = KIND_CREATE;
-    if (rcpt_zero) {
-      pre = 4;  // INVALID_RECIPIENT, grapevine.proto:72
-    } else {
-      cls = 1;
-      x[0] = u4lo(c3); x[1] = u4hi(c3); x[2] = u4lo(c4); x[3] = u4hi(c4);
-    }
+    if (rcpt_zero) pre = 4;  // INVALID_RECIPIENT, grapevine.proto:72
+    else cls = 1;
   } else if ((type == 2u || type == 4u) && id_zero) {
     kind = type == 2u ? KIND_NEXT_READ : KIND_NEXT_DEL;
     cls = 0;
     sub = type == 4u ? 1u : 0u;
-    x[0] = u4lo(c1); x[1] = u4hi(c1); x[2] = u4lo(c2); x[3] = u4hi(c2);
+    xa = c1;
+    xb = c2;
   } else {
     kind = type == 2u ? KIND_READ : (type == 3u ? KIND_UPDATE : KIND_DELETE);
     uint32_t s = id_decode(a.kc, u4lo(c0), u4hi(c0), a.N);
     o.slot = s;
     if (s == kNone) pre = 2;  // NOT_FOUND: the id names no slot
-    else if (kind == KIND_DELETE && !rcpt_zero) {
-      cls = 2;
-      x[0] = u4lo(c3); x[1] = u4hi(c3); x[2] = u4lo(c4); x[3] = u4hi(c4);
-    }
+    else if (kind == KIND_DELETE && !rcpt_zero) cls = 2;
   }
+  o.x[0] = xa.x; o.x[1] = xa.y; o.x[2] = xa.z; o.x[3] = xa.w;
+  o.x[4] = xb.x; o.x[5] = xb.y; o.x[6] = xb.z; o.x[7] = xb.w;
   Key128 key;
   uint32_t q = a.Q;
-  if (cls < 3) {
+  {
+    // the PRF runs for every op (fixed work); only participants use it
+    const uint64_t x[4] = {u4lo(xa), u4hi(xa), u4lo(xb), u4hi(xb)};
     uint64_t hi, lo;
     recipient_hash(a.kc, x, hi, lo);
-    o.h_hi = hi;
-    o.h_lo = lo;
-    q = a.logQ ? (uint32_t)(hi >> (64 - a.logQ)) : 0u;
-    key.hi = hi;
-    key.lo = s1_lo(lo, cls, i, sub);
-  } else {
-    key.hi = ~0ull;
-    key.lo = (~0ull << 21) | ((uint64_t)i << 1);
+    if (cls < 3) {
+      o.h_hi = hi;
+      o.h_lo = lo;
+      q = a.logQ ? (uint32_t)(hi >> (64 - a.logQ)) : 0u;
+      key.hi = hi;
+      key.lo = s1_lo(lo, cls, i, sub);
+    } else {
+      key.hi = ~0ull;
+      key.lo = (~0ull << 21) | ((uint64_t)i << 1);
+    }
   }
   o.kind = kind;
   o.pre_status = pre;
@@ -213,7 +235,8 @@ __global__ __launch_bounds__(256) void k_meta(MetaArgs a) {
   a.ops[i] = o;
   a.kinds[i] = kind;
   a.s1keys[i] = key;
-  atomicAdd(&a.qcount[q], 1u);
+  atomicAdd(&s_hist[q], 1u);
+  hist_flush(s_hist, a.Q + 1, a.qcount);
 }
 
 // ------------------------------------------------------ mailbox passes M1/M2
@@ -232,35 +255,60 @@ struct MArgs {
   uint4* mbox;             // R rows x 64 uint4
   uint4* side;             // R entries
   M1Out* m1out;
-  uint32_t* cflag;
-  uint32_t* m1slot;
   const ROp* rop;          // M2
-  const uint32_t* fstatus; // M2
+  const RRes* rres;        // M2
   Scal* scal;
   uint32_t Q, Sr, B, dummy_blocks;
   uint64_t N;
   KeyCtx kc;
 };
 
-// Phase A shared by M1 and M2: discover groups of the sorted key range
-// [start, end) of this partition into LDS.  Returns the group count, or
+// packed per-op info kept in LDS: seq | class<<20 | sub<<22 | success<<23
+__device__ inline uint32_t pack_s1(uint64_t lo, uint32_t succ) {
+  return s1_seq(lo) | (s1_class(lo) << 20) | (s1_sub(lo) << 22) | (succ << 23);
+}
+__device__ inline uint32_t pk_seq(uint32_t p) { return p & kSeqMask; }
+__device__ inline uint32_t pk_sub(uint32_t p) { return (p >> 22) & 1u; }
+__device__ inline uint32_t pk_succ(uint32_t p) { return (p >> 23) & 1u; }
+
+// Per-op info of sorted position m of the partition starting at `start`.
+// Positions beyond the LDS stash (a partition with > kStash ops in one batch)
+// re-read the key (and for M2 the status): correct, but a data-dependent read.
+template <bool kM2>
+__device__ inline uint32_t op_info(const MArgs& a, const uint32_t* stash, uint32_t start,
+                                   uint32_t m) {
+  const uint32_t k = m - start;
+  if (k < (uint32_t)kStash) return stash[k];
+  const Key128 key = a.keys[m];
+  uint32_t succ = 0;
+  if (kM2) succ = a.rres[s1_seq(key.lo)].status == 1u ? 1u : 0u;
+  return pack_s1(key.lo, succ);
+}
+
+// Phase A shared by M1 and M2: discover the groups of the sorted key range
+// [start, end) into LDS and stash each op's packed info.  Each key (and for M2
+// each op's status) is read exactly once.  Returns the group count, or
 // kGroupMax+1 on overflow.
 template <bool kM2>
 __device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end,
-                                    GroupL* g, uint32_t* s_w, uint32_t* s_ng) {
+                                    GroupL* g, uint32_t* stash, Key128* s_key,
+                                    uint32_t* s_w, uint32_t* s_ng) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) *s_ng = 0;
-  __syncthreads();
+  Key128 last = {~0ull, ~0ull};
   for (uint32_t base = start; base < end; base += 256) {
     const uint32_t i = base + tid;
     const bool valid = i < end;
-    Key128 key = {~0ull, ~0ull}, prev = {~0ull, ~0ull};
-    uint32_t fst = 0;
+    Key128 key = {~0ull, ~0ull};
+    uint32_t succ = 0;
     if (valid) {
       key = a.keys[i];
-      if (i > 0) prev = a.keys[i - 1];
-      if (kM2) fst = a.fstatus[s1_seq(key.lo)];
+      if (kM2) succ = a.rres[s1_seq(key.lo)].status == 1u ? 1u : 0u;
     }
+    s_key[tid] = key;
+    __syncthreads();
+    const Key128 prev = tid > 0 ? s_key[tid - 1] : last;
+    last = s_key[255];
     const bool head = valid && (i == start || key.hi != prev.hi ||
                                 s1_group(key.lo) != s1_group(prev.lo));
     const uint64_t bm = __ballot(head);
@@ -286,6 +334,7 @@ __device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end
       G.slot = -1;
       G.n_succ = G.n_delok = G.fl = 0;
     }
+    if (valid && i - start < (uint32_t)kStash) stash[i - start] = pack_s1(key.lo, succ);
     __syncthreads();
     if (valid && incl >= 1 && incl - 1 < (uint32_t)kGroupMax) {
       GroupL& G = g[incl - 1];
@@ -296,16 +345,17 @@ __device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end
       } else if (cls == 1) {
         atomicAdd(&G.n_create, 1u);
         atomicMin(&G.fcs, seq);
-        if (kM2 && fst == 1u) atomicAdd(&G.n_succ, 1u);
+        if (kM2 && succ) atomicAdd(&G.n_succ, 1u);
       } else {
         atomicAdd(&G.n_x, 1u);
-        if (kM2 && fst == 1u) atomicAdd(&G.n_delok, 1u);
+        if (kM2 && succ) atomicAdd(&G.n_delok, 1u);
       }
     }
     __syncthreads();
     if (tid == 0) *s_ng = ng0 + tot;
     __syncthreads();
   }
+  __syncthreads();
   uint32_t ng = *s_ng;
   return ng > (uint32_t)kGroupMax ? (uint32_t)kGroupMax + 1 : ng;
 }
@@ -343,66 +393,88 @@ __device__ inline void side_prepass(const MArgs& a, uint32_t q, GroupL* g, uint3
   }
 }
 
-__device__ inline void m1_write(const MArgs& a, uint32_t seq, uint32_t status, uint32_t slot,
-                                uint32_t flags, uint4 id) {
-  M1Out o;
-  o.status = status;
-  o.slot = slot;
-  o.flags = flags;
-  o.pad = 0;
-  o.id[0] = id.x; o.id[1] = id.y; o.id[2] = id.z; o.id[3] = id.w;
-  a.m1out[seq] = o;
-  a.cflag[seq] = flags;
-  a.m1slot[seq] = slot;
+// Wave-cooperative write of up to 64 M1Out records (one per lane): each store
+// instruction covers 8 whole 128-B records, so no record line is ever left
+// partially written in L2 (partial lines make write-back traffic depend on
+// eviction timing).  All 64 lanes must call.
+__device__ inline void m1_write_wave(const MArgs& a, bool valid, uint32_t seq, uint32_t status,
+                                     uint32_t slot, uint32_t flags, uint4 id) {
+  const uint32_t lane = lane_id();
+  uint4* base = reinterpret_cast<uint4*>(a.m1out);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int src = it * 8 + (int)(lane >> 3);
+    const uint32_t chunk = lane & 7u;
+    const uint32_t v = __shfl((uint32_t)valid, src), sq = __shfl(seq, src);
+    const uint4 hdr = make_uint4(__shfl(status, src), __shfl(slot, src), __shfl(flags, src), 0u);
+    const uint4 sid = shfl4(id, src);
+    const uint4 d = chunk == 0 ? hdr : (chunk == 1 ? sid : make_uint4(0, 0, 0, 0));
+    if (v) base[(uint64_t)sq * 8 + chunk] = d;
+  }
 }
 
 // Resolve the next-message ops (class 0) of group G against its mailbox row v
 // (lane 2+k holds id k): the op that has d delete-nexts before it reads id d.
-__device__ void m1_resolve_next(const MArgs& a, const GroupL& G, uint4 v) {
+__device__ void m1_resolve_next(const MArgs& a, const GroupL& G, uint4 v, const uint32_t* stash,
+                                uint32_t start) {
   const uint32_t lane = lane_id();
   const uint32_t len = G.len;
   uint32_t carry = 0;
   for (uint32_t c = 0; c < G.n_next; c += 64) {
     const bool valid = c + lane < G.n_next;
-    Key128 key = {0, 0};
-    if (valid) key = a.keys[G.first + c + lane];
-    const uint32_t seq = s1_seq(key.lo), sub = s1_sub(key.lo);
+    uint32_t p = 0;
+    if (valid) p = op_info<false>(a, stash, start, G.first + c + lane);
+    const uint32_t seq = pk_seq(p), sub = pk_sub(p);
     const uint64_t dm = __ballot(valid && sub);
     const uint32_t d = carry + mbcnt64(dm);
     carry += (uint32_t)__popcll(dm);
     const uint4 id = shfl4(v, 2 + (int)min(d, 61u));
-    if (valid) {
-      if (d < len) {
-        uint32_t slot = id_decode(a.kc, u4lo(id), u4hi(id), a.N);
-        m1_write(a, seq, kPending, slot, sub ? CF_POP : 0u, id);
-      } else {
-        m1_write(a, seq, 2u, kNone, 0u, make_uint4(0, 0, 0, 0));
+    const bool found = d < len;
+    const uint32_t slot = found ? id_decode(a.kc, u4lo(id), u4hi(id), a.N) : kNone;
+    m1_write_wave(a, valid, seq, found ? kPending : 2u, slot, (found && sub) ? CF_POP : 0u,
+                  found ? id : make_uint4(0, 0, 0, 0));
+  }
+}
+
+// ops that touch no mailbox: the same per-op footprint as participants
+// (one key read [+ status read, ROp read for M2] and the same writes)
+template <bool kM2>
+__device__ void dummy_partition(const MArgs& a, uint32_t b) {
+  const uint32_t start = a.qstart[a.Q], end = a.qstart[a.Q + 1];
+  const uint32_t nb = a.dummy_blocks;
+  const uint32_t len = end - start, per = (len + nb - 1) / nb;
+  const uint32_t lo = start + b * per, hi = min(end, lo + per);
+  for (uint32_t base = lo; base < hi; base += 256) {
+    const uint32_t i = base + threadIdx.x;
+    const bool valid = i < hi;
+    uint32_t seq = 0;
+    if (valid) seq = s1_seq(a.keys[i].lo);
+    if (kM2) {
+      if (valid) {
+        const uint32_t st = a.rres[seq].status;
+        const ROp r = a.rop[seq];
+        asm volatile("" ::"v"(st), "v"(r.id[0]), "v"(r.x[0]));
       }
+    } else {
+      m1_write_wave(a, valid, seq, kPending, kNone, 0u, make_uint4(0, 0, 0, 0));
     }
   }
 }
 
 __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __shared__ GroupL g[kGroupMax];
+  __shared__ uint32_t stash[kStash];
+  __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t q = blockIdx.x;
   if (q >= a.Q) {
-    // dummy partition: ops that touch no mailbox; same per-op reads/writes
-    const uint32_t start = a.qstart[a.Q], end = a.qstart[a.Q + 1];
-    const uint32_t nb = a.dummy_blocks, b = q - a.Q;
-    const uint32_t len = end - start, per = (len + nb - 1) / nb;
-    const uint32_t lo = start + b * per, hi = min(end, lo + per);
-    for (uint32_t i = lo + tid; i < hi; i += 256) {
-      Key128 key = a.keys[i];
-      if (i > 0) (void)a.keys[i - 1];
-      m1_write(a, s1_seq(key.lo), kPending, kNone, 0u, make_uint4(0, 0, 0, 0));
-    }
+    dummy_partition<false>(a, q - a.Q);
     return;
   }
   const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
-  const uint32_t ng = discover_groups<false>(a, start, end, g, s_w, &s_ng);
+  const uint32_t ng = discover_groups<false>(a, start, end, g, stash, s_key, s_w, &s_ng);
   if (ng > (uint32_t)kGroupMax) {
     if (tid == 0) atomicOr(&a.scal->error, 1u);
     return;
@@ -424,7 +496,7 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = s_sg[j0 + u];
-      if (k >= 0) m1_resolve_next(a, g[k], v[u]);
+      if (k >= 0) m1_resolve_next(a, g[k], v[u], stash, start);
     }
   }
   __syncthreads();
@@ -458,164 +530,188 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   // Phase E: creates get their mailbox verdict; every remaining op is visited once.
   for (uint32_t k = wave; k < ng; k += 4) {
     const GroupL& G = g[k];
+    const uint4 z = make_uint4(0, 0, 0, 0);
     if (G.slot < 0) {
-      for (uint32_t c = lane; c < G.n_next; c += 64) {
-        Key128 key = a.keys[G.first + c];
-        m1_write(a, s1_seq(key.lo), 2u, kNone, 0u, make_uint4(0, 0, 0, 0));
+      for (uint32_t c = 0; c < G.n_next; c += 64) {
+        const bool valid = c + lane < G.n_next;
+        const uint32_t p = valid ? op_info<false>(a, stash, start, G.first + c + lane) : 0u;
+        m1_write_wave(a, valid, pk_seq(p), 2u, kNone, 0u, z);
       }
     }
     const bool exists1 = G.flags & 1u, admitted = G.flags & 2u;
-    for (uint32_t r = lane; r < G.n_create; r += 64) {
-      Key128 key = a.keys[G.first + G.n_next + r];
+    for (uint32_t c = 0; c < G.n_create; c += 64) {
+      const uint32_t r = c + lane;
+      const bool valid = r < G.n_create;
+      const uint32_t p = valid ? op_info<false>(a, stash, start, G.first + G.n_next + r) : 0u;
       const bool ok = exists1 ? (G.fl + r < GVS_MAILBOX_SLOTS) : (admitted && r < GVS_MAILBOX_SLOTS);
       const uint32_t st = ok ? kPending : ((exists1 || admitted) ? 5u : 6u);
-      m1_write(a, s1_seq(key.lo), st, kNone, ok ? CF_MBOX_OK : 0u, make_uint4(0, 0, 0, 0));
+      m1_write_wave(a, valid, pk_seq(p), st, kNone, ok ? CF_MBOX_OK : 0u, z);
     }
-    for (uint32_t r = lane; r < G.n_x; r += 64) {
-      Key128 key = a.keys[G.first + G.n_next + G.n_create + r];
-      m1_write(a, s1_seq(key.lo), kPending, kNone, 0u, make_uint4(0, 0, 0, 0));
+    for (uint32_t c = 0; c < G.n_x; c += 64) {
+      const bool valid = c + lane < G.n_x;
+      const uint32_t p =
+          valid ? op_info<false>(a, stash, start, G.first + G.n_next + G.n_create + c + lane) : 0u;
+      m1_write_wave(a, valid, pk_seq(p), kPending, kNone, 0u, z);
     }
   }
 }
 
-// ---------------------------------------------------------- allocation scans
+// ---------------------------------------------------------- allocation
 
 struct AllocArgs {
   const uint32_t* kinds;
-  const uint32_t* cflag;
-  const uint32_t* m1slot;
-  uint32_t* pfx_pop;   // B: exclusive prefix of pops
-  uint32_t* pfx_s;     // B: exclusive prefix of mailbox-ok creates
-  uint32_t* ring;
-  Scal* scal;
-  uint32_t B;
-  uint64_t N, ring_size;
-};
-
-// One block of 1024 threads: two flag scans in seq order and the free-ring
-// window write for delete-next pops (a permutation of [tail, tail+B)).
-__global__ __launch_bounds__(1024) void k_alloc_a(AllocArgs a) {
-  __shared__ uint32_t s_w[2][16];
-  __shared__ uint32_t s_carry[2];
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  if (a.scal->error) return;
-  if (tid == 0) {
-    s_carry[0] = 0;
-    s_carry[1] = 0;
-  }
-  __syncthreads();
-  for (uint32_t base = 0; base < a.B; base += 1024) {
-    const uint32_t i = base + tid;
-    const uint32_t cf = a.cflag[i];
-    const bool pop = cf & CF_POP;
-    const bool s = (cf & CF_MBOX_OK) && a.kinds[i] == KIND_CREATE;
-    const uint64_t mp = __ballot(pop), ms = __ballot(s);
-    if (lane == 0) {
-      s_w[0][wave] = (uint32_t)__popcll(mp);
-      s_w[1][wave] = (uint32_t)__popcll(ms);
-    }
-    __syncthreads();
-    uint32_t op = 0, os = 0, tp = 0, ts = 0;
-    for (uint32_t w = 0; w < 16; ++w) {
-      op += w < wave ? s_w[0][w] : 0u;
-      os += w < wave ? s_w[1][w] : 0u;
-      tp += s_w[0][w];
-      ts += s_w[1][w];
-    }
-    a.pfx_pop[i] = s_carry[0] + op + mbcnt64(mp);
-    a.pfx_s[i] = s_carry[1] + os + mbcnt64(ms);
-    __syncthreads();
-    if (tid == 0) {
-      s_carry[0] += tp;
-      s_carry[1] += ts;
-    }
-    __syncthreads();
-  }
-  const uint32_t pops = s_carry[0], scnt = s_carry[1];
-  const uint64_t tail = a.scal->tail;
-  for (uint32_t i = tid; i < a.B; i += 1024) {
-    const uint32_t P = a.pfx_pop[i];
-    const bool pop = a.cflag[i] & CF_POP;
-    const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
-    const uint32_t val = pop ? a.m1slot[i] : kNone;
-    a.ring[(tail + pos) % a.ring_size] = val;
-  }
-  if (tid == 0) {
-    Scal* s = a.scal;
-    s->pops = pops;
-    s->scnt = scnt;
-    s->count1 = s->count - pops;
-    const uint64_t room = a.N - s->count1;
-    s->m = scnt < room ? scnt : room;
-    s->head0 = s->head;
-    s->tail0 = tail;
-  }
-}
-
-struct AllocBArgs {
-  const uint4* img;
-  const OpState* ops;
-  const uint32_t* kinds;
-  const uint32_t* cflag;
   const M1Out* m1out;
-  const uint32_t* pfx_s;
-  const uint32_t* ring;
+  const OpState* ops;
+  uint32_t* pflag;  // bit0 pop, bit1 mailbox-ok create
+  uint32_t* pslot;  // popped slot
+  uint32_t* bsum;   // 2 per block
+  uint32_t* cslot;  // allocated slot per op (kNone if not a successful create)
+  uint32_t* ring;
   ROp* rop;
   uint64_t* rkeys;
-  uint32_t* tcount;  // NT+1 tile counters
-  const Scal* scal;
-  uint32_t B, W, S, NT;
+  uint32_t* pcount;  // W+1 partition counters
+  Scal* scal;
+  uint32_t B, nblk, W, S;
   uint64_t N, ring_size;
   KeyCtx kc;
 };
 
-// Per op: capacity cutoff (TOO_MANY_MESSAGES before the mailbox checks), slot
-// allocation from the free ring, id PRP, and the message-pass routing key.
-__global__ __launch_bounds__(256) void k_alloc_b(AllocBArgs a) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.B) return;
+// seq-order compact flags (coalesced, fixed) + per-block counts
+__global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
+  __shared__ uint32_t s_w[16];
   if (a.scal->error) return;
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const M1Out m1 = a.m1out[i];
+  const uint32_t kind = a.kinds[i];
+  const bool pop = (m1.flags & CF_POP) != 0u;
+  const bool s = (m1.flags & CF_MBOX_OK) != 0u && kind == KIND_CREATE;
+  a.pflag[i] = (pop ? 1u : 0u) | (s ? 2u : 0u);
+  a.pslot[i] = m1.slot;
+  uint32_t tp, ts;
+  (void)block1024_prefix(pop, s_w, &tp);
+  (void)block1024_prefix(s, s_w, &ts);
+  if (threadIdx.x == 0) {
+    a.bsum[2 * blockIdx.x] = tp;
+    a.bsum[2 * blockIdx.x + 1] = ts;
+  }
+}
+
+// One workgroup: (1) delete-next pops -> free ring window [tail, tail+B) in seq
+// order (a permutation of the window); (2) the allocation window
+// [head, head+B) is read in order, exactly once, and its first m entries are
+// handed to the successful creates in seq order (TOO_MANY_MESSAGES cutoff).
+__global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_off[2][1024];
+  __shared__ uint32_t s_win[2048];
+  const uint32_t tid = threadIdx.x;
+  if (a.scal->error) return;
+  // block offsets (nblk <= 1024)
+  uint32_t vp = tid < a.nblk ? a.bsum[2 * tid] : 0u, vs = tid < a.nblk ? a.bsum[2 * tid + 1] : 0u;
+  s_off[0][tid] = vp;
+  s_off[1][tid] = vs;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t x = tid >= off ? s_off[0][tid - off] : 0u, y = tid >= off ? s_off[1][tid - off] : 0u;
+    __syncthreads();
+    s_off[0][tid] += x;
+    s_off[1][tid] += y;
+    __syncthreads();
+  }
+  const uint32_t pops = s_off[0][1023], scnt = s_off[1][1023];
+  Scal* sc = a.scal;
+  const uint64_t tail0 = sc->tail, head0 = sc->head;
+  const uint64_t count1 = sc->count - pops;
+  const uint64_t room = a.N - count1;
+  const uint64_t m = scnt < room ? scnt : room;
+  // (1) pops -> ring
+  for (uint32_t c = 0; c < a.nblk; ++c) {
+    const uint32_t i = c * 1024 + tid;
+    const uint32_t f = a.pflag[i], slot = a.pslot[i];
+    const bool pop = f & 1u;
+    uint32_t tot;
+    const uint32_t pre = block1024_prefix(pop, s_w, &tot);
+    const uint32_t P = (c ? s_off[0][c - 1] : 0u) + pre;
+    const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
+    a.ring[(tail0 + pos) % a.ring_size] = pop ? slot : kNone;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // (2) allocation window, streamed in order through a 2048-entry LDS ring
+  uint32_t loaded = 0;  // window entries loaded so far (multiple of 1024)
+  for (uint32_t c = 0; c < a.nblk; ++c) {
+    const uint32_t i = c * 1024 + tid;
+    const bool s = a.pflag[i] & 2u;
+    uint32_t tot;
+    const uint32_t pre = block1024_prefix(s, s_w, &tot);
+    const uint32_t S0 = c ? s_off[1][c - 1] : 0u;
+    const uint32_t Si = S0 + pre;
+    const uint32_t need = (uint32_t)min((uint64_t)(S0 + tot), m);
+    while (loaded < need) {  // uniform across the block
+      s_win[(loaded + tid) & 2047u] = a.ring[(head0 + loaded + tid) % a.ring_size];
+      loaded += 1024;
+      __syncthreads();
+    }
+    const bool success = s && (uint64_t)Si < m;
+    a.cslot[i] = success ? s_win[Si & 2047u] : kNone;
+    __syncthreads();
+  }
+  while (loaded < a.B) {  // read the rest of the window: fixed B entries per batch
+    const uint32_t v = a.ring[(head0 + loaded + tid) % a.ring_size];
+    asm volatile("" ::"v"(v));
+    loaded += 1024;
+  }
+  if (tid == 0) {
+    sc->pops = pops;
+    sc->scnt = scnt;
+    sc->count1 = count1;
+    sc->m = m;
+    sc->head0 = head0;
+    sc->tail0 = tail0;
+  }
+}
+
+// Per op: statuses, ids, message-pass routing keys, partition histogram.
+__global__ __launch_bounds__(1024) void k_alloc_b(AllocArgs a) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_hist[kBinsMax];
+  const uint32_t tid = threadIdx.x;
+  if (a.scal->error) return;
+  for (uint32_t b = tid; b <= a.W; b += 1024) s_hist[b] = 0;
+  // S_i: block offset + in-block prefix of mailbox-ok creates
+  uint32_t boff = 0;
+  for (uint32_t b = 0; b < blockIdx.x; ++b) boff += a.bsum[2 * b + 1];
+  const uint32_t i = blockIdx.x * 1024 + tid;
+  const uint32_t f = a.pflag[i];
+  uint32_t tot;
+  const uint32_t S_i = boff + block1024_prefix((f & 2u) != 0u, s_w, &tot);
   const uint32_t kind = a.kinds[i];
   const OpState os = a.ops[i];
   const M1Out m1 = a.m1out[i];
-  const uint32_t cf = a.cflag[i];
-  const uint32_t S_i = a.pfx_s[i];
-  const uint4* row = a.img + (uint64_t)i * 64;
-  const uint4 c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4];
-  const uint64_t count1 = a.scal->count1, m = a.scal->m, head0 = a.scal->head0;
-  const uint64_t ctr0 = a.scal->ctr;
+  const uint32_t cs = a.cslot[i];
+  const Scal* sc = a.scal;
+  const uint64_t count1 = sc->count1, ctr0 = sc->ctr;
 
-  ROp r;
+  ROp r = {};
   r.kind = kind;
-  r.flags = 0;
   r.status = os.pre_status;
   r.slot = kNone;
   r.id[0] = os.id[0]; r.id[1] = os.id[1]; r.id[2] = os.id[2]; r.id[3] = os.id[3];
-  uint4 xa = c3, xb = c4;  // recipient
+  for (int k = 0; k < 8; ++k) r.x[k] = os.x[k];
   uint32_t cls = 3;
-
-  const bool s = (cf & CF_MBOX_OK) && kind == KIND_CREATE;
-  const uint64_t succ_before = S_i < m ? S_i : m;
-  bool success = false;
+  uint64_t L, R;
+  id_encode(a.kc, cs == kNone ? 0u : cs, ctr0 + S_i, L, R);  // fixed work for every op
   if (kind == KIND_CREATE && os.pre_status == kPending) {
-    if (count1 + S_i >= a.N) r.status = 7;  // TOO_MANY_MESSAGES
-    else if (!s) r.status = m1.status;      // 5 or 6 from the mailbox pass
-    else success = true;
-  }
-  // free-ring gather: successes read [head0, head0+m), others the rest of the window
-  const uint64_t rpos = success ? (uint64_t)S_i : m + (i - succ_before);
-  const uint32_t ring_slot = a.ring[(head0 + rpos) % a.ring_size];
-  if (success) {
-    uint64_t L, R;
-    id_encode(a.kc, ring_slot, ctr0 + S_i, L, R);
-    r.slot = ring_slot;
-    r.status = kPending;
-    r.id[0] = (uint32_t)L; r.id[1] = (uint32_t)(L >> 32);
-    r.id[2] = (uint32_t)R; r.id[3] = (uint32_t)(R >> 32);
-    cls = 1;
+    if (count1 + S_i >= a.N) r.status = 7;  // TOO_MANY_MESSAGES (checked before 5/6)
+    else if (cs == kNone) r.status = m1.status;  // 5 or 6 from the mailbox pass
+    else {
+      r.slot = cs;
+      r.status = kPending;
+      r.id[0] = (uint32_t)L; r.id[1] = (uint32_t)(L >> 32);
+      r.id[2] = (uint32_t)R; r.id[3] = (uint32_t)(R >> 32);
+      cls = 1;
+    }
   } else if (kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL) {
-    xa = c1;
-    xb = c2;  // auth identity
     r.status = m1.status;
     if (m1.status == kPending) {
       r.slot = m1.slot;
@@ -626,20 +722,19 @@ __global__ __launch_bounds__(256) void k_alloc_b(AllocBArgs a) {
     r.slot = os.slot;
     if (os.slot != kNone) cls = 2;
   }
-  r.x[0] = xa.x; r.x[1] = xa.y; r.x[2] = xa.z; r.x[3] = xa.w;
-  r.x[4] = xb.x; r.x[5] = xb.y; r.x[6] = xb.z; r.x[7] = xb.w;
   a.rop[i] = r;
   uint64_t rowp = kRNullRow;
-  uint32_t tile = a.NT;
+  uint32_t part = a.W;
   if (cls < 3) {
     const uint32_t sl = r.slot;
-    rowp = (uint64_t)(sl % a.W) * a.S + sl / a.W;
-    tile = (uint32_t)(rowp / kTile);
+    part = sl % a.W;
+    rowp = (uint64_t)part * a.S + sl / a.W;
   } else {
     cls = 0;
   }
   a.rkeys[i] = r_key(rowp, cls, i);
-  atomicAdd(&a.tcount[tile], 1u);
+  atomicAdd(&s_hist[part], 1u);
+  hist_flush(s_hist, a.W + 1, a.pcount);
 }
 
 // ---------------------------------------------------------------- R pass
@@ -647,23 +742,23 @@ __global__ __launch_bounds__(256) void k_alloc_b(AllocBArgs a) {
 struct RArgs {
   uint4* table;             // N rows x 64 uint4, partition-major
   const uint64_t* rkeys;    // sorted
-  const uint32_t* tstart;   // NT+2
+  const uint32_t* pstart;   // W+2
   const ROp* rop;
   const uint4* img;
-  uint4* out;               // user responses (65 uint4 each) for seq < n
-  uint4* out_scratch;       // responses for padding rows seq >= n
-  uint32_t* fstatus;
+  uint4* resp;              // B internal slots of kRespSlot bytes
+  RRes* rres;
   const Scal* scal;
-  uint32_t n, B, W, S, NT, null_blocks;
+  uint32_t n, B, W, S, null_blocks;
 };
 
 __device__ inline void write_response(const RArgs& a, uint32_t seq, uint4 rec, uint32_t status) {
   const uint32_t lane = lane_id();
-  uint4* dst = seq < a.n ? a.out + (uint64_t)seq * 65 : a.out_scratch + (uint64_t)(seq - a.n) * 65;
+  uint4* dst = a.resp + (uint64_t)seq * (kRespSlot / 16);
   dst[lane] = rec;
-  if (lane == 0) {
-    dst[64] = make_uint4(status, 0, 0, 0);
-    a.fstatus[seq] = status;
+  if (lane < 8) {
+    const uint4 t = make_uint4(lane == 0 ? status : 0u, 0, 0, 0);
+    dst[64 + lane] = t;                                        // status line of the slot
+    reinterpret_cast<uint4*>(a.rres)[(uint64_t)seq * 8 + lane] = t;  // whole RRes line
   }
 }
 
@@ -679,13 +774,21 @@ __device__ inline uint4 fail_record(uint4 q, uint32_t status) {
   return r;
 }
 
+// packed R-pass op: row offset in partition << 20 | seq
+__device__ inline uint32_t r_op_at(const RArgs& a, const uint32_t* stash, uint32_t start,
+                                   uint32_t k, uint64_t rowbase) {
+  if (k < (uint32_t)kStash) return stash[k];
+  const uint64_t key = a.rkeys[start + k];
+  return ((uint32_t)((key >> 22) - rowbase) << 20) | ((uint32_t)key & kSeqMask);
+}
+
 // Apply the ops routed to one row, in (class, seq) order, to the row held in v
 // (16 B per lane).  Wave-uniform control flow; data moves by lane-wise select.
-__device__ void r_apply(const RArgs& a, uint4& v, uint32_t first, uint32_t cnt) {
+__device__ void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, uint32_t start,
+                        uint64_t rowbase, uint32_t first, uint32_t cnt) {
   const uint32_t lane = lane_id();
   for (uint32_t k = 0; k < cnt; ++k) {
-    const uint64_t key = a.rkeys[first + k];
-    const uint32_t seq = (uint32_t)key & kSeqMask;
+    const uint32_t seq = r_op_at(a, stash, start, first + k, rowbase) & kSeqMask;
     const ROp r = a.rop[seq];
     const uint4 q = a.img[(uint64_t)seq * 64 + lane];
     const uint32_t kind = __builtin_amdgcn_readfirstlane(r.kind);
@@ -728,37 +831,60 @@ __device__ void r_apply(const RArgs& a, uint4& v, uint32_t first, uint32_t cnt) 
 
 template <int U>
 __global__ __launch_bounds__(256) void k_rpass(RArgs a) {
+  __shared__ uint32_t stash[kStash];
   __shared__ uint32_t s_first[kTile], s_cnt[kTile];
+  __shared__ uint32_t s_tile[kRowsMax / kTile + 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
   if (w >= a.W) {
-    // ops that touch no row: write their (failure) responses
-    const uint32_t start = a.tstart[a.NT], end = a.B;
+    // ops that touch no row: same footprint (key, ROp, image, response, result)
+    const uint32_t start = a.pstart[a.W], end = a.pstart[a.W + 1];
     const uint32_t nb = a.null_blocks, b = w - a.W;
     const uint32_t len = end - start, per = (len + nb - 1) / nb;
     const uint32_t lo = start + b * per, hi = min(end, lo + per);
     for (uint32_t i = lo + wave; i < hi; i += 4) {
       const uint32_t seq = (uint32_t)a.rkeys[i] & kSeqMask;
-      const uint32_t st = __builtin_amdgcn_readfirstlane(a.rop[seq].status);
+      const ROp r = a.rop[seq];
+      const uint32_t st = __builtin_amdgcn_readfirstlane(r.status);
+      asm volatile("" ::"v"(r.id[0]), "v"(r.kind));
       const uint4 q = a.img[(uint64_t)seq * 64 + lane];
       write_response(a, seq, fail_record(q, st), st);
     }
     return;
   }
-  uint4* part = a.table + (uint64_t)w * a.S * 64;
+  const uint32_t start = a.pstart[w], end = a.pstart[w + 1];
+  const uint32_t cnt = end - start;
+  const uint64_t rowbase = (uint64_t)w * a.S;
+  // stash this partition's ops (each key read once): row offset << 20 | seq
+  for (uint32_t k = tid; k < cnt && k < (uint32_t)kStash; k += 256) {
+    const uint64_t key = a.rkeys[start + k];
+    stash[k] = ((uint32_t)((key >> 22) - rowbase) << 20) | ((uint32_t)key & kSeqMask);
+  }
+  __syncthreads();
   const uint32_t tiles = a.S / kTile;
+  // first op of each tile: lower bound over the sorted stash
+  for (uint32_t t = tid; t <= tiles; t += 256) {
+    uint32_t lo = 0, hi = cnt;
+    const uint32_t target = t * kTile;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((r_op_at(a, stash, start, mid, rowbase) >> 20) < target) lo = mid + 1;
+      else hi = mid;
+    }
+    s_tile[t] = lo;
+  }
+  __syncthreads();
+  uint4* part = a.table + rowbase * 64;
   for (uint32_t t = 0; t < tiles; ++t) {
-    const uint32_t tile = w * tiles + t;
-    const uint32_t lo = a.tstart[tile], hi = a.tstart[tile + 1];
+    const uint32_t lo = s_tile[t], hi = s_tile[t + 1];
     s_cnt[tid] = 0;
     s_first[tid] = 0xFFFFFFFFu;
     __syncthreads();
-    const uint64_t rowbase = (uint64_t)tile * kTile;
-    for (uint32_t i = lo + tid; i < hi; i += 256) {
-      const uint32_t o = (uint32_t)((a.rkeys[i] >> 22) - rowbase);
+    for (uint32_t k = lo + tid; k < hi; k += 256) {
+      const uint32_t o = (r_op_at(a, stash, start, k, rowbase) >> 20) - t * kTile;
       atomicAdd(&s_cnt[o], 1u);
-      atomicMin(&s_first[o], i);
+      atomicMin(&s_first[o], k);
     }
     __syncthreads();
     const uint32_t rb = t * kTile + wave * 64;
@@ -770,7 +896,7 @@ __global__ __launch_bounds__(256) void k_rpass(RArgs a) {
       for (int u = 0; u < U; ++u) {
         const uint32_t o = wave * 64 + j + u;
         const uint32_t c = s_cnt[o];
-        if (c) r_apply(a, v[u], s_first[o], c);
+        if (c) r_apply(a, v[u], stash, start, rowbase, s_first[o], c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) part[(uint64_t)(rb + j + u) * 64 + lane] = v[u];
@@ -783,80 +909,83 @@ __global__ __launch_bounds__(256) void k_rpass(RArgs a) {
 
 struct PostArgs {
   const uint32_t* kinds;
-  const uint32_t* fstatus;
+  const RRes* rres;
   const ROp* rop;
-  uint32_t* pfx;  // scratch B
+  uint32_t* dflag;
+  uint32_t* dslot;
+  uint32_t* bsum;
   uint32_t* ring;
   Scal* scal;
-  uint32_t B;
+  uint32_t B, nblk;
   uint64_t ring_size;
 };
 
-// by-id deletes append their slots to the free ring in seq order; commit scalars
-__global__ __launch_bounds__(1024) void k_post(PostArgs a) {
+__global__ __launch_bounds__(1024) void k_post_sum(PostArgs a) {
   __shared__ uint32_t s_w[16];
-  __shared__ uint32_t s_carry;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (a.scal->error) return;
-  if (tid == 0) s_carry = 0;
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t st = a.rres[i].status, slot = a.rop[i].slot;
+  const bool d = a.kinds[i] == KIND_DELETE && st == 1u;
+  a.dflag[i] = d ? 1u : 0u;
+  a.dslot[i] = slot;
+  uint32_t tot;
+  (void)block1024_prefix(d, s_w, &tot);
+  if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
+}
+
+// one workgroup: by-id deletes -> free ring in seq order; commit scalars
+__global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_off[1024];
+  const uint32_t tid = threadIdx.x;
+  if (a.scal->error) return;
+  s_off[tid] = tid < a.nblk ? a.bsum[tid] : 0u;
   __syncthreads();
-  for (uint32_t base = 0; base < a.B; base += 1024) {
-    const uint32_t i = base + tid;
-    const bool d = a.kinds[i] == KIND_DELETE && a.fstatus[i] == 1u;
-    const uint64_t md = __ballot(d);
-    if (lane == 0) s_w[wave] = (uint32_t)__popcll(md);
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t x = tid >= off ? s_off[tid - off] : 0u;
     __syncthreads();
-    uint32_t o = 0, t = 0;
-    for (uint32_t w = 0; w < 16; ++w) {
-      o += w < wave ? s_w[w] : 0u;
-      t += s_w[w];
-    }
-    a.pfx[i] = s_carry + o + mbcnt64(md);
-    __syncthreads();
-    if (tid == 0) s_carry += t;
+    s_off[tid] += x;
     __syncthreads();
   }
-  const uint32_t nd = s_carry;
-  const uint64_t tail = a.scal->tail0 + a.scal->pops;
-  for (uint32_t i = tid; i < a.B; i += 1024) {
-    const bool d = a.kinds[i] == KIND_DELETE && a.fstatus[i] == 1u;
-    const uint32_t P = a.pfx[i];
+  const uint32_t nd = s_off[1023];
+  Scal* sc = a.scal;
+  const uint64_t tail = sc->tail0 + sc->pops;
+  for (uint32_t c = 0; c < a.nblk; ++c) {
+    const uint32_t i = c * 1024 + tid;
+    const bool d = a.dflag[i] != 0u;
+    const uint32_t slot = a.dslot[i];
+    uint32_t tot;
+    const uint32_t pre = block1024_prefix(d, s_w, &tot);
+    const uint32_t P = (c ? s_off[c - 1] : 0u) + pre;
     const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
-    const uint32_t val = d ? a.rop[i].slot : kNone;
-    a.ring[(tail + pos) % a.ring_size] = val;
+    a.ring[(tail + pos) % a.ring_size] = d ? slot : kNone;
   }
   if (tid == 0) {
-    Scal* s = a.scal;
-    s->nd = nd;
-    s->count = s->count1 + s->m - nd;
-    s->head = s->head0 + s->m;
-    s->tail = s->tail0 + s->pops + nd;
-    s->ctr += s->m;
-    s->batches += 1;
+    sc->nd = nd;
+    sc->count = sc->count1 + sc->m - nd;
+    sc->head = sc->head0 + sc->m;
+    sc->tail = sc->tail0 + sc->pops + nd;
+    sc->ctr += sc->m;
+    sc->batches += 1;
   }
 }
 
 // ----------------------------------------------------------------- M2 pass
 
-__device__ inline void m2_visit(const MArgs& a, uint32_t sorted_idx, Key128& key, ROp& r,
-                                uint32_t& st) {
-  key = a.keys[sorted_idx];
-  const uint32_t seq = s1_seq(key.lo);
-  r = a.rop[seq];
-  st = a.fstatus[seq];
-}
-
 // Build the new state of one mailbox row: pop D' ids, append the ids of the
 // successful creates (a prefix of the class-1 members), remove ids of
-// successful by-id deletes, clear the row if it ends empty.
-__device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched) {
+// successful by-id deletes, clear the row if it ends empty.  Each member's
+// ROp is read exactly once here.
+__device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched,
+                         const uint32_t* stash, uint32_t start) {
   const uint32_t lane = lane_id();
   const uint32_t len = matched ? G.len : 0u;
   const uint32_t dp = min(G.n_del, len);
   for (uint32_t c = 0; c < G.n_next; c += 64) {  // visit pops (state needs only the count)
     if (c + lane < G.n_next) {
-      Key128 key; ROp r; uint32_t st;
-      m2_visit(a, G.first + c + lane, key, r, st);
+      const uint32_t p = op_info<true>(a, stash, start, G.first + c + lane);
+      const ROp r = a.rop[pk_seq(p)];
+      asm volatile("" ::"v"(r.id[0]), "v"(r.x[0]));
     }
   }
   if (dp) {
@@ -867,9 +996,13 @@ __device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched
   uint32_t cur = len - dp;
   for (uint32_t c = 0; c < G.n_create; c += 64) {
     const bool valid = c + lane < G.n_create;
-    Key128 key = {0, 0}; ROp r = {}; uint32_t st = 0;
-    if (valid) m2_visit(a, G.first + G.n_next + c + lane, key, r, st);
-    const uint64_t ms = __ballot(valid && st == 1u);
+    ROp r = {};
+    uint32_t p = 0;
+    if (valid) {
+      p = op_info<true>(a, stash, start, G.first + G.n_next + c + lane);
+      r = a.rop[pk_seq(p)];
+    }
+    const uint64_t ms = __ballot(valid && pk_succ(p));
     const uint32_t ns = (uint32_t)__popcll(ms);
     if (!matched && c == 0) {
       const uint4 x0 = shfl4(make_uint4(r.x[0], r.x[1], r.x[2], r.x[3]), 0);
@@ -885,9 +1018,13 @@ __device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched
   }
   for (uint32_t c = 0; c < G.n_x; c += 64) {
     const bool valid = c + lane < G.n_x;
-    Key128 key = {0, 0}; ROp r = {}; uint32_t st = 0;
-    if (valid) m2_visit(a, G.first + G.n_next + G.n_create + c + lane, key, r, st);
-    uint64_t md = __ballot(valid && st == 1u);
+    ROp r = {};
+    uint32_t p = 0;
+    if (valid) {
+      p = op_info<true>(a, stash, start, G.first + G.n_next + G.n_create + c + lane);
+      r = a.rop[pk_seq(p)];
+    }
+    uint64_t md = __ballot(valid && pk_succ(p));
     const uint4 myid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
     while (md) {
       const int b = __builtin_ctzll(md);
@@ -895,9 +1032,9 @@ __device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched
       const uint4 did = shfl4(myid, b);
       const uint64_t hit = __ballot(lane >= 2 && eq4(v, did));
       if (hit) {
-        const uint32_t p = (uint32_t)__builtin_ctzll(hit);
+        const uint32_t pos = (uint32_t)__builtin_ctzll(hit);
         const uint4 nxt = shfl4(v, (int)min(lane + 1, 63u));
-        if (lane >= p) v = lane < 63 ? nxt : make_uint4(0, 0, 0, 0);
+        if (lane >= pos) v = lane < 63 ? nxt : make_uint4(0, 0, 0, 0);
         cur -= 1;
       }
     }
@@ -932,6 +1069,8 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
 
 __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __shared__ GroupL g[kGroupMax];
+  __shared__ uint32_t stash[kStash];
+  __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ int16_t s_place[kSrMax];
   __shared__ uint8_t s_flag[kSrMax];
@@ -944,19 +1083,11 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   if (q >= a.Q) {
-    const uint32_t start = a.qstart[a.Q], end = a.qstart[a.Q + 1];
-    const uint32_t nb = a.dummy_blocks, b = q - a.Q;
-    const uint32_t len = end - start, per = (len + nb - 1) / nb;
-    const uint32_t lo = start + b * per, hi = min(end, lo + per);
-    for (uint32_t i = lo + tid; i < hi; i += 256) {
-      Key128 key; ROp r; uint32_t st;
-      m2_visit(a, i, key, r, st);
-      if (i > 0) (void)a.keys[i - 1];
-    }
+    dummy_partition<true>(a, q - a.Q);
     return;
   }
   const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
-  const uint32_t ng = discover_groups<true>(a, start, end, g, s_w, &s_ng);
+  const uint32_t ng = discover_groups<true>(a, start, end, g, stash, s_key, s_w, &s_ng);
   if (ng > (uint32_t)kGroupMax) return;  // M1 already flagged the batch
   if (tid == 0) {
     s_occ = 0;
@@ -1009,10 +1140,10 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
       const uint32_t j = j0 + u;
       const int k = s_sg[j], p = s_place[j];
       uint4 sd = a.side[(uint64_t)q * a.Sr + j];
-      if (k >= 0) m2_apply(a, g[k], v[u], true);
+      if (k >= 0) m2_apply(a, g[k], v[u], true, stash, start);
       if (p >= 0) {  // a new mailbox takes a row that is (or became) empty
         v[u] = make_uint4(0, 0, 0, 0);
-        m2_apply(a, g[p], v[u], false);
+        m2_apply(a, g[p], v[u], false, stash, start);
       }
       if (k >= 0 || p >= 0) {
         const GroupL& G = g[p >= 0 ? p : k];
@@ -1034,12 +1165,26 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
     if (G.slot >= 0 || s_gflag[k]) continue;
     const uint32_t cnt = G.n_next + G.n_create + G.n_x;
     for (uint32_t c = lane; c < cnt; c += 64) {
-      Key128 key; ROp r; uint32_t st;
-      m2_visit(a, G.first + c, key, r, st);
+      const uint32_t p = op_info<true>(a, stash, start, G.first + c);
+      const ROp r = a.rop[pk_seq(p)];
+      asm volatile("" ::"v"(r.id[0]), "v"(r.x[0]));
     }
   }
   if (tid == 0 && s_delta) atomicAdd((unsigned long long*)&a.scal->n_mailboxes,
                                      (unsigned long long)(int64_t)(int32_t)s_delta);
+}
+
+// ------------------------------------------------------------------ k_out
+
+// internal response slots (kRespSlot B, whole lines) -> caller layout (1040 B)
+__global__ __launch_bounds__(256) void k_out(const uint4* __restrict__ resp, uint32_t n,
+                                             uint4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = lane_id();
+  if (i >= n) return;
+  const uint4* src = resp + (uint64_t)i * (kRespSlot / 16);
+  out[(uint64_t)i * 65 + lane] = src[lane];
+  if (lane == 0) out[(uint64_t)i * 65 + 64] = src[64];
 }
 
 }  // namespace gvs

@@ -42,8 +42,11 @@ def diff_tables(got, want, limit=5):
     return out
 
 
-def run_stream(store, model, params, batches, n, check_table=True):
-    """Drive `batches` seeded batches through both; assert bit-exact parity."""
+def run_stream(store, model, params, batches, n, check_table=True, seen=None):
+    """Drive `batches` seeded batches through both; assert bit-exact parity.
+    Returns a Counter of the status codes seen (coverage evidence)."""
+    from collections import Counter
+    seen = Counter() if seen is None else seen
     for b in range(batches):
         reqs = model.gen_batch(n, params)
         want = model.process_batch(reqs)
@@ -54,7 +57,8 @@ def run_stream(store, model, params, batches, n, check_table=True):
         assert st["messages"] == model.messages, (b, st, model.messages)
         assert st["mailboxes"] == model.mailboxes, (b, st, model.mailboxes)
         assert st["creation_counter"] == model.creation_counter
+        seen.update(int(x) for x in want["status_code"])
     if check_table:
         dt = diff_tables(store.dump_messages(), model.dump_messages())
         assert not dt, "\n".join(dt)
-    return True
+    return seen

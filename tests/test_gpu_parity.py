@@ -33,7 +33,8 @@ def test_library_is_native():
 def test_mixed_stream_small():
     store, model = make_pair(4096, 16, 32, 1024)
     model.seed(11)
-    run_stream(store, model, ffi.gen_params(n_identities=300), batches=12, n=1024)
+    seen = run_stream(store, model, ffi.gen_params(n_identities=300), batches=12, n=1024)
+    assert {0, 1, 2, 4} <= set(seen), seen
 
 
 def test_create_heavy_then_drain():
@@ -48,16 +49,18 @@ def test_create_heavy_then_drain():
 def test_hot_recipient_62_limit():
     store, model = make_pair(8192, 16, 32, 1024)
     model.seed(13)
-    run_stream(store, model, ffi.gen_params(create=50, read=20, update=10, delete=20,
-                                            hot=40, n_identities=100), batches=8, n=1024)
+    seen = run_stream(store, model, ffi.gen_params(create=50, read=20, update=10, delete=20,
+                                                   hot=40, n_identities=100), batches=8, n=1024)
+    assert seen[5] > 0, seen
 
 
 def test_message_capacity_exhaustion():
     # N = 256 slots, creates only: TOO_MANY_MESSAGES once full, then deletes free slots
     store, model = make_pair(256, 4, 64, 1024)
     model.seed(14)
-    run_stream(store, model, ffi.gen_params(create=100, read=0, update=0, delete=0,
-                                            n_identities=50), batches=2, n=300)
+    seen = run_stream(store, model, ffi.gen_params(create=100, read=0, update=0, delete=0,
+                                                   n_identities=50), batches=2, n=300)
+    assert seen[7] > 0, seen
     run_stream(store, model, ffi.gen_params(create=50, read=0, update=0, delete=50, nxt=50,
                                             n_identities=50), batches=4, n=500)
 
@@ -66,7 +69,8 @@ def test_recipient_capacity_exhaustion():
     # 4 partitions x 16 rows = 64 mailboxes for 2000 identities
     store, model = make_pair(4096, 4, 16, 1024)
     model.seed(15)
-    run_stream(store, model, ffi.gen_params(n_identities=2000), batches=6, n=1024)
+    seen = run_stream(store, model, ffi.gen_params(n_identities=2000), batches=6, n=1024)
+    assert seen[6] > 0, seen
 
 
 def test_partial_batches_and_single_access():
