@@ -22,7 +22,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kGroupMax = 512;            // distinct recipients per mailbox partition per batch
 constexpr int kStash = 2048;              // per-partition ops kept in LDS (beyond: re-read)
 constexpr int kRowsMax = 4096;            // message rows per partition (S)
-constexpr int kBinsMax = 16384;           // histogram bins (Q+1, W+1) kept in LDS
+constexpr int kBinsMax = 32768;           // histogram bins (Q+1, W+1) kept in LDS
 constexpr int kSrMax = 1024;              // mailbox rows per partition
 constexpr int kTile = 256;                // message rows per R-pass tile
 constexpr int kSeqBits = 20;              // B <= 2^20

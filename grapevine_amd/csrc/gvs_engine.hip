@@ -57,6 +57,7 @@ struct gvs_handle {
   Scal* scal = nullptr;
   // per-batch scratch
   uint32_t nblk = 0;
+  uint64_t extra = 0;
   uint4* img = nullptr;
   uint32_t* types = nullptr;
   OpState* ops = nullptr;
@@ -82,6 +83,7 @@ struct gvs_handle {
   uint4* out_stage = nullptr;
   hipEvent_t ev[kMaxStages + 1] = {};
   bool timed = false;
+  int rpass_variant = 2;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -138,6 +140,8 @@ static int validate(const gvs_config* c) {
   if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << kSeqBits))
     return GVS_ERR_INVALID_ARG;
   if (c->flags != 0) return GVS_ERR_INVALID_ARG;
+  for (int i = 1; i < 7; ++i)
+    if (c->reserved[i] != 0) return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
 
@@ -171,10 +175,17 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   h->R = (uint64_t)h->Q * h->Sr;
   h->B = cfg->max_batch;
   h->logQ = log2u(h->Q);
-  uint64_t S = h->N / 2048;
+  // rows per message-table partition (one workgroup each): reserved[0] if set,
+  // else N/16384 clamped to [256, 4096] (C3: 1024 rows -> 16384 workgroups, so
+  // the grid is many times the resident capacity and its tail is short)
+  uint64_t S = cfg->reserved[0] ? cfg->reserved[0] : h->N / 16384;
   if (S < (uint64_t)kTile) S = kTile;
-  if (S > 4096) S = 4096;
+  if (S > (uint64_t)kRowsMax) S = kRowsMax;
   if (S > h->N) S = h->N;
+  if (!is_pow2(S)) {
+    delete h;
+    return GVS_ERR_INVALID_ARG;
+  }
   h->S = (uint32_t)S;
   h->W = (uint32_t)(h->N / S);
   h->NT = (uint32_t)(h->N / kTile);
@@ -215,24 +226,28 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   A(side, h->R);
   A(ring, h->ring_size);
   A(scal, 1);
-  A(img, B * 64);
+  // per-op arrays carry E extra records after the B real ones; record B is the
+  // shared dummy of the dry-run ops (fixed instruction footprint)
+  const uint64_t E = 64;
+  h->extra = E;
+  A(img, (B + E) * 64);
   A(types, B);
   A(ops, B);
   A(kinds, B);
   A(s1keys, B);
   A(qcount, h->Q + 1);
   A(qstart, h->Q + 2);
-  A(m1out, B);
+  A(m1out, B + E);
   A(pflag, B);
   A(pslot, B);
   A(bsum, 2 * h->nblk);
   A(cslot, B);
-  A(rop, B);
+  A(rop, B + E);
   A(rkeys, B);
   A(pcount, h->W + 1);
   A(pstart, h->W + 2);
-  A(rres, B);
-  A(resp, B * (kRespSlot / 16));
+  A(rres, B + E);
+  A(resp, (B + E) * (kRespSlot / 16));
   A(dflag, B);
   A(dslot, B);
   A(bsum2, h->nblk);
@@ -240,7 +255,9 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   A(out_stage, B * 65);
 #undef A
   hipStream_t s = h->stream;
-  if (hipMemsetAsync(h->table, 0, h->N * 1024, s) != hipSuccess ||
+  if (hipMemsetAsync(h->img + B * 64, 0, E * 1024, s) != hipSuccess ||
+      hipMemsetAsync(h->rop + B, 0, E * sizeof(ROp), s) != hipSuccess ||
+      hipMemsetAsync(h->table, 0, h->N * 1024, s) != hipSuccess ||
       hipMemsetAsync(h->mbox, 0, h->R * 1024, s) != hipSuccess ||
       hipMemsetAsync(h->side, 0, h->R * 16, s) != hipSuccess)
     return fail(GVS_ERR_DEVICE);
@@ -370,7 +387,16 @@ static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_o
     a.W = h->W;
     a.S = h->S;
     a.null_blocks = kNullBlocks;
-    hipLaunchKernelGGL(k_rpass<4>, dim3(h->W + kNullBlocks), dim3(256), 0, s, a);
+    const dim3 g(h->W + kNullBlocks), b(256);
+    switch (h->rpass_variant) {
+      case 0: hipLaunchKernelGGL((k_rpass<4, false, false, 1>), g, b, 0, s, a); break;
+      case 1: hipLaunchKernelGGL((k_rpass<4, true, true, 1>), g, b, 0, s, a); break;
+      case 3: hipLaunchKernelGGL((k_rpass<8, true, false, 4>), g, b, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_rpass<8, false, true, 4>), g, b, 0, s, a); break;
+      case 5: hipLaunchKernelGGL((k_rpass<2, true, true, 8>), g, b, 0, s, a); break;
+      case 6: hipLaunchKernelGGL((k_rpass<16, true, true, 2>), g, b, 0, s, a); break;
+      default: hipLaunchKernelGGL((k_rpass<8, true, true, 4>), g, b, 0, s, a); break;
+    }
   }
   mark(st++);
   {
@@ -467,6 +493,15 @@ int gvs_set_timing(gvs_handle* h, int on) {
   if (!h) return GVS_ERR_INVALID_ARG;
   h->timed = on != 0;
   return GVS_OK;
+}
+
+int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
+  if (!h || !key) return GVS_ERR_INVALID_ARG;
+  if (std::strcmp(key, "rpass_variant") == 0 && value >= 0 && value <= 6) {
+    h->rpass_variant = (int)value;
+    return GVS_OK;
+  }
+  return GVS_ERR_INVALID_ARG;
 }
 
 int gvs_last_timings(gvs_handle* h, const char** names, float* ms, int cap) {

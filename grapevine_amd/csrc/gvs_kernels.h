@@ -184,7 +184,7 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   const bool id_zero = !nz4(c0);
   const bool auth_zero = !nz4(c1) && !nz4(c2);
   const bool rcpt_zero = !nz4(c3) && !nz4(c4);
-  uint32_t kind, pre = kPending, cls = 3, sub = 0;
+  uint32_t kind = 0xFFFFFFFFu, pre = kPending, cls = 3, sub = 0;
   uint4 xa = c3, xb = c4;  // mailbox key: recipient, or auth for next ops
   if (i >= a.n) {
     kind = KIND_PAD;
@@ -202,9 +202,11 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
     sub = type == 4u ? 1u : 0u;
     xa = c1;
     xb = c2;
-  } else {
+  }
+  const uint32_t dec = id_decode(a.kc, u4lo(c0), u4hi(c0), a.N);  // every op: fixed work
+  if (kind == 0xFFFFFFFFu) {
+    const uint32_t s = dec;
     kind = type == 2u ? KIND_READ : (type == 3u ? KIND_UPDATE : KIND_DELETE);
-    uint32_t s = id_decode(a.kc, u4lo(c0), u4hi(c0), a.N);
     o.slot = s;
     if (s == kNone) pre = 2;  // NOT_FOUND: the id names no slot
     else if (kind == KIND_DELETE && !rcpt_zero) cls = 2;
@@ -415,15 +417,23 @@ __device__ inline void m1_write_wave(const MArgs& a, bool valid, uint32_t seq, u
 
 // Resolve the next-message ops (class 0) of group G against its mailbox row v
 // (lane 2+k holds id k): the op that has d delete-nexts before it reads id d.
-__device__ void m1_resolve_next(const MArgs& a, const GroupL& G, uint4 v, const uint32_t* stash,
-                                uint32_t start) {
+// Not inlined, and run once per workgroup in "dry" mode (one fake op writing
+// the shared dummy record `dry_seq` = B), so every workgroup fetches
+// this code whatever the batch holds: instruction fetch then does not depend
+// on the request mix.
+__device__ __attribute__((noinline)) void m1_resolve_next(const MArgs& a, const GroupL& G,
+                                                          uint4 v, const uint32_t* stash,
+                                                          uint32_t start, uint32_t dry_seq) {
   const uint32_t lane = lane_id();
-  const uint32_t len = G.len;
+  const bool dry = dry_seq != kNone;
+  const uint32_t len = dry ? 62u : G.len;
+  const uint32_t n_next = dry ? 1u : G.n_next;
   uint32_t carry = 0;
-  for (uint32_t c = 0; c < G.n_next; c += 64) {
-    const bool valid = c + lane < G.n_next;
+  for (uint32_t c = 0; c < n_next; c += 64) {
+    const bool valid = c + lane < n_next;
     uint32_t p = 0;
-    if (valid) p = op_info<false>(a, stash, start, G.first + c + lane);
+    if (valid) p = op_info<false>(a, stash, start, (dry ? start : G.first) + c + lane);
+    if (dry) p = dry_seq | (1u << 22);
     const uint32_t seq = pk_seq(p), sub = pk_sub(p);
     const uint64_t dm = __ballot(valid && sub);
     const uint32_t d = carry + mbcnt64(dm);
@@ -469,6 +479,10 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t q = blockIdx.x;
+  if (wave == 0) {  // fixed instruction footprint, see m1_resolve_next
+    GroupL fake = {};
+    m1_resolve_next(a, fake, make_uint4(0, 0, 0, 0), stash, 0u, a.B);
+  }
   if (q >= a.Q) {
     dummy_partition<false>(a, q - a.Q);
     return;
@@ -496,7 +510,7 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = s_sg[j0 + u];
-      if (k >= 0) m1_resolve_next(a, g[k], v[u], stash, start);
+      if (k >= 0) m1_resolve_next(a, g[k], v[u], stash, start, kNone);
     }
   }
   __syncthreads();
@@ -783,54 +797,80 @@ __device__ inline uint32_t r_op_at(const RArgs& a, const uint32_t* stash, uint32
 }
 
 // Apply the ops routed to one row, in (class, seq) order, to the row held in v
-// (16 B per lane).  Wave-uniform control flow; data moves by lane-wise select.
-__device__ void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, uint32_t start,
-                        uint64_t rowbase, uint32_t first, uint32_t cnt) {
+// (16 B per lane).  Branch-free over op kinds (lane-wise selects), so every op
+// runs the same instructions.  With `dry` set, a first fake op (the shared
+// dummy record `dry_seq` = B) runs on a zero row whose result is discarded:
+// wave 0 of every workgroup runs each inlined copy of this code once, so the
+// instruction fetch does not depend on the request mix.
+__device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, uint32_t start,
+                               uint64_t rowbase, uint32_t first, uint32_t cnt, bool dry,
+                               uint32_t dry_seq) {
   const uint32_t lane = lane_id();
-  for (uint32_t k = 0; k < cnt; ++k) {
-    const uint32_t seq = r_op_at(a, stash, start, first + k, rowbase) & kSeqMask;
+  const uint32_t n = cnt + (dry ? 1u : 0u);
+  for (uint32_t k = 0; k < n; ++k) {
+    const bool isdry = dry && k == 0;
+    const uint32_t kk = isdry ? 0u : k - (dry ? 1u : 0u);
+    const uint32_t pk = r_op_at(a, stash, start, first + kk, rowbase);
+    const uint32_t seq = isdry ? dry_seq : (pk & kSeqMask);
     const ROp r = a.rop[seq];
     const uint4 q = a.img[(uint64_t)seq * 64 + lane];
     const uint32_t kind = __builtin_amdgcn_readfirstlane(r.kind);
-    const uint4 vr = shfl4(v, (int)lane + 2);  // lanes 1,2 see the row's recipient
-    const uint64_t m_eq = __ballot(eq4(q, v));
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 cur = isdry ? z : v;
+    const uint4 vr = shfl4(cur, (int)lane + 2);  // lanes 1,2 see the row's recipient
+    const uint64_t m_eq = __ballot(eq4(q, cur));
     const uint64_t m_eqr = __ballot(eq4(q, vr));
-    const bool exists = (__ballot(nz4(v)) & 1ull) != 0;
+    const bool exists = (__ballot(nz4(cur)) & 1ull) != 0;
     const uint4 rid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
-    const bool rid_match = (__ballot(lane == 0 && eq4(v, rid)) & 1ull) != 0;
+    const bool rid_match = (__ballot(lane == 0 && eq4(cur, rid)) & 1ull) != 0;
     const bool id_match = (m_eq & 1ull) != 0;
     const bool auth_ok = ((m_eq & 6ull) == 6ull) || ((m_eqr & 6ull) == 6ull);
     const bool rcpt_ok = (m_eq & 0x18ull) == 0x18ull;
-    uint32_t status;
-    uint4 resp = v;
-    if (kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL) {
-      status = (exists && rid_match) ? 1u : 8u;  // resolved by M1; mismatch = internal error
-      if (status == 1u && kind == KIND_NEXT_DEL) v = make_uint4(0, 0, 0, 0);
-    } else if (kind == KIND_CREATE) {
-      status = exists ? 8u : 1u;  // the allocator only hands out free rows
-      if (status == 1u) {
-        v = lane == 0 ? rid : q;  // sender = auth, recipient, ts, payload from the image
-        resp = v;
-      }
-    } else {
-      const bool found = exists && id_match && auth_ok;
-      if (!found) status = 2u;                               // NOT_FOUND
-      else if (kind != KIND_READ && !rcpt_ok) status = 4u;   // INVALID_RECIPIENT
-      else status = 1u;
-      if (status == 1u && kind == KIND_UPDATE) {
-        if (lane >= 5) v = q;  // timestamp (lane 5 low half) + payload
-        resp = v;
-      } else if (status == 1u && kind == KIND_DELETE) {
-        v = make_uint4(0, 0, 0, 0);
-      }
-    }
-    if (status != 1u) resp = fail_record(q, status);
+    const bool is_next = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
+    const bool is_create = kind == KIND_CREATE;
+    // next ops were resolved by M1 (mismatch = internal error); the allocator
+    // only hands out free rows to creates; by-id ops check existence, auth
+    // (grapevine.proto:84,97,107) and then the recipient (:99-101,:110-112)
+    const uint32_t st_next = (exists && rid_match) ? 1u : 8u;
+    const uint32_t st_create = exists ? 8u : 1u;
+    const bool found = exists && id_match && auth_ok;
+    const uint32_t st_byid = !found ? 2u : ((kind != KIND_READ && !rcpt_ok) ? 4u : 1u);
+    const uint32_t status = is_next ? st_next : (is_create ? st_create : st_byid);
+    const bool ok = status == 1u;
+    const bool del = ok && (kind == KIND_NEXT_DEL || kind == KIND_DELETE);
+    const bool cre = ok && is_create;
+    const bool upd = ok && kind == KIND_UPDATE;
+    const uint4 v_create = lane == 0 ? rid : q;  // sender = auth, recipient, ts, payload
+    const uint4 v_upd = lane >= 5 ? q : cur;     // timestamp (lane 5 low half) + payload
+    const uint4 nv = del ? z : (cre ? v_create : (upd ? v_upd : cur));
+    const uint4 resp = ok ? ((cre || upd) ? nv : cur) : fail_record(q, status);
     write_response(a, seq, resp, status);
+    if (!isdry) v = nv;
   }
 }
 
-template <int U>
-__global__ __launch_bounds__(256) void k_rpass(RArgs a) {
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ inline uint4 ld_row(const uint4* p) {
+  if (NT) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+template <bool NT>
+__device__ inline void st_row(uint4* p, uint4 x) {
+  if (NT) {
+    v4u v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+  } else {
+    *p = x;
+  }
+}
+
+template <int U, bool NTL, bool NTS, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t stash[kStash];
   __shared__ uint32_t s_first[kTile], s_cnt[kTile];
   __shared__ uint32_t s_tile[kRowsMax / kTile + 1];
@@ -843,8 +883,11 @@ __global__ __launch_bounds__(256) void k_rpass(RArgs a) {
     const uint32_t nb = a.null_blocks, b = w - a.W;
     const uint32_t len = end - start, per = (len + nb - 1) / nb;
     const uint32_t lo = start + b * per, hi = min(end, lo + per);
-    for (uint32_t i = lo + wave; i < hi; i += 4) {
-      const uint32_t seq = (uint32_t)a.rkeys[i] & kSeqMask;
+    // wave 0 first runs a fake op on the shared dummy record: fixed code path
+    const uint32_t i0 = wave == 0 ? lo - 4 : lo + wave;
+    for (uint32_t i = i0; i < hi || i == i0; i += 4) {
+      const bool isdry = wave == 0 && i == i0;
+      const uint32_t seq = isdry ? a.B : ((uint32_t)a.rkeys[i] & kSeqMask);
       const ROp r = a.rop[seq];
       const uint32_t st = __builtin_amdgcn_readfirstlane(r.status);
       asm volatile("" ::"v"(r.id[0]), "v"(r.kind));
@@ -891,15 +934,16 @@ __global__ __launch_bounds__(256) void k_rpass(RArgs a) {
     for (uint32_t j = 0; j < 64; j += U) {
       uint4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = part[(uint64_t)(rb + j + u) * 64 + lane];
+      for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t o = wave * 64 + j + u;
         const uint32_t c = s_cnt[o];
-        if (c) r_apply(a, v[u], stash, start, rowbase, s_first[o], c);
+        const bool dry = (t == 0 && j == 0 && wave == 0);  // see r_apply
+        if (c || dry) r_apply(a, v[u], stash, start, rowbase, s_first[o], c, dry, a.B);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) part[(uint64_t)(rb + j + u) * 64 + lane] = v[u];
+      for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }
     __syncthreads();
   }

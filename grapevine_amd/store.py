@@ -20,7 +20,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgvstore
 EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
-    "gvs_synchronize", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
+    "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
 )
 
 
@@ -50,6 +50,7 @@ def load_library(path=None):
     lib.gvs_dump_messages.argtypes = [vp, vp, ctypes.c_uint64]
     lib.gvs_synchronize.argtypes = [vp]
     lib.gvs_set_timing.argtypes = [vp, i32]
+    lib.gvs_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     lib.gvs_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
                                      ctypes.POINTER(ctypes.c_float), i32]
     lib.gvs_last_error.argtypes = [vp]
@@ -118,6 +119,9 @@ class ObliviousStore:
 
     def synchronize(self):
         self._check(self.lib.gvs_synchronize(self.h))
+
+    def set_option(self, key, value):
+        self._check(self.lib.gvs_set_option(self.h, key.encode(), int(value)))
 
     def set_timing(self, on=True):
         self._check(self.lib.gvs_set_timing(self.h, 1 if on else 0))

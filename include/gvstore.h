@@ -125,7 +125,9 @@ typedef struct gvs_config {
   uint32_t device;              /* HIP device ordinal */
   uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key */
   uint32_t flags;               /* reserved, must be 0 */
-  uint32_t reserved[7];
+  uint32_t reserved[7];         /* [0]: message rows per table-pass workgroup
+                                   (power of two 256..4096; 0 = automatic);
+                                   the rest must be 0 */
 } gvs_config;
 
 typedef struct gvs_stats {
@@ -170,6 +172,11 @@ int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
 
 /* Wait for all work on the handle's stream. */
 int gvs_synchronize(gvs_handle *h);
+
+/* Tuning knobs (engine-internal choices that never change results):
+ * "rpass_variant" 0..6 selects the message-pass kernel instantiation
+ * (rows in flight per wave, non-temporal loads/stores). */
+int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 
 /* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */
 int gvs_set_timing(gvs_handle *h, int on);

@@ -59,6 +59,14 @@ def lib():
         L.gvo_live_message.argtypes = [vp, u64, vp]
         L.gvo_live_message.restype = ctypes.c_int
         L.gvo_identity.argtypes = [u32, ctypes.c_char_p]
+        L.gvp_create.argtypes = [ctypes.POINTER(abi.GvsConfig)]
+        L.gvp_create.restype = vp
+        L.gvp_destroy.argtypes = [vp]
+        L.gvp_process_batch.argtypes = [vp, vp, u32, vp]
+        L.gvp_process_batch.restype = ctypes.c_int
+        for f in ("gvp_messages", "gvp_mailboxes", "gvp_oram_accesses"):
+            getattr(L, f).argtypes = [vp]
+            getattr(L, f).restype = u64
         L.gvo_gen_batch.argtypes = [vp, ctypes.POINTER(GenParams), ctypes.POINTER(u64), vp, u32, u64]
         _LIB = L
     return _LIB
@@ -161,3 +169,46 @@ class Model:
         if self.L.gvo_live_message(self.m, i, rec.ctypes.data) != 0:
             raise IndexError(i)
         return rec[0]
+
+
+class PathOramModel:
+    """The Path ORAM restatement of the reference's CPU store path
+    (oracle/gvs_pathoram.c): CPU baseline, cross-checked against Model."""
+
+    def __init__(self, config):
+        self.L = lib()
+        self.config = config
+        self.m = self.L.gvp_create(ctypes.byref(config))
+        if not self.m:
+            raise MemoryError("gvp_create failed")
+
+    def close(self):
+        if self.m:
+            self.L.gvp_destroy(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process_batch(self, reqs):
+        reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+        out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
+        rc = self.L.gvp_process_batch(self.m, reqs.ctypes.data, len(reqs), out.ctypes.data)
+        if rc != 0:
+            raise ValueError(f"pathoram rejected batch: {rc}")
+        return out
+
+    @property
+    def messages(self):
+        return self.L.gvp_messages(self.m)
+
+    @property
+    def mailboxes(self):
+        return self.L.gvp_mailboxes(self.m)
+
+    @property
+    def oram_accesses(self):
+        return self.L.gvp_oram_accesses(self.m)

@@ -74,6 +74,17 @@ void gvo_identity(uint32_t i, uint8_t out[32]);
 void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
                    gvs_request *reqs, uint32_t n, uint64_t op_base);
 
+/* Path ORAM restatement of the reference's CPU path (gvs_pathoram.c): the
+ * same handler semantics over three Path ORAMs; the timed CPU baseline. */
+typedef struct gvp_model gvp_model;
+gvp_model *gvp_create(const gvs_config *cfg);
+void gvp_destroy(gvp_model *m);
+int gvp_process_batch(gvp_model *m, const gvs_request *reqs, uint32_t n, gvs_response *out);
+void gvp_apply_one(gvp_model *m, const gvs_request *req, gvs_response *out);
+uint64_t gvp_messages(const gvp_model *m);
+uint64_t gvp_mailboxes(const gvp_model *m);
+uint64_t gvp_oram_accesses(const gvp_model *m);
+
 #ifdef __cplusplus
 }
 #endif
