@@ -150,17 +150,14 @@ def cpu_baseline(budget_s, threads):
 def main():
     a = parse()
     import torch
-    import torch.distributed as dist
-    from grapevine_amd import abi
+    from grapevine_amd import abi, dist as gdist
     from grapevine_amd.store import ObliviousStore
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ri = gdist.rank_info()
+    world, rank, local = ri.world, ri.rank, ri.local
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    gdist.init("nccl")  # RCCL; used only for the barrier and the max-time reduction
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -168,7 +165,7 @@ def main():
     cfg = abi.make_config(N, max_batch=B, device=local)
     store = ObliviousStore(cfg)
     g = torch.Generator(device=dev)
-    g.manual_seed(0x6772617065 + 3 + 7919 * rank)
+    g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
     pool[:, 0] |= 1
     known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000)
@@ -179,8 +176,7 @@ def main():
     for i in range(a.warmup):
         store.process_batch_device(batches[i].data_ptr(), B, d_out.data_ptr())
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stage = {}
@@ -189,14 +185,9 @@ def main():
         for k, v in store.last_timings().items():
             stage[k] = stage.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    gdist.barrier(ri)
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
     stage_ms = {k: v / a.steps for k, v in stage.items()}
     st = store.stats()
     statuses = torch.bincount(d_out[:, 1024].to(torch.int64), minlength=9)[:9].tolist()
@@ -245,8 +236,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     store.close()
-    if world > 1:
-        dist.destroy_process_group()
+    gdist.finalize(ri)
 
 
 if __name__ == "__main__":

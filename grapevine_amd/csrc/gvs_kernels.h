@@ -809,8 +809,8 @@ __device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, 
   const uint32_t n = cnt + (dry ? 1u : 0u);
   for (uint32_t k = 0; k < n; ++k) {
     const bool isdry = dry && k == 0;
-    const uint32_t kk = isdry ? 0u : k - (dry ? 1u : 0u);
-    const uint32_t pk = r_op_at(a, stash, start, first + kk, rowbase);
+    const uint32_t kidx = isdry ? 0u : first + k - (dry ? 1u : 0u);  // dry: stash[0], in LDS
+    const uint32_t pk = r_op_at(a, stash, start, kidx, rowbase);
     const uint32_t seq = isdry ? dry_seq : (pk & kSeqMask);
     const ROp r = a.rop[seq];
     const uint4 q = a.img[(uint64_t)seq * 64 + lane];
@@ -885,7 +885,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
     const uint32_t lo = start + b * per, hi = min(end, lo + per);
     // wave 0 first runs a fake op on the shared dummy record: fixed code path
     const uint32_t i0 = wave == 0 ? lo - 4 : lo + wave;
-    for (uint32_t i = i0; i < hi || i == i0; i += 4) {
+    for (uint32_t i = i0; i < hi || (wave == 0 && i == i0); i += 4) {
       const bool isdry = wave == 0 && i == i0;
       const uint32_t seq = isdry ? a.B : ((uint32_t)a.rkeys[i] & kSeqMask);
       const ROp r = a.rop[seq];
