@@ -25,7 +25,7 @@ constexpr int kRowsMax = 4096;            // message rows per partition (S)
 constexpr int kBinsMax = 32768;           // histogram bins (Q+1, W+1) kept in LDS
 constexpr int kSrMax = 1024;              // mailbox rows per partition
 constexpr int kTile = 256;                // message rows per R-pass tile
-constexpr int kSeqBits = 20;              // B <= 2^20
+constexpr int kSeqBits = 20;              // seq <= B <= 2^19 (seq B = shared dummy record)
 constexpr uint32_t kSeqMask = (1u << kSeqBits) - 1;
 
 enum Kind : uint32_t {
@@ -215,5 +215,20 @@ __device__ inline bool nz4(uint4 a) { return (a.x | a.y | a.z | a.w) != 0u; }
 
 __device__ inline uint64_t u4lo(uint4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
 __device__ inline uint64_t u4hi(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
+
+// Pin a loaded value: the load must happen here even if the value is only
+// used on a rarely taken path (keeps full-table read passes full).
+__device__ inline void keep4(uint4& x) {
+  asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
+}
+
+// c ? x : y per component through a mask the optimiser cannot turn back into
+// an indexed access (which would move a register array to scratch)
+__device__ inline uint4 sel4(uint32_t c, uint4 x, uint4 y) {
+  uint32_t m = 0u - c;
+  asm volatile("" : "+v"(m));
+  return make_uint4((x.x & m) | (y.x & ~m), (x.y & m) | (y.y & ~m), (x.z & m) | (y.z & ~m),
+                    (x.w & m) | (y.w & ~m));
+}
 
 }  // namespace gvs

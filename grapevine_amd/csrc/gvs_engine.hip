@@ -83,7 +83,7 @@ struct gvs_handle {
   uint4* out_stage = nullptr;
   hipEvent_t ev[kMaxStages + 1] = {};
   bool timed = false;
-  int rpass_variant = 2;
+  int rpass_variant = 6;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -137,7 +137,7 @@ static int validate(const gvs_config* c) {
   if (c->mailbox_partition_slots == 0 || c->mailbox_partition_slots > (uint32_t)kSrMax ||
       (c->mailbox_partition_slots % 16) != 0)
     return GVS_ERR_INVALID_ARG;
-  if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << kSeqBits))
+  if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << (kSeqBits - 1)))
     return GVS_ERR_INVALID_ARG;
   if (c->flags != 0) return GVS_ERR_INVALID_ARG;
   for (int i = 1; i < 7; ++i)
@@ -395,6 +395,10 @@ static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_o
       case 4: hipLaunchKernelGGL((k_rpass<8, false, true, 4>), g, b, 0, s, a); break;
       case 5: hipLaunchKernelGGL((k_rpass<2, true, true, 8>), g, b, 0, s, a); break;
       case 6: hipLaunchKernelGGL((k_rpass<16, true, true, 2>), g, b, 0, s, a); break;
+      case 7: hipLaunchKernelGGL((k_rpass<32, true, true, 1>), g, b, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_rpass<16, true, true, 1>), g, b, 0, s, a); break;
+      case 9: hipLaunchKernelGGL((k_rpass<8, true, true, 2>), g, b, 0, s, a); break;
+      case 10: hipLaunchKernelGGL((k_rpass<16, false, true, 2>), g, b, 0, s, a); break;
       default: hipLaunchKernelGGL((k_rpass<8, true, true, 4>), g, b, 0, s, a); break;
     }
   }
@@ -497,7 +501,7 @@ int gvs_set_timing(gvs_handle* h, int on) {
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
-  if (std::strcmp(key, "rpass_variant") == 0 && value >= 0 && value <= 6) {
+  if (std::strcmp(key, "rpass_variant") == 0 && value >= 0 && value <= 10) {
     h->rpass_variant = (int)value;
     return GVS_OK;
   }

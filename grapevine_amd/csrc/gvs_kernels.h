@@ -298,7 +298,8 @@ __device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   if (tid == 0) *s_ng = 0;
   Key128 last = {~0ull, ~0ull};
-  for (uint32_t base = start; base < end; base += 256) {
+  // at least one (possibly empty) iteration: the same code runs in every workgroup
+  for (uint32_t base = start; base < end || base == start; base += 256) {
     const uint32_t i = base + tid;
     const bool valid = i < end;
     Key128 key = {~0ull, ~0ull};
@@ -362,17 +363,37 @@ __device__ uint32_t discover_groups(const MArgs& a, uint32_t start, uint32_t end
   return ng > (uint32_t)kGroupMax ? (uint32_t)kGroupMax + 1 : ng;
 }
 
+// Group of (hi, glo) among g[0, ng), or -1: a fixed-step lower bound (the same
+// ten steps whatever ng is; g has kGroupMax + 1 entries).
 __device__ inline int find_group(const GroupL* g, uint32_t ng, uint64_t hi, uint64_t glo) {
-  int lo = 0, hi_i = (int)ng - 1;
-  while (lo <= hi_i) {
-    int mid = (lo + hi_i) >> 1;
-    const GroupL& G = g[mid];
-    if (G.hi == hi && G.glo == glo) return mid;
-    bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
-    if (less) lo = mid + 1;
-    else hi_i = mid - 1;
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t step = kGroupMax; step > 0; step >>= 1) {
+    const uint32_t c = pos + step;
+    const GroupL& G = g[min(c - 1, (uint32_t)kGroupMax)];
+    const bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
+    pos = (c <= ng && less) ? c : pos;
   }
-  return -1;
+  const GroupL& G = g[min(pos, (uint32_t)kGroupMax)];
+  return (pos < ng && G.hi == hi && G.glo == glo) ? (int)pos : -1;
+}
+
+// Sink descriptor g[ng] that follows the real groups: every per-group loop
+// also visits it (with all of its ops masked off), so each loop body runs in
+// every workgroup, empty partitions included.
+__device__ inline void init_sink(GroupL* g, uint32_t ng, uint32_t start) {
+  if (threadIdx.x == 0) {
+    GroupL& G = g[ng];
+    G.hi = ~0ull;
+    G.glo = ~0ull;
+    G.first = start;
+    G.n_next = G.n_del = G.n_create = G.n_x = 1;
+    G.fcs = 0xFFFFFFFFu;
+    G.len = 0;
+    G.flags = 0;
+    G.slot = -1;
+    G.n_succ = G.n_delok = G.fl = 0;
+  }
 }
 
 // Phase B shared: map occupied mailbox rows of the partition to groups.
@@ -381,17 +402,14 @@ __device__ inline void side_prepass(const MArgs& a, uint32_t q, GroupL* g, uint3
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
     uint4 sd = a.side[(uint64_t)q * a.Sr + j];
     uint64_t hi = u4lo(sd), w1 = u4hi(sd);
-    int16_t sg = -1;
-    if (w1 & 1u) {
-      atomicAdd(s_occ, 1u);
-      int k = find_group(g, ng, hi, w1 >> 23);
-      if (k >= 0) {
-        g[k].slot = (int32_t)j;
-        g[k].len = (uint32_t)(w1 >> 1) & 63u;
-        sg = (int16_t)k;
-      }
+    const bool occ = (w1 & 1u) != 0;
+    const int k = occ ? find_group(g, ng, hi, w1 >> 23) : -1;
+    if (occ) atomicAdd(s_occ, 1u);
+    if (k >= 0) {
+      g[k].slot = (int32_t)j;
+      g[k].len = (uint32_t)(w1 >> 1) & 63u;
     }
-    s_sg[j] = sg;
+    s_sg[j] = (int16_t)k;
   }
 }
 
@@ -417,13 +435,12 @@ __device__ inline void m1_write_wave(const MArgs& a, bool valid, uint32_t seq, u
 
 // Resolve the next-message ops (class 0) of group G against its mailbox row v
 // (lane 2+k holds id k): the op that has d delete-nexts before it reads id d.
-// Not inlined, and run once per workgroup in "dry" mode (one fake op writing
-// the shared dummy record `dry_seq` = B), so every workgroup fetches
-// this code whatever the batch holds: instruction fetch then does not depend
-// on the request mix.
-__device__ __attribute__((noinline)) void m1_resolve_next(const MArgs& a, const GroupL& G,
-                                                          uint4 v, const uint32_t* stash,
-                                                          uint32_t start, uint32_t dry_seq) {
+// It has a single call site, which every workgroup also runs once in "dry"
+// mode (one fake op writing the shared dummy record `dry_seq` = B), so the
+// code executed does not depend on the request mix.
+__device__ __forceinline__ void m1_resolve_next(const MArgs& a, const GroupL& G, uint4 v,
+                                                const uint32_t* stash, uint32_t start,
+                                                uint32_t dry_seq) {
   const uint32_t lane = lane_id();
   const bool dry = dry_seq != kNone;
   const uint32_t len = dry ? 62u : G.len;
@@ -472,17 +489,13 @@ __device__ void dummy_partition(const MArgs& a, uint32_t b) {
 }
 
 __global__ __launch_bounds__(256) void k_m1(MArgs a) {
-  __shared__ GroupL g[kGroupMax];
+  __shared__ GroupL g[kGroupMax + 1];
   __shared__ uint32_t stash[kStash];
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t q = blockIdx.x;
-  if (wave == 0) {  // fixed instruction footprint, see m1_resolve_next
-    GroupL fake = {};
-    m1_resolve_next(a, fake, make_uint4(0, 0, 0, 0), stash, 0u, a.B);
-  }
   if (q >= a.Q) {
     dummy_partition<false>(a, q - a.Q);
     return;
@@ -497,40 +510,58 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
     s_occ = 0;
     s_empt = 0;
   }
+  init_sink(g, ng, start);
   __syncthreads();
   side_prepass(a, q, g, ng, s_sg, &s_occ);
   __syncthreads();
 
-  // Phase C: stream every mailbox row of the partition (read-only pass).
+  // Phase C: stream every mailbox row of the partition (read-only pass).  Rows
+  // owned by a group go one at a time (branch-free select) through the single
+  // copy of m1_resolve_next; wave 0's first chunk also runs it once dry.
   const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
   for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
     uint4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
-#pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int k = s_sg[j0 + u];
-      if (k >= 0) m1_resolve_next(a, g[k], v[u], stash, start, kNone);
+      v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
+      keep4(v[u]);  // every row is read, used or not
+    }
+    uint32_t mm = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) mm |= s_sg[j0 + u] >= 0 ? (1u << u) : 0u;
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    bool dry = j0 == 0;
+    while (mm || dry) {
+      const uint32_t bit = dry ? 1u : (mm & (0u - mm));
+      if (!dry) mm &= mm - 1u;
+      uint4 cur = v[0];
+#pragma unroll
+      for (int uu = 1; uu < 4; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      const int k = s_sg[j0 + (uint32_t)__builtin_ctz(bit)];
+      m1_resolve_next(a, g[(!dry && k >= 0) ? (uint32_t)k : ng], cur, stash, start,
+                      dry ? a.B : kNone);
+      dry = false;
     }
   }
   __syncthreads();
 
   // Phase D: free rows after pops, admission of new recipients by the seq of
-  // their first create (grapevine.proto:74 TOO_MANY_RECIPIENTS).
-  for (uint32_t k = tid; k < ng; k += 256) {
+  // their first create (grapevine.proto:74 TOO_MANY_RECIPIENTS).  Loops run
+  // over the sink g[ng] too (see init_sink).
+  for (uint32_t k = tid; k <= ng; k += 256) {
     const GroupL& G = g[k];
     if (G.slot >= 0 && G.len == min(G.n_del, G.len)) atomicAdd(&s_empt, 1u);
   }
   __syncthreads();
   const uint32_t freeq = (a.Sr - s_occ) + s_empt;
-  for (uint32_t k = tid; k < ng; k += 256) {
+  for (uint32_t k = tid; k <= ng; k += 256) {
     GroupL& G = g[k];
     const uint32_t len1 = G.slot >= 0 ? G.len - min(G.n_del, G.len) : 0u;
     const bool exists1 = len1 > 0;
     const bool isnew = !exists1 && G.n_create > 0;
     uint32_t rank = 0;
     if (isnew) {
-      for (uint32_t k2 = 0; k2 < ng; ++k2) {
+      for (uint32_t k2 = 0; k2 <= ng; ++k2) {
         const GroupL& H = g[k2];
         const uint32_t hl = H.slot >= 0 ? H.len - min(H.n_del, H.len) : 0u;
         if (hl == 0 && H.n_create > 0 && H.fcs < G.fcs) ++rank;
@@ -542,12 +573,13 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __syncthreads();
 
   // Phase E: creates get their mailbox verdict; every remaining op is visited once.
-  for (uint32_t k = wave; k < ng; k += 4) {
+  for (uint32_t k = wave; k <= ng; k += 4) {
     const GroupL& G = g[k];
+    const bool real = k < ng;  // the sink's ops are all masked off
     const uint4 z = make_uint4(0, 0, 0, 0);
     if (G.slot < 0) {
       for (uint32_t c = 0; c < G.n_next; c += 64) {
-        const bool valid = c + lane < G.n_next;
+        const bool valid = real && c + lane < G.n_next;
         const uint32_t p = valid ? op_info<false>(a, stash, start, G.first + c + lane) : 0u;
         m1_write_wave(a, valid, pk_seq(p), 2u, kNone, 0u, z);
       }
@@ -555,14 +587,14 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
     const bool exists1 = G.flags & 1u, admitted = G.flags & 2u;
     for (uint32_t c = 0; c < G.n_create; c += 64) {
       const uint32_t r = c + lane;
-      const bool valid = r < G.n_create;
+      const bool valid = real && r < G.n_create;
       const uint32_t p = valid ? op_info<false>(a, stash, start, G.first + G.n_next + r) : 0u;
       const bool ok = exists1 ? (G.fl + r < GVS_MAILBOX_SLOTS) : (admitted && r < GVS_MAILBOX_SLOTS);
       const uint32_t st = ok ? kPending : ((exists1 || admitted) ? 5u : 6u);
       m1_write_wave(a, valid, pk_seq(p), st, kNone, ok ? CF_MBOX_OK : 0u, z);
     }
     for (uint32_t c = 0; c < G.n_x; c += 64) {
-      const bool valid = c + lane < G.n_x;
+      const bool valid = real && c + lane < G.n_x;
       const uint32_t p =
           valid ? op_info<false>(a, stash, start, G.first + G.n_next + G.n_create + c + lane) : 0u;
       m1_write_wave(a, valid, pk_seq(p), kPending, kNone, 0u, z);
@@ -935,12 +967,28 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
+      // rows of this chunk that have ops (wave-uniform); wave 0's first chunk
+      // also runs the dry op, so the single copy of the apply code below is
+      // executed by every workgroup whatever the batch holds (see r_apply)
+      const bool dry = (t == 0 && j == 0 && wave == 0);
+      uint32_t mm = dry ? 1u : 0u;
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) mm |= s_cnt[wave * 64 + j + u] ? (1u << u) : 0u;
+      mm = __builtin_amdgcn_readfirstlane(mm);
+      bool first_dry = dry;
+      while (mm) {
+        const uint32_t u = (uint32_t)__builtin_ctz(mm);
+        const uint32_t bit = mm & (0u - mm);
+        mm &= mm - 1u;
+        // branch-free select of row u (keeps v[] in registers)
+        uint4 cur = v[0];
+#pragma unroll
+        for (int uu = 1; uu < U; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
         const uint32_t o = wave * 64 + j + u;
-        const uint32_t c = s_cnt[o];
-        const bool dry = (t == 0 && j == 0 && wave == 0);  // see r_apply
-        if (c || dry) r_apply(a, v[u], stash, start, rowbase, s_first[o], c, dry, a.B);
+        r_apply(a, cur, stash, start, rowbase, s_first[o], s_cnt[o], first_dry, a.B);
+        first_dry = false;
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
@@ -1020,14 +1068,17 @@ __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
 // successful creates (a prefix of the class-1 members), remove ids of
 // successful by-id deletes, clear the row if it ends empty.  Each member's
 // ROp is read exactly once here.
-__device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched,
-                         const uint32_t* stash, uint32_t start) {
+// With `dry` (G = the sink), one fake member of each class reads the shared
+// dummy record B instead and the caller discards v: every workgroup runs the
+// single copy of this code once whatever the batch holds.
+__device__ __forceinline__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched,
+                                         const uint32_t* stash, uint32_t start, bool dry) {
   const uint32_t lane = lane_id();
   const uint32_t len = matched ? G.len : 0u;
   const uint32_t dp = min(G.n_del, len);
   for (uint32_t c = 0; c < G.n_next; c += 64) {  // visit pops (state needs only the count)
     if (c + lane < G.n_next) {
-      const uint32_t p = op_info<true>(a, stash, start, G.first + c + lane);
+      const uint32_t p = dry ? a.B : op_info<true>(a, stash, start, G.first + c + lane);
       const ROp r = a.rop[pk_seq(p)];
       asm volatile("" ::"v"(r.id[0]), "v"(r.x[0]));
     }
@@ -1043,7 +1094,7 @@ __device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched
     ROp r = {};
     uint32_t p = 0;
     if (valid) {
-      p = op_info<true>(a, stash, start, G.first + G.n_next + c + lane);
+      p = dry ? a.B : op_info<true>(a, stash, start, G.first + G.n_next + c + lane);
       r = a.rop[pk_seq(p)];
     }
     const uint64_t ms = __ballot(valid && pk_succ(p));
@@ -1065,7 +1116,7 @@ __device__ void m2_apply(const MArgs& a, const GroupL& G, uint4& v, bool matched
     ROp r = {};
     uint32_t p = 0;
     if (valid) {
-      p = op_info<true>(a, stash, start, G.first + G.n_next + G.n_create + c + lane);
+      p = dry ? a.B : op_info<true>(a, stash, start, G.first + G.n_next + G.n_create + c + lane);
       r = a.rop[pk_seq(p)];
     }
     uint64_t md = __ballot(valid && pk_succ(p));
@@ -1092,7 +1143,7 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
                                        uint32_t* s_w) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < n; base += 256) {
+  for (uint32_t base = 0; base < n || base == 0; base += 256) {  // runs even for n = 0
     const uint32_t i = base + tid;
     const bool f = i < n && flag[i];
     const uint64_t m = __ballot(f);
@@ -1112,7 +1163,7 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
 }
 
 __global__ __launch_bounds__(256) void k_m2(MArgs a) {
-  __shared__ GroupL g[kGroupMax];
+  __shared__ GroupL g[kGroupMax + 1];
   __shared__ uint32_t stash[kStash];
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
@@ -1120,7 +1171,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __shared__ uint8_t s_flag[kSrMax];
   __shared__ uint16_t s_pfx[kSrMax + 1];
   __shared__ uint16_t s_gpfx[kGroupMax + 1];
-  __shared__ uint8_t s_gflag[kGroupMax];
+  __shared__ uint8_t s_gflag[kGroupMax + 1];
   __shared__ int16_t s_pend[kGroupMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -1137,11 +1188,13 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
     s_occ = 0;
     s_delta = 0;
   }
+  init_sink(g, ng, start);
   __syncthreads();
   side_prepass(a, q, g, ng, s_sg, &s_occ);
   __syncthreads();
-  // final lengths; pending = groups with no row that end non-empty
-  for (uint32_t k = tid; k < ng; k += 256) {
+  // final lengths; pending = groups with no row that end non-empty (the sink
+  // g[ng] gets fl = 0, flag 0)
+  for (uint32_t k = tid; k <= ng; k += 256) {
     GroupL& G = g[k];
     const uint32_t len = G.slot >= 0 ? G.len : 0u;
     const uint32_t dp = min(G.n_del, len);
@@ -1158,8 +1211,8 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __syncthreads();
   block_flag_scan(s_flag, a.Sr, s_pfx, s_w);
   block_flag_scan(s_gflag, ng, s_gpfx, s_w);
-  for (uint32_t k = tid; k < ng; k += 256)
-    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  for (uint32_t k = tid; k <= ng; k += 256)
+    if (k < ng && s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
   __syncthreads();
   const uint32_t npend = s_gpfx[ng];
   if (tid == 0 && npend > s_pfx[a.Sr]) atomicOr(&a.scal->error, 2u);
@@ -1173,43 +1226,68 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   if (tid == 0) atomicAdd(&s_delta, npend);
   __syncthreads();
 
-  // Phase C: rewrite every row of the partition exactly once.
+  // Phase C: rewrite every row of the partition exactly once.  Rows with work
+  // go one at a time (branch-free select) through the single copy of
+  // m2_apply; wave 0's first chunk also runs it once dry on the sink.
   uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4* side = a.side + (uint64_t)q * a.Sr;
   for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
+    uint4 v[4], sd[4];
+    uint32_t mm = 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint32_t j = j0 + u;
-      const int k = s_sg[j], p = s_place[j];
-      uint4 sd = a.side[(uint64_t)q * a.Sr + j];
-      if (k >= 0) m2_apply(a, g[k], v[u], true, stash, start);
-      if (p >= 0) {  // a new mailbox takes a row that is (or became) empty
-        v[u] = make_uint4(0, 0, 0, 0);
-        m2_apply(a, g[p], v[u], false, stash, start);
+      v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
+      sd[u] = side[j0 + u];
+      mm |= (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0) ? (1u << u) : 0u;
+    }
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    bool dry = j0 == 0;
+    while (mm || dry) {
+      const uint32_t bit = dry ? 1u : (mm & (0u - mm));
+      if (!dry) mm &= mm - 1u;
+      uint4 cur = v[0];
+#pragma unroll
+      for (int uu = 1; uu < 4; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      const uint32_t j = j0 + (uint32_t)__builtin_ctz(bit);
+      const int k = dry ? -1 : s_sg[j], p = dry ? -1 : s_place[j];
+      // pass 0: the row's own group; pass 1: a new mailbox placed in the row
+      // (one that is, or became, empty)
+#pragma unroll 1
+      for (uint32_t pass = 0; pass < 2; ++pass) {
+        const int gi = pass == 0 ? k : p;
+        if (gi < 0 && !(dry && pass == 0)) continue;
+        if (pass == 1) cur = make_uint4(0, 0, 0, 0);
+        m2_apply(a, g[gi >= 0 ? (uint32_t)gi : ng], cur, pass == 0 && !dry, stash, start, dry);
       }
-      if (k >= 0 || p >= 0) {
-        const GroupL& G = g[p >= 0 ? p : k];
-        if (G.fl > 0) {
-          const uint64_t w1 = (G.glo << 23) | ((uint64_t)G.fl << 1) | 1ull;
-          sd = make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
-                          (uint32_t)(w1 >> 32));
-        } else {
-          sd = make_uint4(0, 0, 0, 0);
+      const GroupL& G = g[p >= 0 ? (uint32_t)p : (k >= 0 ? (uint32_t)k : ng)];
+      const uint64_t w1 = (G.glo << 23) | ((uint64_t)G.fl << 1) | 1ull;
+      const uint4 nsd = G.fl > 0 ? make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                                              (uint32_t)(w1 >> 32))
+                                 : make_uint4(0, 0, 0, 0);
+      if (!dry) {
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) {
+          v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
+          sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
         }
       }
-      part[(uint64_t)j * 64 + lane] = v[u];
-      if (lane == 0) a.side[(uint64_t)q * a.Sr + j] = sd;
+      dry = false;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      part[(uint64_t)(j0 + u) * 64 + lane] = v[u];
+      if (lane == 0) side[j0 + u] = sd[u];
     }
   }
-  // Phase D: members of groups that own no row (misses, failed creates) are visited too.
-  for (uint32_t k = wave; k < ng; k += 4) {
+  // Phase D: members of groups that own no row (misses, failed creates) are
+  // visited too; the sink's three fake members read the dummy record B.
+  for (uint32_t k = wave; k <= ng; k += 4) {
     const GroupL& G = g[k];
-    if (G.slot >= 0 || s_gflag[k]) continue;
+    const bool real = k < ng;
+    if (real && (G.slot >= 0 || s_gflag[k])) continue;
     const uint32_t cnt = G.n_next + G.n_create + G.n_x;
     for (uint32_t c = lane; c < cnt; c += 64) {
-      const uint32_t p = op_info<true>(a, stash, start, G.first + c);
+      const uint32_t p = real ? op_info<true>(a, stash, start, G.first + c) : a.B;
       const ROp r = a.rop[pk_seq(p)];
       asm volatile("" ::"v"(r.id[0]), "v"(r.x[0]));
     }

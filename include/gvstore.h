@@ -121,7 +121,7 @@ typedef struct gvs_config {
   uint64_t msg_capacity;        /* N message slots; power of two, >= 256 */
   uint32_t mailbox_partitions;  /* Q; power of two */
   uint32_t mailbox_partition_slots; /* S_r mailboxes per partition; R = Q*S_r */
-  uint32_t max_batch;           /* B; power of two, 256 .. 2^20 */
+  uint32_t max_batch;           /* B; power of two, 1024 .. 2^19 */
   uint32_t device;              /* HIP device ordinal */
   uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key */
   uint32_t flags;               /* reserved, must be 0 */
@@ -174,7 +174,7 @@ int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
 int gvs_synchronize(gvs_handle *h);
 
 /* Tuning knobs (engine-internal choices that never change results):
- * "rpass_variant" 0..6 selects the message-pass kernel instantiation
+ * "rpass_variant" 0..10 selects the message-pass kernel instantiation
  * (rows in flight per wave, non-temporal loads/stores). */
 int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 

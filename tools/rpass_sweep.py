@@ -14,10 +14,32 @@ def main():
     from grapevine_amd import abi
     from grapevine_amd.store import ObliviousStore
     log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
-    variants = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(7))
+    variants = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(11))
     rows = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
+    copy_reference(torch)
     for S in rows:
         run(torch, abi, ObliviousStore, log2n, variants, S)
+
+
+def copy_reference(torch):
+    """Device-to-device copy of 8 GiB: the read+write streaming rate this box
+    reaches with a library kernel (ceiling reference for the table pass)."""
+    dev = torch.device("cuda", 0)
+    a = torch.empty(1 << 33, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    ts = []
+    for _ in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts[1:])[len(ts[1:]) // 2]
+    print(f"d2d copy 8 GiB: {ms:.3f} ms  {2 * (1 << 33) / ms / 1e6:.0f} GB/s (read+write)", flush=True)
+    del a, b
+    torch.cuda.empty_cache()
 
 
 def run(torch, abi, ObliviousStore, log2n, variants, S):
