@@ -243,6 +243,39 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
 
 // ------------------------------------------------------ mailbox passes M1/M2
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ inline uint4 ld_row(const uint4* p) {
+  if (NT) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+template <bool NT>
+__device__ inline void st_row(uint4* p, uint4 x) {
+  if (NT) {
+    v4u v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+  } else {
+    *p = x;
+  }
+}
+
+constexpr int kMU = 8;  // mailbox rows per wave and chunk in the M1/M2 row passes
+
+// One chunk of kMU rows (16 B per lane each), loads issued back to back
+// without branches; a chunk that runs past Sr (Sr not a multiple of 4 kMU)
+// re-reads the last row for the missing ones, a fixed per-config footprint.
+__device__ inline void load_rows(uint4 (&v)[kMU], const uint4* part, uint32_t j0, uint32_t Sr) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int u = 0; u < kMU; ++u)
+    v[u] = ld_row<true>(&part[(uint64_t)min(j0 + u, Sr - 1u) * 64 + lane]);
+}
+
+
 struct GroupL {  // 64 B LDS descriptor of one recipient group
   uint64_t hi, glo;
   uint32_t first, n_next, n_del, n_create;
@@ -494,12 +527,17 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar branches
   const uint32_t q = blockIdx.x;
   if (q >= a.Q) {
     dummy_partition<false>(a, q - a.Q);
     return;
   }
+  // the wave's first chunk of rows is in flight during the group discovery
+  const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4 va[kMU], vb[kMU];
+  load_rows(va, part, wave * kMU, a.Sr);
   const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
   const uint32_t ng = discover_groups<false>(a, start, end, g, stash, s_key, s_w, &s_ng);
   if (ng > (uint32_t)kGroupMax) {
@@ -517,18 +555,18 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
 
   // Phase C: stream every mailbox row of the partition (read-only pass).  Rows
   // owned by a group go one at a time (branch-free select) through the single
-  // copy of m1_resolve_next; wave 0's first chunk also runs it once dry.
-  const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
-  for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
-      keep4(v[u]);  // every row is read, used or not
-    }
+  // copy of m1_resolve_next; wave 0's first chunk also runs it once dry.  The
+  // next chunk is loaded while the current one is worked on.
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+    if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
+    uint4 v[kMU];
     uint32_t mm = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) mm |= s_sg[j0 + u] >= 0 ? (1u << u) : 0u;
+    for (int u = 0; u < kMU; ++u) {
+      v[u] = va[u];
+      keep4(v[u]);  // every row is read, used or not
+      mm |= (j0 + u < a.Sr && s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
+    }
     mm = __builtin_amdgcn_readfirstlane(mm);
     bool dry = j0 == 0;
     while (mm || dry) {
@@ -536,12 +574,14 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
       if (!dry) mm &= mm - 1u;
       uint4 cur = v[0];
 #pragma unroll
-      for (int uu = 1; uu < 4; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
       const int k = s_sg[j0 + (uint32_t)__builtin_ctz(bit)];
       m1_resolve_next(a, g[(!dry && k >= 0) ? (uint32_t)k : ng], cur, stash, start,
                       dry ? a.B : kNone);
       dry = false;
     }
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) va[u] = vb[u];
   }
   __syncthreads();
 
@@ -881,26 +921,6 @@ __device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, 
   }
 }
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-
-template <bool NT>
-__device__ inline uint4 ld_row(const uint4* p) {
-  if (NT) {
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return *p;
-}
-template <bool NT>
-__device__ inline void st_row(uint4* p, uint4 x) {
-  if (NT) {
-    v4u v = {x.x, x.y, x.z, x.w};
-    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
-  } else {
-    *p = x;
-  }
-}
-
 template <int U, bool NTL, bool NTS, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t stash[kStash];
@@ -1174,13 +1194,19 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __shared__ uint8_t s_gflag[kGroupMax + 1];
   __shared__ int16_t s_pend[kGroupMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar branches
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   if (q >= a.Q) {
     dummy_partition<true>(a, q - a.Q);
     return;
   }
+  // the wave's first chunk of rows is in flight during the group discovery
+  uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4* side = a.side + (uint64_t)q * a.Sr;
+  uint4 va[kMU], vb[kMU];
+  load_rows(va, part, wave * kMU, a.Sr);
   const uint32_t start = a.qstart[q], end = a.qstart[q + 1];
   const uint32_t ng = discover_groups<true>(a, start, end, g, stash, s_key, s_w, &s_ng);
   if (ng > (uint32_t)kGroupMax) return;  // M1 already flagged the batch
@@ -1228,17 +1254,18 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
 
   // Phase C: rewrite every row of the partition exactly once.  Rows with work
   // go one at a time (branch-free select) through the single copy of
-  // m2_apply; wave 0's first chunk also runs it once dry on the sink.
-  uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
-  uint4* side = a.side + (uint64_t)q * a.Sr;
-  for (uint32_t j0 = wave * 4; j0 < a.Sr; j0 += 16) {
-    uint4 v[4], sd[4];
+  // m2_apply; wave 0's first chunk also runs it once dry on the sink.  The
+  // next chunk is loaded while the current one is worked on.
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+    if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
+    uint4 v[kMU], sd[kMU];
     uint32_t mm = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v[u] = part[(uint64_t)(j0 + u) * 64 + lane];
-      sd[u] = side[j0 + u];
-      mm |= (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0) ? (1u << u) : 0u;
+    for (int u = 0; u < kMU; ++u) {
+      const bool in = j0 + u < a.Sr;  // wave-uniform
+      v[u] = va[u];
+      sd[u] = in ? side[j0 + u] : make_uint4(0, 0, 0, 0);
+      mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
     }
     mm = __builtin_amdgcn_readfirstlane(mm);
     bool dry = j0 == 0;
@@ -1247,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
       if (!dry) mm &= mm - 1u;
       uint4 cur = v[0];
 #pragma unroll
-      for (int uu = 1; uu < 4; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
       const uint32_t j = j0 + (uint32_t)__builtin_ctz(bit);
       const int k = dry ? -1 : s_sg[j], p = dry ? -1 : s_place[j];
       // pass 0: the row's own group; pass 1: a new mailbox placed in the row
@@ -1266,7 +1293,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
                                  : make_uint4(0, 0, 0, 0);
       if (!dry) {
 #pragma unroll
-        for (int uu = 0; uu < 4; ++uu) {
+        for (int uu = 0; uu < kMU; ++uu) {
           v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
           sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
         }
@@ -1274,9 +1301,12 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
       dry = false;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      part[(uint64_t)(j0 + u) * 64 + lane] = v[u];
-      if (lane == 0) side[j0 + u] = sd[u];
+    for (int u = 0; u < kMU; ++u) {
+      if (j0 + u < a.Sr) {
+        st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
+        if (lane == 0) side[j0 + u] = sd[u];
+      }
+      va[u] = vb[u];
     }
   }
   // Phase D: members of groups that own no row (misses, failed creates) are

@@ -28,8 +28,9 @@ WORKER = textwrap.dedent("""
     el = gdist.max_over_ranks(ri, time.perf_counter() - t0 + 0.01 * ri.rank)
     total = gdist.sum_over_ranks(ri, 3 * 512)
     oks = gdist.sum_over_ranks(ri, ok)
-    print(json.dumps(dict(rank=ri.rank, world=ri.world, elapsed=el, total=total, oks=oks,
-                          digest=shard.digest(), local_ok=ok)))
+    with open(os.path.join({out!r}, "rank%d.json" % ri.rank), "w") as f:
+        json.dump(dict(rank=ri.rank, world=ri.world, elapsed=el, total=total, oks=oks,
+                       digest=shard.digest(), local_ok=ok), f)
     gdist.finalize(ri)
 """)
 
@@ -44,14 +45,18 @@ def free_port():
 
 def test_two_rank_shards_gloo(tmp_path):
     script = tmp_path / "worker.py"
-    script.write_text(WORKER.format(root=ROOT))
-    port = free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    script.write_text(WORKER.format(root=ROOT, out=str(tmp_path)))
+    for attempt in range(3):  # a free port can be taken between probe and bind
+        port = free_port()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+        busy = "address already in use" in (r.stdout + r.stderr).lower() or "EADDRINUSE" in r.stderr
+        if r.returncode == 0 or not busy:
+            break
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     import json
-    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    rows = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(2)]
     assert sorted(x["rank"] for x in rows) == [0, 1]
     a, b = rows
     assert a["world"] == b["world"] == 2
