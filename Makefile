@@ -5,12 +5,12 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 
 LIB := grapevine_amd/libgvstore.so
 SRCS := grapevine_amd/csrc/gvs_engine.hip
-HDRS := grapevine_amd/csrc/gvs_kernels.h grapevine_amd/csrc/gvs_device.h include/gvstore.h
+HDRS := grapevine_amd/csrc/gvs_kernels.h grapevine_amd/csrc/gvs_device.h grapevine_amd/csrc/gvs_route.h include/gvstore.h
 
 all: $(LIB) oracle
 
 $(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
 
 oracle:
 	$(MAKE) -C oracle

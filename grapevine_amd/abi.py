@@ -74,20 +74,32 @@ class GvsConfig(ctypes.Structure):
         ("device", ctypes.c_uint32),
         ("secret_key", ctypes.c_uint8 * 32),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 7),
+        ("rows_per_partition", ctypes.c_uint32),
+        ("shard_count", ctypes.c_uint32),
+        ("shard_index", ctypes.c_uint32),
+        ("route_capacity", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 3),
     ]
 
 
 class GvsStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "messages", "mailboxes", "batches", "creation_counter", "free_ring_head",
-        "free_ring_tail", "msg_partitions", "msg_partition_slots")]
+        "free_ring_tail", "msg_partitions", "msg_partition_slots", "shards", "route_capacity",
+        "shard_batch")]
+
+COMM_ID_BYTES = 128
 
 
 def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,
-                max_batch=None, device=0, secret_key=None):
-    """Config mirroring gvs_config_init's defaults (R = N/16 mailboxes)."""
+                max_batch=None, device=0, secret_key=None, shard_count=0, shard_index=0,
+                route_capacity=0, rows_per_partition=0):
+    """Config mirroring gvs_config_init's defaults (R = N/16 mailboxes per shard)."""
     cfg = GvsConfig()
+    cfg.shard_count = shard_count
+    cfg.shard_index = shard_index
+    cfg.route_capacity = route_capacity
+    cfg.rows_per_partition = rows_per_partition
     cfg.msg_capacity = msg_capacity
     if mailbox_partitions is None:
         r = max(msg_capacity // 16, 256)

@@ -92,7 +92,12 @@ struct Scal {  // persistent device scalars + per-batch temporaries
 
 struct KeyCtx {
   uint64_t pk0, pk1, hk0, hk1;
+  uint32_t tag;     // id plaintext tag of this shard: kIdTag ^ shard << 8
+  uint32_t nshards; // S (1 when unsharded)
 };
+
+// Plaintext tag of the ids a shard issues (shard < 2^16; shard 0 = kIdTag).
+__host__ __device__ inline uint32_t shard_tag(uint32_t shard) { return kIdTag ^ (shard << 8); }
 
 // ------------------------------------------------------------- SipHash-2-4
 
@@ -141,10 +146,10 @@ __host__ __device__ inline uint64_t feistel_f(const KeyCtx& k, int r, uint64_t x
   return siphash24_blocks(k.pk0, k.pk1, m, 2, 0, 16);
 }
 
-// id = PRP(slot | TAG<<32, ctr); bytes [0:8) = L, [8:16) = R little-endian
+// id = PRP(slot | tag<<32, ctr); bytes [0:8) = L, [8:16) = R little-endian
 __host__ __device__ inline void id_encode(const KeyCtx& k, uint32_t slot, uint64_t ctr,
                                           uint64_t& L, uint64_t& R) {
-  L = (uint64_t)slot | ((uint64_t)kIdTag << 32);
+  L = (uint64_t)slot | ((uint64_t)k.tag << 32);
   R = ctr;
   for (int r = 0; r < 4; ++r) {
     uint64_t nl = R, nr = L ^ feistel_f(k, r, R);
@@ -153,17 +158,34 @@ __host__ __device__ inline void id_encode(const KeyCtx& k, uint32_t slot, uint64
   }
 }
 
-// returns the slot, or kNone when the id does not decode to a valid slot
-__host__ __device__ inline uint32_t id_decode(const KeyCtx& k, uint64_t L, uint64_t R,
-                                              uint64_t n_slots) {
+__host__ __device__ inline uint64_t id_plain_lo(const KeyCtx& k, uint64_t L, uint64_t R) {
   for (int r = 3; r >= 0; --r) {
     uint64_t nl = R ^ feistel_f(k, r, L), nr = L;
     L = nl;
     R = nr;
   }
-  if ((uint32_t)(L >> 32) != kIdTag) return kNone;
+  return L;
+}
+
+// returns the slot, or kNone when the id does not decode to a valid slot of
+// this shard
+__host__ __device__ inline uint32_t id_decode(const KeyCtx& k, uint64_t L, uint64_t R,
+                                              uint64_t n_slots) {
+  L = id_plain_lo(k, L, R);
+  if ((uint32_t)(L >> 32) != k.tag) return kNone;
   if ((uint64_t)(uint32_t)L >= n_slots) return kNone;
   return (uint32_t)L;
+}
+
+// shard that issued the id, or kNone when it decodes to no valid (shard, slot)
+__host__ __device__ inline uint32_t id_shard(const KeyCtx& k, uint64_t L, uint64_t R,
+                                             uint64_t n_slots) {
+  L = id_plain_lo(k, L, R);
+  const uint32_t t = (uint32_t)(L >> 32) ^ kIdTag;
+  if ((t & 0xFF0000FFu) != 0u) return kNone;
+  const uint32_t s = t >> 8;
+  if (s >= k.nshards || (uint64_t)(uint32_t)L >= n_slots) return kNone;
+  return s;
 }
 
 // recipient PRF over the 32-byte key given as 4 little-endian words
@@ -171,6 +193,13 @@ __host__ __device__ inline void recipient_hash(const KeyCtx& k, const uint64_t x
                                                uint64_t& hi, uint64_t& lo) {
   hi = siphash24_blocks(k.hk0, k.hk1, x, 4, 1, 33);
   lo = siphash24_blocks(k.hk0, k.hk1, x, 4, 2, 33);
+}
+
+// shard owning the mailbox of recipient key x (and every message addressed to
+// it): low 16 bits of h_lo, which neither the mailbox partition (top bits of
+// h_hi) nor the group key (h_lo >> 23) uses
+__host__ __device__ inline uint32_t shard_of_hash(uint64_t h_lo, uint32_t nshards) {
+  return (uint32_t)(h_lo & 0xFFFFu) % nshards;
 }
 
 // S1 (mailbox) sort key: hi = h_hi; lo = h_lo[63:23] | class<<21 | seq<<1 | sub

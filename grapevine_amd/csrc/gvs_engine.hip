@@ -1,7 +1,18 @@
 // gvs_engine.hip — host side of libgvstore.so: the C ABI of include/gvstore.h
-// driving the gfx950 kernels of gvs_kernels.h on one HIP stream.
+// driving the gfx950 kernels of gvs_kernels.h / gvs_route.h on one HIP stream.
+//
+// A handle owns one or more shard engines (Engine: the tables and per-batch
+// scratch of one shard) and, when sharded, the router buffers
+// of DESIGN.md §6.  Three modes:
+//   kSingle  one shard, no routing (gvs_create with shard_count <= 1)
+//   kLocal   S shards on one device in this process; the all-to-all is a set
+//            of device copies (gvs_create with shard_count > 1; tests)
+//   kRccl    one shard per process; the all-to-all is RCCL send/recv over
+//            xGMI, error words are max-reduced over ranks (gvs_create_sharded)
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -11,22 +22,23 @@
 
 #include "../../include/gvstore.h"
 #include "gvs_kernels.h"
+#include "gvs_route.h"
 
 using namespace gvs;
 
 static_assert(sizeof(gvs_record) == 1024, "record layout");
 static_assert(sizeof(gvs_request) == 1040, "request layout");
 static_assert(sizeof(gvs_response) == 1040, "response layout");
+static_assert(sizeof(ncclUniqueId) == GVS_COMM_ID_BYTES, "comm id size");
 
 namespace {
 
 constexpr int kNullBlocks = 32;   // R-pass blocks for ops that touch no row
 constexpr int kDummyBlocks = 32;  // M-pass blocks for ops that touch no mailbox
-constexpr int kMaxStages = 16;
+constexpr int kMaxMarks = 24;
+constexpr uint64_t kExtra = 64;   // per-op records after the B real ones (record B = dry dummy)
 
-const char* kStageNames[] = {"copy", "meta", "sort_s1", "m1", "alloc", "sort_r",
-                             "rpass", "post", "m2"};
-constexpr int kNumStages = 9;
+enum Mode { kSingle, kLocal, kRccl };
 
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 uint32_t log2u(uint64_t v) {
@@ -40,24 +52,17 @@ uint64_t ld64(const uint8_t* p) {
   return v;
 }
 
-}  // namespace
-
-struct gvs_handle {
-  gvs_config cfg{};
-  int device = 0;
-  hipStream_t stream = nullptr;
+// One shard: persistent tables + per-batch scratch for a batch of B ops.
+struct Engine {
+  uint32_t shard = 0;
   uint64_t N = 0, R = 0, ring_size = 0;
-  uint32_t Q = 0, Sr = 0, B = 0, W = 0, S = 0, NT = 0, logQ = 0;
+  uint32_t Q = 0, Sr = 0, B = 0, W = 0, S = 0, logQ = 0, nblk = 0;
   KeyCtx kc{};
-  // persistent state
   uint4* table = nullptr;
   uint4* mbox = nullptr;
   uint4* side = nullptr;
   uint32_t* ring = nullptr;
   Scal* scal = nullptr;
-  // per-batch scratch
-  uint32_t nblk = 0;
-  uint64_t extra = 0;
   uint4* img = nullptr;
   uint32_t* types = nullptr;
   OpState* ops = nullptr;
@@ -75,13 +80,42 @@ struct gvs_handle {
   uint32_t* pcount = nullptr;
   uint32_t* pstart = nullptr;
   RRes* rres = nullptr;
-  uint4* resp = nullptr;
+  uint4* resp = nullptr;     // (B + extra) internal response slots of kRespSlot bytes
   uint32_t* dflag = nullptr;
   uint32_t* dslot = nullptr;
   uint32_t* bsum2 = nullptr;
-  uint4* in_stage = nullptr;
+  uint4* recv = nullptr;     // routed modes: S*C incoming request slots
+};
+
+// Router state of one source rank (kLocal: one per virtual rank).
+struct Router {
+  uint32_t* dest = nullptr;
+  uint32_t* bcnt = nullptr;
+  uint32_t* pos = nullptr;
+  uint32_t* tot = nullptr;
+  uint4* send = nullptr;     // S*C outgoing request slots
+  uint4* back = nullptr;     // S*C returning response slots
+};
+
+}  // namespace
+
+struct gvs_handle {
+  gvs_config cfg{};
+  Mode mode = kSingle;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t S = 1;       // shards in the store
+  uint32_t C = 0;       // routed slots per (source, shard)
+  uint32_t Bsub = 0;    // requests per source per call (cfg.max_batch)
+  uint32_t Be = 0;      // ops per shard pipeline (Bsub, or next pow2 >= S*C)
+  std::vector<Engine> eng;
+  std::vector<Router> rt;
+  ncclComm_t comm = nullptr;
+  uint4* in_stage = nullptr;   // host API staging (caller layout)
   uint4* out_stage = nullptr;
-  hipEvent_t ev[kMaxStages + 1] = {};
+  hipEvent_t ev[kMaxMarks] = {};
+  const char* mark_name[kMaxMarks] = {};
+  int n_marks = 0;
   bool timed = false;
   int rpass_variant = 6;
   std::vector<void*> allocs;
@@ -93,6 +127,15 @@ struct gvs_handle {
     hipError_t e_ = (call);                                                     \
     if (e_ != hipSuccess) {                                                     \
       if (h) (h)->err = std::string(#call) + ": " + hipGetErrorString(e_);      \
+      return GVS_ERR_DEVICE;                                                    \
+    }                                                                           \
+  } while (0)
+
+#define GVS_NCCL(h, call)                                                       \
+  do {                                                                          \
+    ncclResult_t r_ = (call);                                                   \
+    if (r_ != ncclSuccess) {                                                    \
+      if (h) (h)->err = std::string(#call) + ": " + ncclGetErrorString(r_);     \
       return GVS_ERR_DEVICE;                                                    \
     }                                                                           \
   } while (0)
@@ -112,21 +155,13 @@ static int dalloc_t(gvs_handle* h, T** p, size_t count) {
   return dalloc(h, reinterpret_cast<void**>(p), count * sizeof(T));
 }
 
-extern "C" {
-
-const char* gvs_version(void) { return "gvstore 0.1.0 (gfx950)"; }
-
-int gvs_config_init(gvs_config* cfg, uint64_t msg_capacity) {
-  if (!cfg || !is_pow2(msg_capacity) || msg_capacity < 256) return GVS_ERR_INVALID_ARG;
-  std::memset(cfg, 0, sizeof *cfg);
-  cfg->msg_capacity = msg_capacity;
-  uint64_t R = msg_capacity / 16 < 256 ? 256 : msg_capacity / 16;  // SURVEY.md §8(a) a9: R = N/16
-  cfg->mailbox_partition_slots = 256;
-  cfg->mailbox_partitions = (uint32_t)(R / 256);
-  cfg->max_batch = msg_capacity < 65536 ? 4096 : 65536;
-  for (int i = 0; i < 32; ++i) cfg->secret_key[i] = (uint8_t)(0x67 + 31 * i);
-  return GVS_OK;
+static void mark(gvs_handle* h, const char* name) {
+  if (!h->timed || h->n_marks >= kMaxMarks) return;
+  (void)hipEventRecord(h->ev[h->n_marks], h->stream);
+  h->mark_name[h->n_marks++] = name;
 }
+
+// ------------------------------------------------------------------ creation
 
 static int validate(const gvs_config* c) {
   if (!c) return GVS_ERR_INVALID_ARG;
@@ -140,68 +175,158 @@ static int validate(const gvs_config* c) {
   if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << (kSeqBits - 1)))
     return GVS_ERR_INVALID_ARG;
   if (c->flags != 0) return GVS_ERR_INVALID_ARG;
-  for (int i = 1; i < 7; ++i)
+  if (c->rows_per_partition && (!is_pow2(c->rows_per_partition) ||
+                                c->rows_per_partition < (uint32_t)kTile ||
+                                c->rows_per_partition > (uint32_t)kRowsMax))
+    return GVS_ERR_INVALID_ARG;
+  if (c->shard_count > kShardsMax) return GVS_ERR_INVALID_ARG;
+  if (c->route_capacity > c->max_batch) return GVS_ERR_INVALID_ARG;
+  for (int i = 0; i < 3; ++i)
     if (c->reserved[i] != 0) return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
 
-int gvs_destroy(gvs_handle* h) {
-  if (!h) return GVS_ERR_INVALID_ARG;
-  (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (void* p : h->allocs) (void)hipFree(p);
-  for (auto& e : h->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
-  delete h;
+// Default C: mean load B/S plus 8 standard deviations of a binomial bucket
+// and a constant, rounded to 64.  Uniformly keyed traffic then overflows with
+// probability far below 1e-12 per batch; skewed traffic (one recipient taking
+// more than C of a source's requests) fails the batch as a whole.
+static uint32_t auto_capacity(uint32_t B, uint32_t S) {
+  if (S <= 1) return B;
+  const double mu = std::ceil((double)B / S);
+  uint64_t c = (uint64_t)std::ceil(mu + 8.0 * std::sqrt(mu) + 64.0);
+  c = (c + 63) / 64 * 64;
+  return (uint32_t)(c < B ? c : B);
+}
+
+static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
+  const gvs_config* cfg = &h->cfg;
+  e.shard = shard;
+  e.N = cfg->msg_capacity;
+  e.Q = cfg->mailbox_partitions;
+  e.Sr = cfg->mailbox_partition_slots;
+  e.R = (uint64_t)e.Q * e.Sr;
+  e.B = B;
+  e.logQ = log2u(e.Q);
+  // rows per message-table partition (one workgroup each): the config value
+  // if set, else N/16384 clamped to [256, 4096] (C3: 1024 rows -> 16384
+  // workgroups, so the grid is many times the resident capacity)
+  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : e.N / 16384;
+  if (S < (uint64_t)kTile) S = kTile;
+  if (S > (uint64_t)kRowsMax) S = kRowsMax;
+  if (S > e.N) S = e.N;
+  if (!is_pow2(S)) return GVS_ERR_INVALID_ARG;
+  e.S = (uint32_t)S;
+  e.W = (uint32_t)(e.N / S);
+  e.nblk = B / 1024;
+  e.ring_size = e.N + B;
+  if (e.W + 1 > (uint32_t)kBinsMax) return GVS_ERR_INVALID_ARG;
+  e.kc.pk0 = ld64(cfg->secret_key);
+  e.kc.pk1 = ld64(cfg->secret_key + 8);
+  e.kc.hk0 = ld64(cfg->secret_key + 16);
+  e.kc.hk1 = ld64(cfg->secret_key + 24);
+  e.kc.tag = shard_tag(shard);
+  e.kc.nshards = h->S;
+
+#define A(ptr, n)                                \
+  do {                                           \
+    if (int r_ = dalloc_t(h, &e.ptr, (n))) return r_; \
+  } while (0)
+  const uint64_t E = kExtra;
+  A(table, e.N * 64);
+  A(mbox, e.R * 64);
+  A(side, e.R);
+  A(ring, e.ring_size);
+  A(scal, 1);
+  A(img, (B + E) * 64);
+  A(types, B);
+  A(ops, B);
+  A(kinds, B);
+  A(s1keys, B);
+  A(qcount, e.Q + 1);
+  A(qstart, e.Q + 2);
+  A(m1out, B + E);
+  A(pflag, B);
+  A(pslot, B);
+  A(bsum, 2 * e.nblk);
+  A(cslot, B);
+  A(rop, B + E);
+  A(rkeys, B);
+  A(pcount, e.W + 1);
+  A(pstart, e.W + 2);
+  A(rres, B + E);
+  A(resp, (B + E) * kSlotU4);
+  A(dflag, B);
+  A(dslot, B);
+  A(bsum2, e.nblk);
+  if (h->mode != kSingle) A(recv, (uint64_t)h->S * h->C * kSlotU4);
+#undef A
+  hipStream_t s = h->stream;
+  GVS_HIP(h, hipMemsetAsync(e.img + (uint64_t)B * 64, 0, E * 1024, s));
+  GVS_HIP(h, hipMemsetAsync(e.rop + B, 0, E * sizeof(ROp), s));
+  GVS_HIP(h, hipMemsetAsync(e.table, 0, e.N * 1024, s));
+  GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
+  GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
+  // free ring = slots 0..N-1 in order; scalars
+  std::vector<uint32_t> ring(e.ring_size, kNone);
+  for (uint64_t i = 0; i < e.N; ++i) ring[i] = (uint32_t)i;
+  Scal sc{};
+  sc.head = 0;
+  sc.tail = e.N;
+  GVS_HIP(h, hipMemcpyAsync(e.ring, ring.data(), ring.size() * 4, hipMemcpyHostToDevice, s));
+  GVS_HIP(h, hipMemcpyAsync(e.scal, &sc, sizeof sc, hipMemcpyHostToDevice, s));
+  GVS_HIP(h, hipStreamSynchronize(s));
   return GVS_OK;
 }
 
-int gvs_create(const gvs_config* cfg, gvs_handle** out) {
+static int router_init(gvs_handle* h, Router& r) {
+  const uint64_t B = h->Bsub, SC = (uint64_t)h->S * h->C;
+  if (int rc = dalloc_t(h, &r.dest, B)) return rc;
+  if (int rc = dalloc_t(h, &r.bcnt, (B / 1024) * h->S)) return rc;
+  if (int rc = dalloc_t(h, &r.pos, B)) return rc;
+  if (int rc = dalloc_t(h, &r.tot, h->S)) return rc;
+  if (int rc = dalloc_t(h, &r.send, SC * kSlotU4)) return rc;
+  if (int rc = dalloc_t(h, &r.back, SC * kSlotU4)) return rc;
+  return GVS_OK;
+}
+
+extern "C" int gvs_destroy(gvs_handle* h);
+
+static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_id,
+                         gvs_handle** out) {
   if (!out) return GVS_ERR_INVALID_ARG;
   *out = nullptr;
-  int rc = validate(cfg);
-  if (rc) return rc;
+  if (int rc = validate(cfg)) return rc;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GVS_ERR_NO_DEVICE;
   if ((int)cfg->device >= ndev) return GVS_ERR_INVALID_ARG;
   gvs_handle* h = new (std::nothrow) gvs_handle();
   if (!h) return GVS_ERR_OUT_OF_MEMORY;
   h->cfg = *cfg;
+  h->mode = mode;
   h->device = (int)cfg->device;
-  h->N = cfg->msg_capacity;
-  h->Q = cfg->mailbox_partitions;
-  h->Sr = cfg->mailbox_partition_slots;
-  h->R = (uint64_t)h->Q * h->Sr;
-  h->B = cfg->max_batch;
-  h->logQ = log2u(h->Q);
-  // rows per message-table partition (one workgroup each): reserved[0] if set,
-  // else N/16384 clamped to [256, 4096] (C3: 1024 rows -> 16384 workgroups, so
-  // the grid is many times the resident capacity and its tail is short)
-  uint64_t S = cfg->reserved[0] ? cfg->reserved[0] : h->N / 16384;
-  if (S < (uint64_t)kTile) S = kTile;
-  if (S > (uint64_t)kRowsMax) S = kRowsMax;
-  if (S > h->N) S = h->N;
-  if (!is_pow2(S)) {
+  h->S = cfg->shard_count ? cfg->shard_count : 1;
+  h->Bsub = cfg->max_batch;
+  if (mode == kRccl && cfg->shard_index >= h->S) {
     delete h;
     return GVS_ERR_INVALID_ARG;
   }
-  h->S = (uint32_t)S;
-  h->W = (uint32_t)(h->N / S);
-  h->NT = (uint32_t)(h->N / kTile);
-  h->nblk = h->B / 1024;
-  h->ring_size = h->N + h->B;
-  if (h->W + 1 > (uint32_t)kBinsMax || h->S > (uint32_t)kRowsMax) {
-    delete h;
-    return GVS_ERR_INVALID_ARG;
+  if (mode == kSingle) {
+    h->C = 0;
+    h->Be = h->Bsub;
+  } else {
+    h->C = cfg->route_capacity ? cfg->route_capacity : auto_capacity(h->Bsub, h->S);
+    uint64_t be = 1024;
+    while (be < (uint64_t)h->S * h->C) be <<= 1;
+    if (be > (1u << (kSeqBits - 1))) {
+      delete h;
+      return GVS_ERR_INVALID_ARG;
+    }
+    h->Be = (uint32_t)be;
   }
-  h->kc.pk0 = ld64(cfg->secret_key);
-  h->kc.pk1 = ld64(cfg->secret_key + 8);
-  h->kc.hk0 = ld64(cfg->secret_key + 16);
-  h->kc.hk1 = ld64(cfg->secret_key + 24);
-
   auto fail = [&](int code) {
+    std::string e = h->err;
     gvs_destroy(h);
+    (void)e;
     return code;
   };
   if (hipSetDevice(h->device) != hipSuccess) return fail(GVS_ERR_DEVICE);
@@ -210,74 +335,34 @@ int gvs_create(const gvs_config* cfg, gvs_handle** out) {
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(GVS_ERR_DEVICE);
 
-  const uint64_t B = h->B;
-#define A(ptr, n)                            \
-  do {                                       \
-    int r_ = dalloc_t(h, &h->ptr, (n));      \
-    if (r_) {                                \
-      std::string e_ = h->err;               \
-      gvs_destroy(h);                        \
-      (void)e_;                              \
-      return r_;                             \
-    }                                        \
-  } while (0)
-  A(table, h->N * 64);
-  A(mbox, h->R * 64);
-  A(side, h->R);
-  A(ring, h->ring_size);
-  A(scal, 1);
-  // per-op arrays carry E extra records after the B real ones; record B is the
-  // shared dummy of the dry-run ops (fixed instruction footprint)
-  const uint64_t E = 64;
-  h->extra = E;
-  A(img, (B + E) * 64);
-  A(types, B);
-  A(ops, B);
-  A(kinds, B);
-  A(s1keys, B);
-  A(qcount, h->Q + 1);
-  A(qstart, h->Q + 2);
-  A(m1out, B + E);
-  A(pflag, B);
-  A(pslot, B);
-  A(bsum, 2 * h->nblk);
-  A(cslot, B);
-  A(rop, B + E);
-  A(rkeys, B);
-  A(pcount, h->W + 1);
-  A(pstart, h->W + 2);
-  A(rres, B + E);
-  A(resp, (B + E) * (kRespSlot / 16));
-  A(dflag, B);
-  A(dslot, B);
-  A(bsum2, h->nblk);
-  A(in_stage, B * 65);
-  A(out_stage, B * 65);
-#undef A
-  hipStream_t s = h->stream;
-  if (hipMemsetAsync(h->img + B * 64, 0, E * 1024, s) != hipSuccess ||
-      hipMemsetAsync(h->rop + B, 0, E * sizeof(ROp), s) != hipSuccess ||
-      hipMemsetAsync(h->table, 0, h->N * 1024, s) != hipSuccess ||
-      hipMemsetAsync(h->mbox, 0, h->R * 1024, s) != hipSuccess ||
-      hipMemsetAsync(h->side, 0, h->R * 16, s) != hipSuccess)
-    return fail(GVS_ERR_DEVICE);
-  // free ring = slots 0..N-1 in order; scalars
-  {
-    std::vector<uint32_t> ring(h->ring_size, kNone);
-    for (uint64_t i = 0; i < h->N; ++i) ring[i] = (uint32_t)i;
-    Scal sc{};
-    sc.head = 0;
-    sc.tail = h->N;
-    if (hipMemcpyAsync(h->ring, ring.data(), ring.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(h->scal, &sc, sizeof sc, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+  const uint32_t n_eng = mode == kLocal ? h->S : 1u;
+  const uint32_t n_src = mode == kSingle ? 0u : (mode == kLocal ? h->S : 1u);
+  h->eng.resize(n_eng);
+  h->rt.resize(n_src);
+  for (uint32_t k = 0; k < n_eng; ++k) {
+    const uint32_t shard = mode == kRccl ? cfg->shard_index : k;
+    if (int rc = engine_init(h, h->eng[k], shard, h->Be)) return fail(rc);
+  }
+  for (uint32_t k = 0; k < n_src; ++k)
+    if (int rc = router_init(h, h->rt[k])) return fail(rc);
+  const uint64_t stage = (uint64_t)h->Bsub * (mode == kLocal ? h->S : 1u);
+  if (int rc = dalloc_t(h, &h->in_stage, stage * kAbiU4)) return fail(rc);
+  if (int rc = dalloc_t(h, &h->out_stage, stage * kAbiU4)) return fail(rc);
+  if (mode == kRccl) {
+    ncclUniqueId id;
+    std::memcpy(&id, comm_id, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&h->comm, (int)h->S, id, (int)cfg->shard_index);
+    if (r != ncclSuccess) {
+      h->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+      h->comm = nullptr;
       return fail(GVS_ERR_DEVICE);
+    }
   }
   *out = h;
   return GVS_OK;
 }
 
-}  // extern "C"
+// ------------------------------------------------------------------ pipeline
 
 template <typename K, int LMAX>
 static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
@@ -293,134 +378,272 @@ static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
   return GVS_OK;
 }
 
-static MArgs margs(gvs_handle* h) {
+static MArgs margs(const Engine& e) {
   MArgs a{};
-  a.keys = h->s1keys;
-  a.qstart = h->qstart;
-  a.mbox = h->mbox;
-  a.side = h->side;
-  a.m1out = h->m1out;
-  a.rop = h->rop;
-  a.rres = h->rres;
-  a.scal = h->scal;
-  a.Q = h->Q;
-  a.Sr = h->Sr;
-  a.B = h->B;
+  a.keys = e.s1keys;
+  a.qstart = e.qstart;
+  a.mbox = e.mbox;
+  a.side = e.side;
+  a.m1out = e.m1out;
+  a.rop = e.rop;
+  a.rres = e.rres;
+  a.scal = e.scal;
+  a.Q = e.Q;
+  a.Sr = e.Sr;
+  a.B = e.B;
   a.dummy_blocks = kDummyBlocks;
-  a.N = h->N;
-  a.kc = h->kc;
+  a.N = e.N;
+  a.kc = e.kc;
   return a;
 }
 
-static AllocArgs aargs(gvs_handle* h) {
+static AllocArgs aargs(const Engine& e) {
   AllocArgs a{};
-  a.kinds = h->kinds;
-  a.m1out = h->m1out;
-  a.ops = h->ops;
-  a.pflag = h->pflag;
-  a.pslot = h->pslot;
-  a.bsum = h->bsum;
-  a.cslot = h->cslot;
-  a.ring = h->ring;
-  a.rop = h->rop;
-  a.rkeys = h->rkeys;
-  a.pcount = h->pcount;
-  a.scal = h->scal;
-  a.B = h->B;
-  a.nblk = h->nblk;
-  a.W = h->W;
-  a.S = h->S;
-  a.N = h->N;
-  a.ring_size = h->ring_size;
-  a.kc = h->kc;
+  a.kinds = e.kinds;
+  a.m1out = e.m1out;
+  a.ops = e.ops;
+  a.pflag = e.pflag;
+  a.pslot = e.pslot;
+  a.bsum = e.bsum;
+  a.cslot = e.cslot;
+  a.ring = e.ring;
+  a.rop = e.rop;
+  a.rkeys = e.rkeys;
+  a.pcount = e.pcount;
+  a.scal = e.scal;
+  a.B = e.B;
+  a.nblk = e.nblk;
+  a.W = e.W;
+  a.S = e.S;
+  a.N = e.N;
+  a.ring_size = e.ring_size;
+  a.kc = e.kc;
   return a;
 }
 
-// Enqueue the whole pipeline for one batch on h->stream; responses for the
-// first n requests are written to d_out (caller layout).
-static int run_pipeline(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out) {
+// Phase A: everything up to the mailbox read pass.  Writes only per-batch
+// scratch, so a batch can still be abandoned after it (error words).
+static int phase_a(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride, uint32_t n) {
   hipStream_t s = h->stream;
-  const uint32_t B = h->B, nblk = h->nblk;
-  int st = 0;
-  auto mark = [&](int i) {
-    if (h->timed) (void)hipEventRecord(h->ev[i], s);
-  };
-  GVS_HIP(h, hipMemsetAsync(&h->scal->error, 0, sizeof(uint32_t), s));
-  GVS_HIP(h, hipMemsetAsync(h->qcount, 0, (h->Q + 1) * sizeof(uint32_t), s));
-  GVS_HIP(h, hipMemsetAsync(h->pcount, 0, (h->W + 1) * sizeof(uint32_t), s));
-  mark(st++);
-  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, n, B, h->img, h->types);
-  mark(st++);
+  const uint32_t B = e.B;
+  GVS_HIP(h, hipMemsetAsync(e.qcount, 0, (e.Q + 1) * sizeof(uint32_t), s));
+  GVS_HIP(h, hipMemsetAsync(e.pcount, 0, (e.W + 1) * sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types);
+  mark(h, "copy");
   {
-    MetaArgs a{h->img, h->types, h->ops, h->kinds, h->s1keys, h->qcount,
-               n, B, h->Q, h->logQ, h->N, h->kc};
-    hipLaunchKernelGGL(k_meta, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, h->qcount, h->qstart, h->Q + 1);
+    MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, e.qcount, n, B, e.Q, e.logQ, e.N, e.kc};
+    hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
   }
-  mark(st++);
-  if (int r = sort_keys<Key128, 4096>(h, h->s1keys, B)) return r;
-  mark(st++);
-  hipLaunchKernelGGL(k_m1, dim3(h->Q + kDummyBlocks), dim3(256), 0, s, margs(h));
-  mark(st++);
+  mark(h, "meta");
+  if (int r = sort_keys<Key128, 4096>(h, e.s1keys, B)) return r;
+  mark(h, "sort_s1");
+  hipLaunchKernelGGL(k_m1, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(e));
+  mark(h, "m1");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+static void launch_rpass(gvs_handle* h, const Engine& e, uint32_t n) {
+  hipStream_t s = h->stream;
+  RArgs a{};
+  a.table = e.table;
+  a.rkeys = e.rkeys;
+  a.pstart = e.pstart;
+  a.rop = e.rop;
+  a.img = e.img;
+  a.resp = e.resp;
+  a.rres = e.rres;
+  a.scal = e.scal;
+  a.n = n;
+  a.B = e.B;
+  a.W = e.W;
+  a.S = e.S;
+  a.null_blocks = kNullBlocks;
+  const dim3 g(e.W + kNullBlocks), b(256);
+  switch (h->rpass_variant) {
+    case 0: hipLaunchKernelGGL((k_rpass<4, false, false, 1>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_rpass<4, true, true, 1>), g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((k_rpass<8, true, false, 4>), g, b, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_rpass<8, false, true, 4>), g, b, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((k_rpass<2, true, true, 8>), g, b, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((k_rpass<16, true, true, 2>), g, b, 0, s, a); break;
+    case 7: hipLaunchKernelGGL((k_rpass<32, true, true, 1>), g, b, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_rpass<16, true, true, 1>), g, b, 0, s, a); break;
+    case 9: hipLaunchKernelGGL((k_rpass<8, true, true, 2>), g, b, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_rpass<16, false, true, 2>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_rpass<8, true, true, 4>), g, b, 0, s, a); break;
+  }
+}
+
+// Phase B: allocation, message pass, commit, mailbox write pass.  Every kernel
+// returns at once if the shard's error word is set.  With d_out, responses for
+// the first n ops are converted to the caller layout; routed shards leave them
+// in e.resp for the return exchange.
+static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B, nblk = e.nblk;
   {
-    AllocArgs a = aargs(h);
+    AllocArgs a = aargs(e);
     hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, h->pcount, h->pstart, h->W + 1);
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.pcount, e.pstart, e.W + 1);
   }
-  mark(st++);
-  if (int r = sort_keys<uint64_t, 8192>(h, h->rkeys, B)) return r;
-  mark(st++);
+  mark(h, "alloc");
+  if (int r = sort_keys<uint64_t, 8192>(h, e.rkeys, B)) return r;
+  mark(h, "sort_r");
+  launch_rpass(h, e, n);
+  mark(h, "rpass");
   {
-    RArgs a{};
-    a.table = h->table;
-    a.rkeys = h->rkeys;
-    a.pstart = h->pstart;
-    a.rop = h->rop;
-    a.img = h->img;
-    a.resp = h->resp;
-    a.rres = h->rres;
-    a.scal = h->scal;
-    a.n = n;
-    a.B = B;
-    a.W = h->W;
-    a.S = h->S;
-    a.null_blocks = kNullBlocks;
-    const dim3 g(h->W + kNullBlocks), b(256);
-    switch (h->rpass_variant) {
-      case 0: hipLaunchKernelGGL((k_rpass<4, false, false, 1>), g, b, 0, s, a); break;
-      case 1: hipLaunchKernelGGL((k_rpass<4, true, true, 1>), g, b, 0, s, a); break;
-      case 3: hipLaunchKernelGGL((k_rpass<8, true, false, 4>), g, b, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_rpass<8, false, true, 4>), g, b, 0, s, a); break;
-      case 5: hipLaunchKernelGGL((k_rpass<2, true, true, 8>), g, b, 0, s, a); break;
-      case 6: hipLaunchKernelGGL((k_rpass<16, true, true, 2>), g, b, 0, s, a); break;
-      case 7: hipLaunchKernelGGL((k_rpass<32, true, true, 1>), g, b, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_rpass<16, true, true, 1>), g, b, 0, s, a); break;
-      case 9: hipLaunchKernelGGL((k_rpass<8, true, true, 2>), g, b, 0, s, a); break;
-      case 10: hipLaunchKernelGGL((k_rpass<16, false, true, 2>), g, b, 0, s, a); break;
-      default: hipLaunchKernelGGL((k_rpass<8, true, true, 4>), g, b, 0, s, a); break;
-    }
-  }
-  mark(st++);
-  {
-    PostArgs a{h->kinds, h->rres, h->rop, h->dflag, h->dslot, h->bsum2, h->ring, h->scal,
-               B, nblk, h->ring_size};
+    PostArgs a{e.kinds, e.rres, e.rop, e.dflag, e.dslot, e.bsum2, e.ring, e.scal, B, nblk,
+               e.ring_size};
     hipLaunchKernelGGL(k_post_sum, dim3(nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
   }
-  mark(st++);
-  hipLaunchKernelGGL(k_m2, dim3(h->Q + kDummyBlocks), dim3(256), 0, s, margs(h));
-  if (n) hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)h->resp, n, d_out);
-  mark(st++);
+  mark(h, "post");
+  hipLaunchKernelGGL(k_m2, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(e));
+  if (d_out && n)
+    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
+  mark(h, "m2");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+static RouteArgs rargs(gvs_handle* h, const Router& r, const Engine& e, const uint4* in,
+                       uint32_t n) {
+  RouteArgs a{};
+  a.in = in;
+  a.n = n;
+  a.B = h->Bsub;
+  a.S = h->S;
+  a.C = h->C;
+  a.dest = r.dest;
+  a.bcnt = r.bcnt;
+  a.pos = r.pos;
+  a.tot = r.tot;
+  a.send = r.send;
+  a.err = &e.scal->error;
+  a.N = e.N;
+  a.kc = e.kc;
+  return a;
+}
+
+static void route(gvs_handle* h, const Router& r, const Engine& e, const uint4* in, uint32_t n) {
+  hipStream_t s = h->stream;
+  const RouteArgs a = rargs(h, r, e, in, n);
+  const uint32_t nblk = h->Bsub / 1024;
+  hipLaunchKernelGGL(k_route_dest, dim3(nblk), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_route_pos, dim3(nblk), dim3(1024), 0, s, a);
+  if (n) hipLaunchKernelGGL(k_route_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_route_fill, dim3((h->S * h->C + 3) / 4), dim3(256), 0, s, a);
+}
+
+static int reset_errors(gvs_handle* h) {
+  for (auto& e : h->eng)
+    GVS_HIP(h, hipMemsetAsync(&e.scal->error, 0, sizeof(uint32_t), h->stream));
+  return GVS_OK;
+}
+
+// all-to-all of S buckets of C slots: src_buf(k) bucket d -> dst_buf(d) bucket k
+static int exchange(gvs_handle* h, bool forward) {
+  const size_t bytes = (size_t)h->C * kRespSlot;
+  const uint64_t span = (uint64_t)h->C * kSlotU4;
+  if (h->mode == kLocal) {
+    for (uint32_t src = 0; src < h->S; ++src)
+      for (uint32_t dst = 0; dst < h->S; ++dst) {
+        // forward: router src, bucket dst -> engine dst, bucket src
+        // back:    engine src, bucket dst -> router dst, bucket src
+        const uint4* from = forward ? h->rt[src].send + dst * span : h->eng[src].resp + dst * span;
+        uint4* to = forward ? h->eng[dst].recv + src * span : h->rt[dst].back + src * span;
+        GVS_HIP(h, hipMemcpyAsync(to, from, bytes, hipMemcpyDeviceToDevice, h->stream));
+      }
+    return GVS_OK;
+  }
+  const uint4* sendbuf = forward ? h->rt[0].send : h->eng[0].resp;
+  uint4* recvbuf = forward ? h->eng[0].recv : h->rt[0].back;
+  GVS_NCCL(h, ncclGroupStart());
+  for (uint32_t p = 0; p < h->S; ++p) {
+    GVS_NCCL(h, ncclSend(sendbuf + p * span, bytes, ncclUint8, (int)p, h->comm, h->stream));
+    GVS_NCCL(h, ncclRecv(recvbuf + p * span, bytes, ncclUint8, (int)p, h->comm, h->stream));
+  }
+  GVS_NCCL(h, ncclGroupEnd());
+  return GVS_OK;
+}
+
+// Make every shard see the OR (kLocal) / max (kRccl) of all error words, so
+// that all shards apply a batch or none does.
+static int agree_errors(gvs_handle* h) {
+  if (h->mode == kLocal) {
+    ErrSet es{};
+    es.n = h->S;
+    for (uint32_t k = 0; k < h->S; ++k) es.e[k] = &h->eng[k].scal->error;
+    hipLaunchKernelGGL(k_err_or, dim3(1), dim3(64), 0, h->stream, es);
+    GVS_HIP(h, hipGetLastError());
+  } else if (h->mode == kRccl) {
+    uint32_t* e = &h->eng[0].scal->error;
+    GVS_NCCL(h, ncclAllReduce(e, e, 1, ncclUint32, ncclMax, h->comm, h->stream));
+  }
+  return GVS_OK;
+}
+
+// Enqueue one batch: n requests in the caller layout at d_in, responses in the
+// caller layout to d_out (kLocal: n <= S*Bsub, source k = requests
+// [k*Bsub, (k+1)*Bsub)).
+static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out) {
+  h->n_marks = 0;
+  mark(h, "start");
+  if (int r = reset_errors(h)) return r;
+  if (h->mode == kSingle) {
+    Engine& e = h->eng[0];
+    if (int r = phase_a(h, e, d_in, kAbiU4, n)) return r;
+    return phase_b(h, e, n, d_out);
+  }
+  const uint32_t n_src = (uint32_t)h->rt.size();
+  for (uint32_t k = 0; k < n_src; ++k) {
+    const uint64_t off = (uint64_t)k * h->Bsub;
+    const uint32_t nk = n > off ? (uint32_t)std::min<uint64_t>(n - off, h->Bsub) : 0u;
+    route(h, h->rt[k], h->eng[k], d_in + off * kAbiU4, nk);
+  }
+  mark(h, "route");
+  if (int r = exchange(h, true)) return r;
+  mark(h, "xchg");
+  const uint32_t SC = h->S * h->C;
+  for (auto& e : h->eng)
+    if (int r = phase_a(h, e, e.recv, kSlotU4, SC)) return r;
+  if (int r = agree_errors(h)) return r;
+  mark(h, "agree");
+  for (auto& e : h->eng)
+    if (int r = phase_b(h, e, SC, nullptr)) return r;
+  if (int r = exchange(h, false)) return r;
+  mark(h, "xchg_back");
+  for (uint32_t k = 0; k < n_src; ++k) {
+    const uint64_t off = (uint64_t)k * h->Bsub;
+    const uint32_t nk = n > off ? (uint32_t)std::min<uint64_t>(n - off, h->Bsub) : 0u;
+    if (nk)
+      hipLaunchKernelGGL(k_route_gather, dim3((nk + 3) / 4), dim3(256), 0, h->stream,
+                         (const uint32_t*)h->rt[k].pos, (const uint4*)h->rt[k].back, nk,
+                         d_out + off * kAbiU4);
+  }
+  mark(h, "gather");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
 }
 
 static int finish(gvs_handle* h) {
+  if (h->mode == kRccl) {
+    if (int r = agree_errors(h)) return r;  // late flags (M2) too: same verdict on every rank
+  } else if (h->mode == kLocal) {
+    if (int r = agree_errors(h)) return r;
+  }
   uint32_t e = 0;
-  GVS_HIP(h, hipMemcpyAsync(&e, &h->scal->error, sizeof e, hipMemcpyDeviceToHost, h->stream));
+  GVS_HIP(h, hipMemcpyAsync(&e, &h->eng[0].scal->error, sizeof e, hipMemcpyDeviceToHost,
+                            h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
+  if (e & 4u) {
+    h->err = "batch overflow: more than route_capacity requests of one source for one shard";
+    return GVS_ERR_BATCH_OVERFLOW;
+  }
   if (e & 1u) {
     h->err = "batch overflow: more than 512 distinct recipients in one mailbox partition";
     return GVS_ERR_BATCH_OVERFLOW;
@@ -432,15 +655,67 @@ static int finish(gvs_handle* h) {
   return GVS_OK;
 }
 
+static uint32_t max_submit(const gvs_handle* h) {
+  return h->Bsub * (h->mode == kLocal ? h->S : 1u);
+}
+
+// ------------------------------------------------------------------ C ABI
+
 extern "C" {
 
+const char* gvs_version(void) { return "gvstore 0.2.0 (gfx950)"; }
+
+int gvs_config_init(gvs_config* cfg, uint64_t msg_capacity) {
+  if (!cfg || !is_pow2(msg_capacity) || msg_capacity < 256) return GVS_ERR_INVALID_ARG;
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->msg_capacity = msg_capacity;
+  uint64_t R = msg_capacity / 16 < 256 ? 256 : msg_capacity / 16;  // SURVEY.md §8(a) a9: R = N/16
+  cfg->mailbox_partition_slots = 256;
+  cfg->mailbox_partitions = (uint32_t)(R / 256);
+  cfg->max_batch = msg_capacity < 65536 ? 4096 : 65536;
+  for (int i = 0; i < 32; ++i) cfg->secret_key[i] = (uint8_t)(0x67 + 31 * i);
+  return GVS_OK;
+}
+
+int gvs_destroy(gvs_handle* h) {
+  if (!h) return GVS_ERR_INVALID_ARG;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  for (void* p : h->allocs) (void)hipFree(p);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return GVS_OK;
+}
+
+int gvs_create(const gvs_config* cfg, gvs_handle** out) {
+  if (!cfg) return GVS_ERR_INVALID_ARG;
+  return create_common(cfg, cfg->shard_count > 1 ? kLocal : kSingle, nullptr, out);
+}
+
+int gvs_comm_unique_id(uint8_t out[GVS_COMM_ID_BYTES]) {
+  if (!out) return GVS_ERR_INVALID_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return GVS_ERR_DEVICE;
+  std::memcpy(out, &id, sizeof id);
+  return GVS_OK;
+}
+
+int gvs_create_sharded(const gvs_config* cfg, const uint8_t comm_id[GVS_COMM_ID_BYTES],
+                       gvs_handle** out) {
+  if (!cfg || !comm_id || cfg->shard_count < 1) return GVS_ERR_INVALID_ARG;
+  return create_common(cfg, kRccl, comm_id, out);
+}
+
 int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_response* out) {
-  if (!h || (!reqs && n) || (!out && n) || n > h->B) return GVS_ERR_INVALID_ARG;
+  if (!h || (!reqs && n) || (!out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   GVS_HIP(h, hipSetDevice(h->device));
   if (n)
     GVS_HIP(h, hipMemcpyAsync(h->in_stage, reqs, (size_t)n * sizeof(gvs_request),
                               hipMemcpyHostToDevice, h->stream));
-  if (int r = run_pipeline(h, h->in_stage, n, h->out_stage)) return r;
+  if (int r = run_batch(h, h->in_stage, n, h->out_stage)) return r;
   if (n)
     GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * sizeof(gvs_response),
                               hipMemcpyDeviceToHost, h->stream));
@@ -448,9 +723,9 @@ int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_re
 }
 
 int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void* d_out) {
-  if (!h || (!d_reqs && n) || (!d_out && n) || n > h->B) return GVS_ERR_INVALID_ARG;
+  if (!h || (!d_reqs && n) || (!d_out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   GVS_HIP(h, hipSetDevice(h->device));
-  if (int r = run_pipeline(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
+  if (int r = run_batch(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
   return finish(h);
 }
 
@@ -460,29 +735,40 @@ int gvs_access(gvs_handle* h, const gvs_request* req, gvs_response* out) {
 
 int gvs_get_stats(gvs_handle* h, gvs_stats* out) {
   if (!h || !out) return GVS_ERR_INVALID_ARG;
-  Scal sc{};
-  GVS_HIP(h, hipMemcpyAsync(&sc, h->scal, sizeof sc, hipMemcpyDeviceToHost, h->stream));
-  GVS_HIP(h, hipStreamSynchronize(h->stream));
-  out->messages = sc.count;
-  out->mailboxes = sc.n_mailboxes;
-  out->batches = sc.batches;
-  out->creation_counter = sc.ctr;
-  out->free_ring_head = sc.head;
-  out->free_ring_tail = sc.tail;
-  out->msg_partitions = h->W;
-  out->msg_partition_slots = h->S;
+  std::memset(out, 0, sizeof *out);
+  for (auto& e : h->eng) {
+    Scal sc{};
+    GVS_HIP(h, hipMemcpyAsync(&sc, e.scal, sizeof sc, hipMemcpyDeviceToHost, h->stream));
+    GVS_HIP(h, hipStreamSynchronize(h->stream));
+    out->messages += sc.count;
+    out->mailboxes += sc.n_mailboxes;
+    out->batches = sc.batches;
+    out->creation_counter += sc.ctr;
+    out->free_ring_head += sc.head;
+    out->free_ring_tail += sc.tail;
+  }
+  out->msg_partitions = h->eng[0].W;
+  out->msg_partition_slots = h->eng[0].S;
+  out->shards = h->eng.size();
+  out->route_capacity = h->C;
+  out->shard_batch = h->Be;
   return GVS_OK;
 }
 
 int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
-  if (!h || !host_dst || bytes < h->N * 1024) return GVS_ERR_INVALID_ARG;
-  std::vector<uint8_t> phys(h->N * 1024);
-  GVS_HIP(h, hipMemcpyAsync(phys.data(), h->table, phys.size(), hipMemcpyDeviceToHost, h->stream));
-  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  if (!h || !host_dst) return GVS_ERR_INVALID_ARG;
+  const uint64_t N = h->eng[0].N;
+  if (bytes < N * 1024 * h->eng.size()) return GVS_ERR_INVALID_ARG;
+  std::vector<uint8_t> phys(N * 1024);
   uint8_t* dst = (uint8_t*)host_dst;
-  for (uint64_t sl = 0; sl < h->N; ++sl) {
-    uint64_t row = (sl % h->W) * h->S + sl / h->W;
-    std::memcpy(dst + sl * 1024, phys.data() + row * 1024, 1024);
+  for (const auto& e : h->eng) {
+    GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
+    GVS_HIP(h, hipStreamSynchronize(h->stream));
+    for (uint64_t sl = 0; sl < N; ++sl) {
+      uint64_t row = (sl % e.W) * e.S + sl / e.W;
+      std::memcpy(dst + sl * 1024, phys.data() + row * 1024, 1024);
+    }
+    dst += N * 1024;
   }
   return GVS_OK;
 }
@@ -508,15 +794,16 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   return GVS_ERR_INVALID_ARG;
 }
 
+// stage i = time from mark i to mark i+1; names are the later mark's
 int gvs_last_timings(gvs_handle* h, const char** names, float* ms, int cap) {
   if (!h) return GVS_ERR_INVALID_ARG;
   if (!h->timed) return 0;
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   int c = 0;
-  for (int i = 0; i < kNumStages && c < cap; ++i, ++c) {
+  for (int i = 0; i + 1 < h->n_marks && c < cap; ++i, ++c) {
     float t = 0.f;
     (void)hipEventElapsedTime(&t, h->ev[i], h->ev[i + 1]);
-    if (names) names[c] = kStageNames[i];
+    if (names) names[c] = h->mark_name[i + 1];
     if (ms) ms[c] = t;
   }
   return c;

@@ -138,19 +138,20 @@ __device__ inline void hist_flush(uint32_t* s_hist, uint32_t nbins, uint32_t* g_
 // ------------------------------------------------------------------ k_copy
 
 // One wave per request: 64 x 16 B of image + the type word.  Rows >= n are
-// padding (zero image, type 0).
-__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint32_t n,
-                                              uint32_t B, uint4* __restrict__ img,
+// padding (zero image, type 0).  `stride` is the input record pitch in 16-B
+// units: 65 for the caller's gvs_request array, 72 for routed slots.
+__global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint32_t stride,
+                                              uint32_t n, uint32_t B, uint4* __restrict__ img,
                                               uint32_t* __restrict__ types) {
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t lane = lane_id();
   if (i >= B) return;
   uint4 v = make_uint4(0, 0, 0, 0);
-  if (i < n) v = in[(uint64_t)i * 65 + lane];
+  if (i < n) v = in[(uint64_t)i * stride + lane];
   img[(uint64_t)i * 64 + lane] = v;
   if (lane == 0) {
     uint32_t t = 0;
-    if (i < n) t = in[(uint64_t)i * 65 + 64].x;
+    if (i < n) t = in[(uint64_t)i * stride + 64].x;
     types[i] = t;
   }
 }

@@ -1,0 +1,159 @@
+// gvs_route.h — gfx950 kernels of the multi-shard request router.
+//
+// A sharded store keeps every message on the shard that owns its recipient's
+// mailbox, so each request touches exactly one shard:
+//   CREATE                      -> shard of the recipient
+//   READ / DELETE with zero id  -> shard of auth_identity (its mailbox)
+//   by-id READ / UPDATE / DELETE -> shard encoded in the id (tag bits)
+//   malformed, zero recipient, undecodable id -> i mod S (answer is the same
+//                                                on every shard)
+// Each source rank packs its requests into S buckets of exactly C slots
+// (stable: submission order is kept inside a bucket), pads the rest with
+// zero requests (type 0, answered as hard errors) and exchanges the buckets
+// all-to-all.  Slots are 1152 B (9 whole 128-B lines) so that no line is ever
+// shared between two requests; every slot is written by one wave.  Sizes seen
+// outside the device are S, C and B only.
+#pragma once
+#include "gvs_device.h"
+
+namespace gvs {
+
+constexpr uint32_t kSlotU4 = kRespSlot / 16;  // 72 x 16 B per routed slot
+constexpr uint32_t kAbiU4 = 65;               // gvs_request / gvs_response: 1040 B
+constexpr uint32_t kShardsMax = 64;
+
+struct RouteArgs {
+  const uint4* in;   // caller requests (kAbiU4 stride)
+  uint32_t n, B, S, C;
+  uint32_t* dest;    // B
+  uint32_t* bcnt;    // nblk * S: per-block per-shard counts
+  uint32_t* pos;     // B: slot in `send`, or kNone
+  uint32_t* tot;     // S: per-shard totals of this source
+  uint4* send;       // S*C slots
+  uint32_t* err;     // the local shard's error word (bit 2: route overflow)
+  uint64_t N;
+  KeyCtx kc;
+};
+
+// request i -> owning shard (S = padding, i >= n)
+__device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
+  if (i >= a.n) return a.S;
+  const uint4* r = a.in + (uint64_t)i * kAbiU4;
+  const uint4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3], c4 = r[4];
+  const uint32_t type = r[64].x;
+  const bool id_zero = !nz4(c0);
+  const bool auth_zero = !nz4(c1) && !nz4(c2);
+  const bool rcpt_zero = !nz4(c3) && !nz4(c4);
+  const bool hard = type < 1u || type > 4u || auth_zero || (type == 3u && id_zero);
+  const bool next = (type == 2u || type == 4u) && id_zero;
+  const uint4 xa = next ? c1 : c3, xb = next ? c2 : c4;
+  // both hashes run for every request (fixed work)
+  const uint64_t x[4] = {u4lo(xa), u4hi(xa), u4lo(xb), u4hi(xb)};
+  const uint64_t lo = siphash24_blocks(a.kc.hk0, a.kc.hk1, x, 4, 2, 33);
+  const uint32_t by_key = shard_of_hash(lo, a.S);
+  const uint32_t by_id = id_shard(a.kc, u4lo(c0), u4hi(c0), a.N);
+  const uint32_t spread = i % a.S;
+  if (hard) return spread;
+  if (type == 1u) return rcpt_zero ? spread : by_key;
+  if (next) return by_key;
+  return by_id != kNone ? by_id : spread;
+}
+
+// dest of every request + per-block per-shard histogram (all S bins stored)
+__global__ __launch_bounds__(1024) void k_route_dest(RouteArgs a) {
+  __shared__ uint32_t s_h[kShardsMax];
+  const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid;
+  if (tid < a.S) s_h[tid] = 0;
+  __syncthreads();
+  const uint32_t d = route_dest(a, i);
+  a.dest[i] = d;
+  if (d < a.S) atomicAdd(&s_h[d], 1u);
+  __syncthreads();
+  if (tid < a.S) a.bcnt[blockIdx.x * a.S + tid] = s_h[tid];
+}
+
+// stable slot of every request: bucket d, rank = earlier requests for d
+__global__ __launch_bounds__(1024) void k_route_pos(RouteArgs a) {
+  __shared__ uint32_t s_off[kShardsMax];
+  __shared__ uint32_t s_wc[kShardsMax][16];
+  __shared__ uint32_t s_over;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t nblk = gridDim.x;
+  if (tid < a.S) {
+    uint32_t o = 0;
+    for (uint32_t b = 0; b < blockIdx.x; ++b) o += a.bcnt[b * a.S + tid];
+    s_off[tid] = o;
+    if (blockIdx.x == nblk - 1) a.tot[tid] = o + a.bcnt[blockIdx.x * a.S + tid];
+  }
+  if (tid == 0) s_over = 0;
+  const uint32_t i = blockIdx.x * 1024 + tid;
+  const uint32_t d = a.dest[i];
+  uint32_t in_wave = 0;
+  for (uint32_t k = 0; k < a.S; ++k) {
+    const uint64_t m = __ballot(d == k);
+    if (d == k) in_wave = mbcnt64(m);
+    if (lane == 0) s_wc[k][wave] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  uint32_t p = kNone;
+  if (d < a.S) {
+    uint32_t r = s_off[d] + in_wave;
+    for (uint32_t w = 0; w < wave; ++w) r += s_wc[d][w];
+    if (r < a.C) p = d * a.C + r;
+    else atomicOr(&s_over, 1u);
+  }
+  a.pos[i] = p;
+  __syncthreads();
+  if (tid == 0) atomicOr(a.err, s_over ? 4u : 0u);  // one atomic per block, always
+}
+
+// one wave per request: its 1040 B into its slot (1152 B, whole lines)
+__global__ __launch_bounds__(256) void k_route_copy(RouteArgs a) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (i >= a.n) return;
+  const uint32_t p = a.pos[i];
+  if (p == kNone) return;
+  const uint4* src = a.in + (uint64_t)i * kAbiU4;
+  uint4* dst = a.send + (uint64_t)p * kSlotU4;
+  dst[lane] = src[lane];
+  if (lane < 8) dst[64 + lane] = lane == 0 ? src[64] : make_uint4(0, 0, 0, 0);
+}
+
+// one wave per slot: zero-fill the slots no request took
+__global__ __launch_bounds__(256) void k_route_fill(RouteArgs a) {
+  const uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (j >= a.S * a.C) return;
+  const uint32_t d = j / a.C, r = j % a.C;
+  if (r < min(a.tot[d], a.C)) return;
+  uint4* dst = a.send + (uint64_t)j * kSlotU4;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  dst[lane] = z;
+  if (lane < 8) dst[64 + lane] = z;
+}
+
+// one wave per request: its response (slot layout) back to the caller layout
+__global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict__ pos,
+                                                      const uint4* __restrict__ back, uint32_t n,
+                                                      uint4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (i >= n) return;
+  const uint32_t p = pos[i];
+  if (p == kNone) return;  // overflowed batch: the call fails, out is undefined
+  const uint4* src = back + (uint64_t)p * kSlotU4;
+  out[(uint64_t)i * kAbiU4 + lane] = src[lane];
+  if (lane == 0) out[(uint64_t)i * kAbiU4 + 64] = src[64];
+}
+
+// single-process shards: OR of every shard's error word into each of them
+struct ErrSet {
+  uint32_t* e[kShardsMax];
+  uint32_t n;
+};
+__global__ void k_err_or(ErrSet s) {
+  if (threadIdx.x != 0) return;
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < s.n; ++k) v |= *s.e[k];
+  for (uint32_t k = 0; k < s.n; ++k) *s.e[k] = v;
+}
+
+}  // namespace gvs

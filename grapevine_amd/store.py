@@ -21,6 +21,7 @@ EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
     "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
+    "gvs_comm_unique_id", "gvs_create_sharded",
 )
 
 
@@ -42,6 +43,9 @@ def load_library(path=None):
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.gvs_config_init.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.c_uint64]
     lib.gvs_create.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.POINTER(vp)]
+    lib.gvs_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.gvs_create_sharded.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.c_char_p,
+                                       ctypes.POINTER(vp)]
     lib.gvs_destroy.argtypes = [vp]
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
@@ -64,14 +68,34 @@ def load_library(path=None):
     return lib
 
 
-class ObliviousStore:
-    """One store on one GPU (one handle; not thread-safe, like `&mut self`)."""
+def comm_unique_id():
+    """RCCL unique id for gvs_create_sharded (call on one rank, share with all)."""
+    buf = ctypes.create_string_buffer(abi.COMM_ID_BYTES)
+    rc = load_library().gvs_comm_unique_id(buf)
+    if rc != 0:
+        raise GvsError(rc, "gvs_comm_unique_id failed")
+    return buf.raw
 
-    def __init__(self, config):
+
+class ObliviousStore:
+    """One store handle (not thread-safe, like `&mut self`).
+
+    - `comm_id=None`, `config.shard_count <= 1`: one shard on one GPU.
+    - `comm_id=None`, `config.shard_count = S > 1`: all S shards on
+      `config.device` in this process (single-GPU test form of the sharded
+      store; a batch is the concatenation of S sources' batches).
+    - `comm_id` given: this process's shard `config.shard_index` of an
+      S-process store over RCCL; every call is collective.
+    """
+
+    def __init__(self, config, comm_id=None):
         self.lib = load_library()
         self.config = config
         h = ctypes.c_void_p()
-        rc = self.lib.gvs_create(ctypes.byref(config), ctypes.byref(h))
+        if comm_id is None:
+            rc = self.lib.gvs_create(ctypes.byref(config), ctypes.byref(h))
+        else:
+            rc = self.lib.gvs_create_sharded(ctypes.byref(config), comm_id, ctypes.byref(h))
         if rc != 0:
             raise GvsError(rc, "gvs_create failed (no GPU, bad config or out of memory)")
         self.h = h
@@ -112,7 +136,7 @@ class ObliviousStore:
         return {f: getattr(s, f) for f, _ in abi.GvsStats._fields_}
 
     def dump_messages(self):
-        n = self.config.msg_capacity
+        n = self.config.msg_capacity * self.stats()["shards"]
         out = np.zeros(n, dtype=abi.RECORD_DTYPE)
         self._check(self.lib.gvs_dump_messages(self.h, out.ctypes.data, n * 1024))
         return out

@@ -118,19 +118,25 @@ typedef struct gvs_response {
 /* ---- configuration ------------------------------------------------------- */
 
 typedef struct gvs_config {
-  uint64_t msg_capacity;        /* N message slots; power of two, >= 256 */
-  uint32_t mailbox_partitions;  /* Q; power of two */
+  uint64_t msg_capacity;        /* N message slots per shard; power of two, >= 256 */
+  uint32_t mailbox_partitions;  /* Q per shard; power of two */
   uint32_t mailbox_partition_slots; /* S_r mailboxes per partition; R = Q*S_r */
-  uint32_t max_batch;           /* B; power of two, 1024 .. 2^19 */
+  uint32_t max_batch;           /* B: requests per gvs_process_batch call (per rank
+                                   when sharded); power of two, 1024 .. 2^19 */
   uint32_t device;              /* HIP device ordinal */
-  uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key */
+  uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key;
+                                   identical on every shard */
   uint32_t flags;               /* reserved, must be 0 */
-  uint32_t reserved[7];         /* [0]: message rows per table-pass workgroup
-                                   (power of two 256..4096; 0 = automatic);
-                                   the rest must be 0 */
+  uint32_t rows_per_partition;  /* message rows per table-pass workgroup (power of
+                                   two 256..4096); 0 = automatic */
+  uint32_t shard_count;         /* S shards of the store (0 or 1 = unsharded) */
+  uint32_t shard_index;         /* this process's shard (gvs_create_sharded) */
+  uint32_t route_capacity;      /* C: request slots per (source, shard) pair and
+                                   batch; 0 = automatic */
+  uint32_t reserved[3];         /* must be 0 */
 } gvs_config;
 
-typedef struct gvs_stats {
+typedef struct gvs_stats {       /* summed over the handle's shards */
   uint64_t messages;            /* live messages */
   uint64_t mailboxes;           /* live mailboxes (recipients with messages) */
   uint64_t batches;             /* batches applied */
@@ -139,15 +145,38 @@ typedef struct gvs_stats {
   uint64_t free_ring_tail;
   uint64_t msg_partitions;      /* W: workgroups of the message-table pass */
   uint64_t msg_partition_slots; /* N / W */
+  uint64_t shards;              /* shards held by this handle */
+  uint64_t route_capacity;      /* C (0 when unsharded) */
+  uint64_t shard_batch;         /* requests each shard's pipeline processes per batch */
 } gvs_stats;
 
 typedef struct gvs_handle gvs_handle;
 
-/* Fill `cfg` with defaults for capacity N (R = N/16 mailboxes, B = 65536). */
+/* Fill `cfg` with defaults for capacity N (R = N/16 mailboxes, B = 65536,
+ * unsharded). */
 int gvs_config_init(gvs_config *cfg, uint64_t msg_capacity);
 
+/* Create a store.  With cfg->shard_count S > 1 the handle holds all S shards
+ * on cfg->device in this process and routes every batch through the same
+ * padded all-to-all as the multi-process form below, with device copies as
+ * the transport (single-GPU test mode: n <= S * max_batch requests per call,
+ * request k belongs to source rank k / max_batch). */
 int gvs_create(const gvs_config *cfg, gvs_handle **out);
 int gvs_destroy(gvs_handle *h);
+
+/* Multi-GPU store, one process per GPU.  Every rank calls
+ * gvs_create_sharded collectively with the same cfg except shard_index
+ * (= its rank) and device, and the same `comm_id` (from gvs_comm_unique_id on
+ * one rank, distributed by the caller).  Each gvs_process_batch call is then
+ * collective: every rank submits its own n <= max_batch requests; each
+ * request is routed to its owning shard inside fixed-size padded sub-batches
+ * (C slots per rank pair) over RCCL, and its response comes back to the rank
+ * that submitted it, in request order.  If any rank's requests for one shard
+ * exceed C, every rank returns GVS_ERR_BATCH_OVERFLOW and nothing is applied. */
+#define GVS_COMM_ID_BYTES 128
+int gvs_comm_unique_id(uint8_t out[GVS_COMM_ID_BYTES]);
+int gvs_create_sharded(const gvs_config *cfg, const uint8_t comm_id[GVS_COMM_ID_BYTES],
+                       gvs_handle **out);
 
 /* Process n <= max_batch requests (host memory) and write n responses in
  * request order.  Requests of one batch are linearised in the order defined
@@ -167,7 +196,8 @@ int gvs_access(gvs_handle *h, const gvs_request *req, gvs_response *out);
 
 int gvs_get_stats(gvs_handle *h, gvs_stats *out);
 
-/* Copy the raw message table (N * 1024 bytes) to host memory; test use. */
+/* Copy the slot-addressed message table (N * 1024 bytes per shard, shards in
+ * order) to host memory; test use. */
 int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
 
 /* Wait for all work on the handle's stream. */

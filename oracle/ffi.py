@@ -68,6 +68,29 @@ def lib():
             getattr(L, f).argtypes = [vp]
             getattr(L, f).restype = u64
         L.gvo_gen_batch.argtypes = [vp, ctypes.POINTER(GenParams), ctypes.POINTER(u64), vp, u32, u64]
+        L.gvo_id_encode_shard.argtypes = [ctypes.c_char_p, u32, u32, u64, ctypes.c_char_p]
+        L.gvo_id_decode_shard.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, u32,
+                                          ctypes.POINTER(u32), ctypes.POINTER(u32),
+                                          ctypes.POINTER(u64)]
+        L.gvo_id_decode_shard.restype = ctypes.c_int
+        L.gvo_route.argtypes = [ctypes.c_char_p, vp, u32, u32, u64]
+        L.gvo_route.restype = u32
+        L.gvo_route_capacity.argtypes = [u32, u32]
+        L.gvo_route_capacity.restype = u32
+        L.gvo_cluster_create.argtypes = [ctypes.POINTER(abi.GvsConfig)]
+        L.gvo_cluster_create.restype = vp
+        L.gvo_cluster_destroy.argtypes = [vp]
+        L.gvo_cluster_capacity.argtypes = [vp]
+        L.gvo_cluster_capacity.restype = u32
+        L.gvo_cluster_shard.argtypes = [vp, u32]
+        L.gvo_cluster_shard.restype = vp
+        L.gvo_cluster_process.argtypes = [vp, vp, u32, vp]
+        L.gvo_cluster_process.restype = ctypes.c_int
+        for f in ("gvo_cluster_messages", "gvo_cluster_mailboxes"):
+            getattr(L, f).argtypes = [vp]
+            getattr(L, f).restype = u64
+        L.gvo_cluster_gen_batch.argtypes = [vp, ctypes.POINTER(GenParams), ctypes.POINTER(u64),
+                                            vp, u32, u64]
         _LIB = L
     return _LIB
 
@@ -88,6 +111,33 @@ def id_decode(key16: bytes, msg_id: bytes, n_slots: int):
     s, c = ctypes.c_uint32(), ctypes.c_uint64()
     ok = lib().gvo_id_decode(key16, msg_id, n_slots, ctypes.byref(s), ctypes.byref(c))
     return (s.value, c.value) if ok else None
+
+
+def id_encode_shard(key16: bytes, shard: int, slot: int, ctr: int) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().gvo_id_encode_shard(key16, shard, slot, ctr, out)
+    return out.raw
+
+
+def id_decode_shard(key16: bytes, msg_id: bytes, n_slots: int, n_shards: int):
+    sh, s, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    ok = lib().gvo_id_decode_shard(key16, msg_id, n_slots, n_shards, ctypes.byref(sh),
+                                   ctypes.byref(s), ctypes.byref(c))
+    return (sh.value, s.value, c.value) if ok else None
+
+
+def route(config, reqs):
+    """Owning shard of each request (index i = position in its source batch)."""
+    reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+    key = bytes(config.secret_key)
+    B = config.max_batch
+    return np.array([lib().gvo_route(key, reqs[i:i + 1].ctypes.data, i % B, config.shard_count,
+                                     config.msg_capacity) for i in range(len(reqs))],
+                    dtype=np.uint32)
+
+
+def route_capacity(batch, n_shards):
+    return lib().gvo_route_capacity(batch, n_shards)
 
 
 def identity(i: int) -> bytes:
@@ -169,6 +219,87 @@ class Model:
         if self.L.gvo_live_message(self.m, i, rec.ctypes.data) != 0:
             raise IndexError(i)
         return rec[0]
+
+
+class _ShardView(Model):
+    """A shard model owned by a Cluster (not freed on its own)."""
+
+    def __init__(self, cluster, ptr, config):
+        self.L = cluster.L
+        self.config = config
+        self.m = ptr
+        self.rng = ctypes.c_uint64(0)
+        self.ops = 0
+
+    def close(self):
+        self.m = None
+
+
+class Cluster:
+    """S shard seqmodels behind the engine's routing: the
+    oracle of a sharded store.  A batch of n <= S*max_batch requests is the
+    concatenation of the sources' batches (source k = [k*B, (k+1)*B))."""
+
+    def __init__(self, config):
+        self.L = lib()
+        self.config = config
+        self.c = self.L.gvo_cluster_create(ctypes.byref(config))
+        if not self.c:
+            raise ValueError("invalid oracle cluster config")
+        self.S = config.shard_count
+        self.capacity = self.L.gvo_cluster_capacity(self.c)
+        self.rng = ctypes.c_uint64(0)
+        self.ops = 0
+
+    def close(self):
+        if self.c:
+            self.L.gvo_cluster_destroy(self.c)
+            self.c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def shard(self, k):
+        return _ShardView(self, self.L.gvo_cluster_shard(self.c, k), self.config)
+
+    def process_batch(self, reqs):
+        """-> responses, or None when the batch overflows a (source, shard) bucket."""
+        reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+        out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
+        rc = self.L.gvo_cluster_process(self.c, reqs.ctypes.data, len(reqs), out.ctypes.data)
+        if rc == abi.GVS_ERR_BATCH_OVERFLOW:
+            return None
+        if rc != 0:
+            raise ValueError(f"oracle cluster rejected batch: {rc}")
+        return out
+
+    def seed(self, s):
+        self.rng = ctypes.c_uint64(s)
+
+    def gen_batch(self, n, params):
+        reqs = np.zeros(n, dtype=abi.REQUEST_DTYPE)
+        self.L.gvo_cluster_gen_batch(self.c, ctypes.byref(params), ctypes.byref(self.rng),
+                                     reqs.ctypes.data, n, self.ops)
+        self.ops += n
+        return reqs
+
+    @property
+    def messages(self):
+        return self.L.gvo_cluster_messages(self.c)
+
+    @property
+    def mailboxes(self):
+        return self.L.gvo_cluster_mailboxes(self.c)
+
+    @property
+    def creation_counter(self):
+        return sum(self.shard(k).creation_counter for k in range(self.S))
+
+    def dump_messages(self):
+        return np.concatenate([self.shard(k).dump_messages() for k in range(self.S)])
 
 
 class PathOramModel:

@@ -8,6 +8,7 @@
  */
 #include "gvs_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -76,9 +77,14 @@ static uint64_t feistel_f(const uint8_t key[16], int r, uint64_t x) {
   return gvo_siphash24(ld64(key), ld64(key + 8), msg, 16);
 }
 
-void gvo_id_encode(const uint8_t key[16], uint32_t slot, uint64_t ctr,
-                   uint8_t out[16]) {
-  uint64_t L = (uint64_t)slot | ((uint64_t)ID_TAG << 32), R = ctr;
+/* [D] shard k of a sharded store issues ids with tag ID_TAG ^ k << 8, so an
+ * id names its shard; shard 0 and the unsharded store use
+ * ID_TAG itself. */
+static uint32_t shard_tag(uint32_t shard) { return ID_TAG ^ (shard << 8); }
+
+void gvo_id_encode_shard(const uint8_t key[16], uint32_t shard, uint32_t slot, uint64_t ctr,
+                         uint8_t out[16]) {
+  uint64_t L = (uint64_t)slot | ((uint64_t)shard_tag(shard) << 32), R = ctr;
   for (int r = 0; r < 4; ++r) {
     uint64_t nl = R, nr = L ^ feistel_f(key, r, R);
     L = nl;
@@ -88,19 +94,39 @@ void gvo_id_encode(const uint8_t key[16], uint32_t slot, uint64_t ctr,
   st64(out + 8, R);
 }
 
-int gvo_id_decode(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
-                  uint32_t *slot, uint64_t *ctr) {
+void gvo_id_encode(const uint8_t key[16], uint32_t slot, uint64_t ctr, uint8_t out[16]) {
+  gvo_id_encode_shard(key, 0, slot, ctr, out);
+}
+
+static void id_plain(const uint8_t key[16], const uint8_t id[16], uint64_t *Lo, uint64_t *Ro) {
   uint64_t L = ld64(id), R = ld64(id + 8);
   for (int r = 3; r >= 0; --r) {
     uint64_t nl = R ^ feistel_f(key, r, L), nr = L;
     L = nl;
     R = nr;
   }
-  if ((uint32_t)(L >> 32) != ID_TAG) return 0;
+  *Lo = L;
+  *Ro = R;
+}
+
+int gvo_id_decode_shard(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
+                        uint32_t n_shards, uint32_t *shard, uint32_t *slot, uint64_t *ctr) {
+  uint64_t L, R;
+  id_plain(key, id, &L, &R);
+  uint32_t t = (uint32_t)(L >> 32) ^ ID_TAG;
+  if ((t & 0xFF0000FFu) != 0) return 0;
+  if ((t >> 8) >= (n_shards ? n_shards : 1u)) return 0;
   if ((uint64_t)(uint32_t)L >= n_slots) return 0;
+  *shard = t >> 8;
   *slot = (uint32_t)L;
   *ctr = R;
   return 1;
+}
+
+int gvo_id_decode(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
+                  uint32_t *slot, uint64_t *ctr) {
+  uint32_t shard;
+  return gvo_id_decode_shard(key, id, n_slots, 1, &shard, slot, ctr);
 }
 
 /* recipient PRF: (h_hi, h_lo) = SipHash(X || 1), SipHash(X || 2); the
@@ -125,6 +151,7 @@ typedef struct mailbox {
 
 struct gvo_model {
   gvs_config cfg;
+  uint32_t shard;  /* index in a sharded store (tag of the ids it issues) */
   uint64_t N;
   uint32_t Q, Sr, B, logQ;
   uint8_t prp_key[16], hash_key[16];
@@ -154,6 +181,7 @@ gvo_model *gvo_create(const gvs_config *cfg) {
   gvo_model *m = (gvo_model *)calloc(1, sizeof *m);
   if (!m) return NULL;
   m->cfg = *cfg;
+  m->shard = cfg->shard_count > 1 ? cfg->shard_index : 0;
   m->N = cfg->msg_capacity;
   m->Q = cfg->mailbox_partitions;
   m->Sr = cfg->mailbox_partition_slots;
@@ -219,9 +247,10 @@ static void remove_mailbox(gvo_model *m, mailbox *mb) {
 }
 
 static gvs_record *lookup(gvo_model *m, const uint8_t id[16], uint32_t *slot_out) {
-  uint32_t slot;
+  uint32_t slot, shard;
   uint64_t ctr;
-  if (!gvo_id_decode(m->prp_key, id, m->N, &slot, &ctr)) return NULL;
+  if (!gvo_id_decode_shard(m->prp_key, id, m->N, 1u << 16, &shard, &slot, &ctr)) return NULL;
+  if (shard != m->shard) return NULL; /* issued by another shard */
   gvs_record *r = &m->table[slot];
   if (memcmp(r->msg_id, id, 16) != 0) return NULL;
   if (slot_out) *slot_out = slot;
@@ -291,7 +320,7 @@ static void do_create(gvo_model *m, const gvs_request *rq, gvs_response *o) {
   m->head++;
   uint64_t ctr = m->ctr++;
   gvs_record *r = &m->table[slot];
-  gvo_id_encode(m->prp_key, slot, ctr, r->msg_id);
+  gvo_id_encode_shard(m->prp_key, m->shard, slot, ctr, r->msg_id);
   memcpy(r->sender, rq->auth_identity, 32); /* sender = auth_identity */
   memcpy(r->recipient, rq->recipient, 32);
   r->timestamp = rq->timestamp; /* server time, README.md:143-144 */
@@ -503,8 +532,18 @@ void gvo_identity(uint32_t i, uint8_t out[32]) {
   for (int j = 0; j < 4; ++j) st64(out + 8 * j, splitmix64(&s) | 1u);
 }
 
-void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
-                   gvs_request *reqs, uint32_t n, uint64_t op_base) {
+/* a model to draw a live message from: the only one, or (sharded store) one
+ * chosen uniformly; NULL when it holds no message */
+static const gvo_model *pick_model(const gvo_model *const *ms, uint32_t nm, uint64_t *rng) {
+  const gvo_model *m = nm > 1 ? ms[rnd_below(rng, nm)] : ms[0];
+  return m->n_live ? m : NULL;
+}
+static const gvs_record *pick_live(const gvo_model *m, uint64_t *rng) {
+  return &m->table[m->live[rnd_below(rng, (uint32_t)m->n_live)]];
+}
+
+static void gen_requests(const gvo_model *const *ms, uint32_t nm, const gvo_gen_params *p,
+                         uint64_t *rng, gvs_request *reqs, uint32_t n, uint64_t op_base) {
   uint32_t nid = p->n_identities ? p->n_identities : 1;
   for (uint32_t i = 0; i < n; ++i) {
     gvs_request *rq = &reqs[i];
@@ -537,16 +576,18 @@ void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
     }
     if (t != GVS_REQUEST_UPDATE && rnd_below(rng, 100) < p->pct_next) {
       memset(rq->msg_id, 0, 16);
-      if (hot) gvo_identity(0, rq->auth_identity);
-      else if (m->n_live && rnd_below(rng, 100) < 70) {
-        const gvs_record *lr = &m->table[m->live[rnd_below(rng, (uint32_t)m->n_live)]];
-        memcpy(rq->auth_identity, lr->recipient, 32);
+      if (hot) {
+        gvo_identity(0, rq->auth_identity);
+      } else {
+        const gvo_model *m = pick_model(ms, nm, rng);
+        if (m && rnd_below(rng, 100) < 70) memcpy(rq->auth_identity, pick_live(m, rng)->recipient, 32);
       }
       continue;
     }
     /* by-id operation */
-    if (m->n_live && rnd_below(rng, 100) >= p->pct_miss) {
-      const gvs_record *lr = &m->table[m->live[rnd_below(rng, (uint32_t)m->n_live)]];
+    const gvo_model *m = pick_model(ms, nm, rng);
+    if (m && rnd_below(rng, 100) >= p->pct_miss) {
+      const gvs_record *lr = pick_live(m, rng);
       memcpy(rq->msg_id, lr->msg_id, 16);
       if (rnd_below(rng, 100) >= p->pct_bad_auth)
         memcpy(rq->auth_identity, rnd_below(rng, 2) ? lr->sender : lr->recipient, 32);
@@ -556,4 +597,146 @@ void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
       rq->msg_id[0] |= 1; /* random, nonzero, almost surely absent */
     }
   }
+}
+
+void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
+                   gvs_request *reqs, uint32_t n, uint64_t op_base) {
+  gen_requests(&m, 1, p, rng, reqs, n, op_base);
+}
+
+/* ------------------------------------------------------ sharded store [D] */
+/* DESIGN.md §6.  A message lives on the shard that owns its recipient's
+ * mailbox, so every request touches exactly one shard; the routing rule is
+ * restated here from grapevine_amd/csrc/gvs_route.h (route_dest).  Requests
+ * of one batch reach a shard in (source rank, submission index) order, which
+ * is global submission order, and each shard linearises its sub-batch as
+ * gvo_process_batch does.  Shards share no state, so the result is a valid
+ * linearisation of the whole batch. */
+
+uint32_t gvo_route(const uint8_t key[32], const gvs_request *rq, uint32_t i, uint32_t n_shards,
+                   uint64_t n_slots) {
+  const uint32_t S = n_shards ? n_shards : 1u;
+  const uint32_t spread = i % S;
+  const uint32_t t = rq->request_type;
+  const int id_zero = is_zero(rq->msg_id, 16);
+  if (is_hard_error(rq)) return spread;
+  const int next = (t == GVS_REQUEST_READ || t == GVS_REQUEST_DELETE) && id_zero;
+  uint64_t hi, lo;
+  if (t == GVS_REQUEST_CREATE) {
+    if (is_zero(rq->recipient, 32)) return spread;
+    gvo_recipient_hash(key + 16, rq->recipient, &hi, &lo);
+    return (uint32_t)(lo & 0xFFFFu) % S;
+  }
+  if (next) {
+    gvo_recipient_hash(key + 16, rq->auth_identity, &hi, &lo);
+    return (uint32_t)(lo & 0xFFFFu) % S;
+  }
+  uint32_t shard, slot;
+  uint64_t ctr;
+  if (gvo_id_decode_shard(key, rq->msg_id, n_slots, S, &shard, &slot, &ctr)) return shard;
+  return spread;
+}
+
+uint32_t gvo_route_capacity(uint32_t batch, uint32_t n_shards) {
+  if (n_shards <= 1) return batch;
+  double mu = (double)((batch + n_shards - 1) / n_shards);
+  uint64_t c = (uint64_t)ceil(mu + 8.0 * sqrt(mu) + 64.0);
+  c = (c + 63) / 64 * 64;
+  return (uint32_t)(c < batch ? c : batch);
+}
+
+struct gvo_cluster {
+  gvs_config cfg;
+  uint32_t S, C, B;
+  gvo_model **shard;
+  gvs_request *sub;
+  gvs_response *subout;
+  uint32_t *dest, *cnt;
+};
+
+gvo_cluster *gvo_cluster_create(const gvs_config *cfg) {
+  if (!cfg || cfg->shard_count < 1) return NULL;
+  gvo_cluster *c = (gvo_cluster *)calloc(1, sizeof *c);
+  if (!c) return NULL;
+  c->cfg = *cfg;
+  c->S = cfg->shard_count;
+  c->B = cfg->max_batch;
+  c->C = cfg->route_capacity ? cfg->route_capacity : gvo_route_capacity(c->B, c->S);
+  c->shard = (gvo_model **)calloc(c->S, sizeof(gvo_model *));
+  c->sub = (gvs_request *)malloc((size_t)c->S * c->C * sizeof(gvs_request));
+  c->subout = (gvs_response *)malloc((size_t)c->S * c->C * sizeof(gvs_response));
+  c->dest = (uint32_t *)malloc((size_t)c->S * c->B * sizeof(uint32_t));
+  c->cnt = (uint32_t *)malloc((size_t)c->S * c->S * sizeof(uint32_t));
+  if (!c->shard || !c->sub || !c->subout || !c->dest || !c->cnt) {
+    gvo_cluster_destroy(c);
+    return NULL;
+  }
+  for (uint32_t k = 0; k < c->S; ++k) {
+    gvs_config sc = *cfg;
+    sc.shard_count = c->S;
+    sc.shard_index = k;
+    uint32_t be = 1024;
+    while (be < c->S * c->C) be <<= 1;
+    sc.max_batch = be;
+    c->shard[k] = gvo_create(&sc);
+    if (!c->shard[k]) {
+      gvo_cluster_destroy(c);
+      return NULL;
+    }
+  }
+  return c;
+}
+
+void gvo_cluster_destroy(gvo_cluster *c) {
+  if (!c) return;
+  if (c->shard)
+    for (uint32_t k = 0; k < c->S; ++k) gvo_destroy(c->shard[k]);
+  free(c->shard);
+  free(c->sub);
+  free(c->subout);
+  free(c->dest);
+  free(c->cnt);
+  free(c);
+}
+
+uint32_t gvo_cluster_capacity(const gvo_cluster *c) { return c->C; }
+gvo_model *gvo_cluster_shard(gvo_cluster *c, uint32_t k) { return k < c->S ? c->shard[k] : NULL; }
+
+/* n <= S*B requests; source rank k submitted [k*B, (k+1)*B) */
+int gvo_cluster_process(gvo_cluster *c, const gvs_request *reqs, uint32_t n, gvs_response *out) {
+  if (n > c->S * c->B) return GVS_ERR_INVALID_ARG;
+  memset(c->cnt, 0, (size_t)c->S * c->S * sizeof(uint32_t));
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t src = i / c->B, d = gvo_route(c->cfg.secret_key, &reqs[i], i % c->B, c->S,
+                                           c->cfg.msg_capacity);
+    c->dest[i] = d;
+    if (++c->cnt[src * c->S + d] > c->C) return GVS_ERR_BATCH_OVERFLOW; /* nothing applied */
+  }
+  for (uint32_t d = 0; d < c->S; ++d) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      if (c->dest[i] == d) c->sub[m++] = reqs[i];
+    int rc = gvo_process_batch(c->shard[d], c->sub, m, c->subout);
+    if (rc) return rc;
+    m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      if (c->dest[i] == d) out[i] = c->subout[m++];
+  }
+  return GVS_OK;
+}
+
+uint64_t gvo_cluster_messages(const gvo_cluster *c) {
+  uint64_t t = 0;
+  for (uint32_t k = 0; k < c->S; ++k) t += c->shard[k]->count;
+  return t;
+}
+uint64_t gvo_cluster_mailboxes(const gvo_cluster *c) {
+  uint64_t t = 0;
+  for (uint32_t k = 0; k < c->S; ++k) t += c->shard[k]->n_mailboxes;
+  return t;
+}
+
+void gvo_cluster_gen_batch(const gvo_cluster *c, const gvo_gen_params *p, uint64_t *rng,
+                           gvs_request *reqs, uint32_t n, uint64_t op_base) {
+  gen_requests((const gvo_model *const *)c->shard, c->S, p, rng, reqs, n, op_base);
 }

@@ -44,6 +44,11 @@ uint64_t gvo_siphash24(uint64_t k0, uint64_t k1, const uint8_t *m, size_t len);
 /* 4-round Feistel PRP over 128 bits used for message ids. */
 void gvo_id_encode(const uint8_t key[16], uint32_t slot, uint64_t ctr,
                    uint8_t out[16]);
+/* The same for shard `shard` of a sharded store (tag ID_TAG ^ shard << 8). */
+void gvo_id_encode_shard(const uint8_t key[16], uint32_t shard, uint32_t slot, uint64_t ctr,
+                         uint8_t out[16]);
+int gvo_id_decode_shard(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
+                        uint32_t n_shards, uint32_t *shard, uint32_t *slot, uint64_t *ctr);
 /* returns 1 if the id decodes to (slot < n_slots, tag ok) */
 int gvo_id_decode(const uint8_t key[16], const uint8_t id[16], uint64_t n_slots,
                   uint32_t *slot, uint64_t *ctr);
@@ -73,6 +78,26 @@ uint64_t gvo_state_digest(const gvo_model *m);
 void gvo_identity(uint32_t i, uint8_t out[32]);
 void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
                    gvs_request *reqs, uint32_t n, uint64_t op_base);
+
+/* Sharded store: S seqmodels behind the engine's routing rule
+ * and its fixed per-(source, shard) capacity C.  `key` is the 32-byte secret
+ * key of gvs_config. */
+uint32_t gvo_route(const uint8_t key[32], const gvs_request *rq, uint32_t i, uint32_t n_shards,
+                   uint64_t n_slots);
+uint32_t gvo_route_capacity(uint32_t batch, uint32_t n_shards);
+typedef struct gvo_cluster gvo_cluster;
+gvo_cluster *gvo_cluster_create(const gvs_config *cfg); /* cfg->shard_count shards */
+void gvo_cluster_destroy(gvo_cluster *c);
+uint32_t gvo_cluster_capacity(const gvo_cluster *c);
+gvo_model *gvo_cluster_shard(gvo_cluster *c, uint32_t k);
+/* n <= S * max_batch; source rank k submitted requests [k*B, (k+1)*B).
+ * GVS_ERR_BATCH_OVERFLOW (nothing applied) if one source has more than C
+ * requests for one shard. */
+int gvo_cluster_process(gvo_cluster *c, const gvs_request *reqs, uint32_t n, gvs_response *out);
+uint64_t gvo_cluster_messages(const gvo_cluster *c);
+uint64_t gvo_cluster_mailboxes(const gvo_cluster *c);
+void gvo_cluster_gen_batch(const gvo_cluster *c, const gvo_gen_params *p, uint64_t *rng,
+                           gvs_request *reqs, uint32_t n, uint64_t op_base);
 
 /* Path ORAM restatement of the reference's CPU path (gvs_pathoram.c): the
  * same handler semantics over three Path ORAMs; the timed CPU baseline. */

@@ -17,6 +17,8 @@ def describe_request(r):
 def diff_responses(got, want, reqs, limit=8):
     """Return a human-readable list of mismatching responses (empty if equal)."""
     n = len(want)
+    if n == 0:
+        return [] if len(got) == 0 else [f"{len(got)} responses for an empty batch"]
     g = got.view(np.uint8).reshape(n, -1)
     w = want.view(np.uint8).reshape(n, -1)
     bad = np.nonzero((g != w).any(axis=1))[0]

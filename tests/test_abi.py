@@ -36,6 +36,7 @@ def test_pod_sizes_match_header():
     assert "GVS_PAYLOAD_BYTES 936" in hdr and "GVS_MAILBOX_SLOTS 62" in hdr
     assert abi.REQUEST_DTYPE.itemsize == 1040 and abi.RESPONSE_DTYPE.itemsize == 1040
     assert ctypes.sizeof(abi.GvsConfig) == 8 + 4 * 4 + 32 + 4 + 28
+    assert ctypes.sizeof(abi.GvsStats) == 11 * 8
 
 
 def test_config_init_and_version_without_gpu():
@@ -55,4 +56,15 @@ def test_invalid_configs_rejected_before_device_use():
     bad = abi.make_config(4096, max_batch=100)  # not a power of two
     assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
     bad = abi.make_config(4096, mailbox_partition_slots=2048)
+    assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
+
+
+def test_invalid_sharded_configs_rejected_before_device_use():
+    lib = load_library()
+    h = ctypes.c_void_p()
+    bad = abi.make_config(4096, max_batch=1024, shard_count=65)  # more than kShardsMax
+    assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
+    bad = abi.make_config(4096, max_batch=1024, shard_count=2, route_capacity=2048)  # C > B
+    assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
+    bad = abi.make_config(4096, max_batch=1024, rows_per_partition=100)
     assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG

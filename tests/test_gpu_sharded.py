@@ -1,0 +1,94 @@
+"""GPU parity of the sharded store against the oracle's cluster
+model (oracle/gvs_oracle.c gvo_cluster_*), bit for bit: responses, per-shard
+message tables, live counts.
+
+The single-GPU box runs the S-shard store in its single-process form (all
+shards on one device, the all-to-all done with device copies), which drives
+the same router, padded sub-batches and shard pipelines as the multi-process
+form; the RCCL transport itself is exercised with one rank (send/recv to
+self, error max-reduction)."""
+import numpy as np
+import pytest
+
+from grapevine_amd import abi
+from grapevine_amd.store import GvsError, ObliviousStore, comm_unique_id
+from oracle import ffi
+
+from parity import diff_responses, run_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def sharded_pair(S, N=4096, B=1024, Q=16, Sr=32, C=0):
+    cfg = abi.make_config(N, mailbox_partitions=Q, mailbox_partition_slots=Sr, max_batch=B,
+                          shard_count=S, route_capacity=C)
+    return ObliviousStore(cfg), ffi.Cluster(cfg)
+
+
+@pytest.mark.parametrize("S", [2, 4])
+def test_local_shards_mixed_stream(S):
+    store, cl = sharded_pair(S)
+    cl.seed(40 + S)
+    st = store.stats()
+    assert st["shards"] == S and st["route_capacity"] == cl.capacity
+    seen = run_stream(store, cl, ffi.gen_params(n_identities=400, hard_error=2, zero_recipient=2),
+                      batches=8, n=S * 1024)
+    assert {0, 1, 2, 4} <= set(seen), seen
+
+
+def test_local_shards_partial_batches():
+    S = 4
+    store, cl = sharded_pair(S)
+    cl.seed(47)
+    p = ffi.gen_params(n_identities=300)
+    for n in (S * 1024, 1, 1500, 3 * 1024 + 5, 0, S * 1024):
+        reqs = cl.gen_batch(n, p)
+        want = cl.process_batch(reqs)
+        got = store.process_batch(reqs)
+        d = diff_responses(got, want, reqs)
+        assert not d, f"n={n}: " + "\n".join(d)
+    assert store.stats()["messages"] == cl.messages
+
+
+def test_local_shards_drain_and_capacity():
+    S = 2
+    store, cl = sharded_pair(S, N=1024, Q=4, Sr=64, C=1024)
+    cl.seed(48)
+    run_stream(store, cl, ffi.gen_params(create=95, read=5, update=0, delete=0, n_identities=150),
+               batches=3, n=S * 1024)
+    run_stream(store, cl, ffi.gen_params(create=5, read=30, update=15, delete=50, nxt=70,
+                                         n_identities=150), batches=4, n=S * 1024)
+
+
+def test_local_shards_bucket_overflow_applies_nothing():
+    S = 4
+    store, cl = sharded_pair(S, C=320)
+    cl.seed(49)
+    run_stream(store, cl, ffi.gen_params(n_identities=300), batches=2, n=S * 1024)
+    before = store.dump_messages()
+    msgs = store.stats()["messages"]
+    hot = cl.gen_batch(S * 1024, ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60,
+                                                n_identities=300))
+    assert cl.process_batch(hot) is None
+    with pytest.raises(GvsError) as ei:
+        store.process_batch(hot)
+    assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW
+    assert store.stats()["messages"] == msgs
+    assert store.dump_messages().tobytes() == before.tobytes()
+    # the store keeps working after a rejected batch
+    run_stream(store, cl, ffi.gen_params(n_identities=300), batches=2, n=S * 1024)
+
+
+def test_rccl_single_rank_routed_path():
+    """gvs_create_sharded with one rank: router, RCCL send/recv to self and the
+    error all-reduce on the data path; must equal the unsharded oracle."""
+    import os
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024,
+                          shard_count=1, shard_index=0)
+    store = ObliviousStore(cfg, comm_id=comm_unique_id())
+    model = ffi.Model(abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32,
+                                      max_batch=1024))
+    model.seed(50)
+    run_stream(store, model, ffi.gen_params(n_identities=300), batches=6, n=1024)
+    store.close()

@@ -46,7 +46,7 @@ def run(torch, abi, ObliviousStore, log2n, variants, S):
     dev = torch.device("cuda", 0)
     N, B = 1 << log2n, 65536
     cfg = abi.make_config(N, max_batch=B)
-    cfg.reserved[0] = S
+    cfg.rows_per_partition = S
     store = ObliviousStore(cfg)
     print(f"rows per partition {store.stats()['msg_partition_slots']}, partitions {store.stats()['msg_partitions']}", flush=True)
     g = torch.Generator(device=dev)
