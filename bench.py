@@ -8,9 +8,13 @@ requests already resident in HBM.  Default workload = BASELINE config 3:
 25/25/25/25 CREATE/READ/UPDATE/DELETE mix with half of the READ/DELETE asking
 for the next message (zero id), as SURVEY.md §8(d) specifies.
 
-Multi-GPU (`torch.distributed.run`): one process per GPU, each owning an
-independent store shard serving its own batches (weak scaling, no data-path
-collective in this round).  Rank 0 prints one JSON line.
+Multi-GPU (`torch.distributed.run`): one process per GPU, each owning one
+shard of a single sharded store (gvs_create_sharded).  Every
+rank submits its own 64K-request batch per step; the engine routes each
+request to the shard that owns it inside fixed-size padded sub-batches over
+RCCL send/recv (xGMI) and returns the responses to the submitting rank.
+Per-GPU work is fixed as N grows (2^24 messages and 64K requests per GPU):
+weak scaling.  Rank 0 prints one JSON line.
 """
 import argparse
 import ctypes
@@ -36,6 +40,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline instances (host threads)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--routed", action="store_true",
+                   help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
 
@@ -149,21 +155,34 @@ def cpu_baseline(budget_s, threads):
 
 def main():
     a = parse()
+    # RCCL prints a version banner on stdout at communicator creation; keep
+    # stdout for the single JSON line and send everything else to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     from grapevine_amd import abi, dist as gdist
     from grapevine_amd.store import ObliviousStore
+
+    from grapevine_amd.store import comm_unique_id
 
     ri = gdist.rank_info()
     world, rank, local = ri.world, ri.rank, ri.local
     if world > 1:
         torch.cuda.set_device(local)
-    gdist.init("nccl")  # RCCL; used only for the barrier and the max-time reduction
+    gdist.init("nccl")  # torch's RCCL: comm-id broadcast, barriers, max-time reduction
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     N, B = 1 << a.log2n, a.batch
-    cfg = abi.make_config(N, max_batch=B, device=local)
-    store = ObliviousStore(cfg)
+    if world > 1 or a.routed:
+        # one shard per rank; the store's own RCCL communicator carries the data path
+        cfg = abi.make_config(N, max_batch=B, device=local, shard_count=world, shard_index=rank)
+        cid = gdist.broadcast_bytes(ri, comm_unique_id() if rank == 0 else None, device=dev)
+        store = ObliviousStore(cfg, comm_id=cid)
+    else:
+        cfg = abi.make_config(N, max_batch=B, device=local)
+        store = ObliviousStore(cfg)
+    shard_batch = store.stats()["shard_batch"]
     g = torch.Generator(device=dev)
     g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
@@ -196,14 +215,16 @@ def main():
         total = world * B * a.steps
         rpass_ms = stage_ms.get("rpass", float("nan"))
         # algorithmic bytes of one message-table pass: every row
-        # read + written, every request image read, every response written
-        alg_bytes = 2 * N * 1024 + B * (1024 + 1040)
+        # read + written, every op's request image read and response written
+        # (a shard's pipeline processes shard_batch ops: B, or the padded
+        # sub-batches of all sources when sharded)
+        alg_bytes = 2 * N * 1024 + shard_batch * (1024 + 1040)
         achieved = alg_bytes / (rpass_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("log2n") == a.log2n and tj.get("batch") == B:
+            if tj.get("log2n") == a.log2n and tj.get("batch") == B and world == 1:
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -224,7 +245,9 @@ def main():
             "config": {"workload": f"C3: 2^{a.log2n} message capacity per GPU, {B}-request batches",
                        "msg_capacity": N, "batch": B,
                        "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,
-                       "parallelism": f"shards{world}"},
+                       "parallelism": f"shards{world}",
+                       "route_capacity": store.stats()["route_capacity"],
+                       "shard_batch": shard_batch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rpass (message-table pass)",
@@ -234,7 +257,8 @@ def main():
             "store": {"messages": st["messages"], "mailboxes": st["mailboxes"],
                       "last_batch_status_hist": statuses},
         }
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     store.close()
     gdist.finalize(ri)
 

@@ -1,7 +1,8 @@
-"""Multi-GPU plumbing for the store: one process per GPU, each owning an
-independent shard.  torch.distributed is plumbing only: a
-barrier around the timed region and a max-over-ranks reduction of the elapsed
-time.  No collective is on the data path in this round."""
+"""Multi-GPU plumbing for the store: one process per GPU, each owning one shard
+(DESIGN.md §6).  torch.distributed is plumbing only: it hands the store's
+RCCL unique id from rank 0 to every rank, and gives a barrier around the timed
+region and a max-over-ranks reduction of the elapsed time.  The data path's
+all-to-all runs on the store's own RCCL communicator inside libgvstore.so."""
 import os
 from dataclasses import dataclass
 
@@ -58,6 +59,21 @@ def sum_over_ranks(ri, value, device=None):
     t = torch.tensor([int(value)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def broadcast_bytes(ri, data, device=None):
+    """rank 0's `data` (bytes) on every rank."""
+    if ri.world == 1:
+        return data
+    import torch
+    import torch.distributed as dist
+    n = torch.tensor([len(data) if ri.rank == 0 else 0], dtype=torch.int64, device=device)
+    dist.broadcast(n, 0)
+    buf = torch.zeros(int(n.item()), dtype=torch.uint8, device=device)
+    if ri.rank == 0:
+        buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    dist.broadcast(buf, 0)
+    return bytes(buf.cpu().numpy().tobytes())
 
 
 def finalize(ri):

@@ -93,3 +93,19 @@ def test_c2_scale_stream():
     run_stream(store, model, p, batches=6, n=4096, check_table=False)
     p = ffi.gen_params(n_identities=20000)
     run_stream(store, model, p, batches=4, n=4096, check_table=True)
+
+
+@pytest.mark.parametrize("name", ["single_mixed", "single_full", "sharded4"])
+def test_golden_fixtures(name):
+    """The HIP engine against the committed fixtures (tests/golden/), with no
+    oracle in the loop."""
+    from golden_io import load
+    cfg, batches = load(name)
+    store = ObliviousStore(cfg)
+    for k, (reqs, want, (msgs, mboxes)) in enumerate(batches):
+        got = store.process_batch(reqs)
+        d = diff_responses(got, want, reqs)
+        assert not d, f"{name} batch {k}: " + "\n".join(d)
+        st = store.stats()
+        assert (st["messages"], st["mailboxes"]) == (msgs, mboxes), (name, k)
+    store.close()

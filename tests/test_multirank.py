@@ -1,36 +1,82 @@
-"""N>1 path on CPU (gloo, world size 2): each rank owns an independent shard
-and serves its own seeded stream; the job time is the max over ranks and the
-aggregate is the sum (what bench.py does over RCCL on GPUs)."""
+"""N>1 path on CPU (gloo, world size 2 and 4): the sharded store's protocol of
+DESIGN.md §6 run as one process per rank, with the oracle standing in for
+each rank's shard pipeline.
+
+Each rank owns shard `rank`.  Every step, each rank takes its own batch,
+routes each request to its owning shard (the engine's rule, restated in
+oracle/gvs_oracle.c gvo_route) into S buckets of exactly C slots padded with
+zero requests, exchanges the buckets with all_to_all, runs its shard on the
+S*C received slots, returns the responses with a second all_to_all and puts
+them back in request order.  The result must equal the single-process
+cluster model on the concatenated batch, rank by rank and bit for bit, and
+every shard's state must equal the cluster's shard.  Timing follows bench.py
+(barrier, max over ranks)."""
+import json
 import os
 import socket
 import subprocess
 import sys
 import textwrap
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 WORKER = textwrap.dedent("""
     import os, sys, time, json
+    import numpy as np
+    import torch
+    import torch.distributed as dist
     sys.path.insert(0, {root!r})
     from grapevine_amd import abi, dist as gdist
     from oracle import ffi
     ri = gdist.init("gloo")
-    cfg = abi.make_config(4096, mailbox_partitions=8, mailbox_partition_slots=32, max_batch=1024)
-    shard = ffi.Model(cfg)                       # this rank's shard (CPU stand-in)
-    shard.seed(gdist.shard_seed(1234, ri.rank))
-    p = ffi.gen_params(n_identities=300)
+    S, r, B = ri.world, ri.rank, 1024
+    base = dict(mailbox_partitions=8, mailbox_partition_slots=32, max_batch=B, shard_count=S)
+    ccfg = abi.make_config(4096, **base)
+    replica = ffi.Cluster(ccfg)              # whole-store oracle, identical on every rank
+    C = replica.capacity
+    be = 1024
+    while be < S * C:
+        be *= 2
+    scfg = abi.make_config(4096, **dict(base, max_batch=be, shard_index=r))
+    shard = ffi.Model(scfg)                  # this rank's shard
+    replica.seed(1234)
+    p = ffi.gen_params(n_identities=300, hard_error=2, zero_recipient=2)
+    rec = abi.REQUEST_DTYPE.itemsize
     gdist.barrier(ri)
     t0 = time.perf_counter()
-    ok = 0
-    for _ in range(3):
-        out = shard.process_batch(shard.gen_batch(512, p))
-        ok += int((out["status_code"] == 1).sum())
-    el = gdist.max_over_ranks(ri, time.perf_counter() - t0 + 0.01 * ri.rank)
-    total = gdist.sum_over_ranks(ri, 3 * 512)
-    oks = gdist.sum_over_ranks(ri, ok)
-    with open(os.path.join({out!r}, "rank%d.json" % ri.rank), "w") as f:
-        json.dump(dict(rank=ri.rank, world=ri.world, elapsed=el, total=total, oks=oks,
-                       digest=shard.digest(), local_ok=ok), f)
+    checked = 0
+    for step in range(4):
+        glob = replica.gen_batch(S * B, p)       # every source's batch, concatenated
+        want = replica.process_batch(glob)
+        mine = glob[r * B:(r + 1) * B]
+        dest = ffi.route(ccfg, mine)
+        send = np.zeros(S * C, dtype=abi.REQUEST_DTYPE)
+        pos = np.zeros(B, dtype=np.int64)
+        fill = np.zeros(S, dtype=np.int64)
+        for i, d in enumerate(dest):
+            assert fill[d] < C                   # no overflow at this capacity
+            pos[i] = d * C + fill[d]
+            send[pos[i]] = mine[i]
+            fill[d] += 1
+        recv = torch.empty(S * C * rec, dtype=torch.uint8)
+        dist.all_to_all_single(recv, torch.from_numpy(send.view(np.uint8).copy()))
+        sub = recv.numpy().view(abi.REQUEST_DTYPE)
+        out = shard.process_batch(sub)           # pads are type 0: hard errors
+        back = torch.empty(S * C * rec, dtype=torch.uint8)
+        dist.all_to_all_single(back, torch.from_numpy(out.view(np.uint8).copy()))
+        got = back.numpy().view(abi.RESPONSE_DTYPE)[pos]
+        assert got.tobytes() == want[r * B:(r + 1) * B].tobytes(), step
+        checked += B
+    el = gdist.max_over_ranks(ri, time.perf_counter() - t0)
+    total = gdist.sum_over_ranks(ri, checked)
+    rs = replica.shard(r)
+    with open(os.path.join({out!r}, "rank%d.json" % r), "w") as f:
+        json.dump(dict(rank=r, world=S, elapsed=el, total=total, capacity=C,
+                       digest_ok=shard.digest() == rs.digest(),
+                       messages=shard.messages, replica_messages=rs.messages,
+                       cluster_messages=replica.messages), f)
     gdist.finalize(ri)
 """)
 
@@ -43,24 +89,24 @@ def free_port():
     return p
 
 
-def test_two_rank_shards_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_protocol_gloo(tmp_path, world):
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=ROOT, out=str(tmp_path)))
     for attempt in range(3):  # a free port can be taken between probe and bind
         port = free_port()
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-               "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port",
+               str(port), str(script)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
         busy = "address already in use" in (r.stdout + r.stderr).lower() or "EADDRINUSE" in r.stderr
         if r.returncode == 0 or not busy:
             break
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    import json
-    rows = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(2)]
-    assert sorted(x["rank"] for x in rows) == [0, 1]
-    a, b = rows
-    assert a["world"] == b["world"] == 2
-    assert a["elapsed"] == b["elapsed"]              # max over ranks, same on both
-    assert a["total"] == b["total"] == 2 * 3 * 512   # weak scaling: work adds up
-    assert a["oks"] == a["local_ok"] + b["local_ok"]
-    assert a["digest"] != b["digest"]                # independent shards, different streams
+    rows = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(world)]
+    assert sorted(x["rank"] for x in rows) == list(range(world))
+    assert len({x["elapsed"] for x in rows}) == 1          # max over ranks, same everywhere
+    assert all(x["total"] == world * 4 * 1024 for x in rows)  # weak scaling: work adds up
+    assert all(x["digest_ok"] for x in rows)
+    assert all(x["messages"] == x["replica_messages"] for x in rows)
+    assert sum(x["messages"] for x in rows) == rows[0]["cluster_messages"] > 0
