@@ -5,7 +5,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-functi
 
 LIB := grapevine_amd/libgvstore.so
 SRCS := grapevine_amd/csrc/gvs_engine.hip
-HDRS := grapevine_amd/csrc/gvs_kernels.h grapevine_amd/csrc/gvs_device.h grapevine_amd/csrc/gvs_route.h include/gvstore.h
+HDRS := grapevine_amd/csrc/gvs_kernels.h grapevine_amd/csrc/gvs_device.h grapevine_amd/csrc/gvs_route.h grapevine_amd/csrc/gvs_crypto.h grapevine_amd/csrc/gvs_seal_dev.h include/gvstore.h
 
 all: $(LIB) oracle
 

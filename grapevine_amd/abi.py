@@ -86,20 +86,26 @@ class GvsStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "messages", "mailboxes", "batches", "creation_counter", "free_ring_head",
         "free_ring_tail", "msg_partitions", "msg_partition_slots", "shards", "route_capacity",
-        "shard_batch")]
+        "shard_batch", "epoch")]
 
 COMM_ID_BYTES = 128
+FLAG_AUTH_STORAGE = 1  # GVS_FLAG_AUTH_STORAGE: AES-CTR + BLAKE2b sealed tables
+ERR_INTEGRITY = -7     # GVS_ERR_INTEGRITY
+
+# gvs_dump_raw / gvs_store_raw regions
+RAW_MESSAGES, RAW_MAILBOXES, RAW_SIDE, RAW_MSG_TAGS, RAW_MBOX_TAGS = range(5)
 
 
 def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,
                 max_batch=None, device=0, secret_key=None, shard_count=0, shard_index=0,
-                route_capacity=0, rows_per_partition=0):
+                route_capacity=0, rows_per_partition=0, auth_storage=False):
     """Config mirroring gvs_config_init's defaults (R = N/16 mailboxes per shard)."""
     cfg = GvsConfig()
     cfg.shard_count = shard_count
     cfg.shard_index = shard_index
     cfg.route_capacity = route_capacity
     cfg.rows_per_partition = rows_per_partition
+    cfg.flags = FLAG_AUTH_STORAGE if auth_storage else 0
     cfg.msg_capacity = msg_capacity
     if mailbox_partitions is None:
         r = max(msg_capacity // 16, 256)

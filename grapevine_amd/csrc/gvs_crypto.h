@@ -1,0 +1,204 @@
+// gvs_crypto.h — primitives of the authenticated-storage mode:
+// AES-128 (FIPS-197) in counter mode and BLAKE2b (RFC 7693), written for gfx950
+// and shared with the host (key schedule, tables, the precomputed MAC key
+// state, host-side unsealing for test dumps).
+//
+// Storage format of one row (message row: 1024 B; mailbox row: 1024 B + its
+// 16-B side entry), sealed at epoch e (the number of batches the store has
+// applied; every row is rewritten every batch, so e is also its version):
+//   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
+//                       (standard CTR, counter in the last two bytes)
+//   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
+//   leaf_i = BLAKE2b-128(ct[256i, 256i+256), person = "gvs-leaf" | le64(i))
+//   tag = BLAKE2b-128(key = mac_key, le64(row) | le32(e) | le32(table)
+//                     | side_ct (or 16 zero bytes) | leaf_0 .. leaf_3)
+// The tag binds row, table and epoch, so a replayed or moved row fails.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gvs {
+
+// ------------------------------------------------------------------ AES-128
+
+struct AesRk {
+  uint32_t w[44];  // expanded encryption key, big-endian words (FIPS-197 §5.2)
+};
+
+__host__ __device__ inline uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+__host__ __device__ inline uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+// te0[x] = S[x]*{02} | S[x] | S[x] | S[x]*{03} (big-endian bytes); the other
+// three round tables are byte rotations of it, S[x] = (te0[x] >> 8) & 0xff.
+template <typename Tab>
+__host__ __device__ inline void aes128_encrypt_words(const AesRk& rk, const Tab& te0, uint32_t s0,
+                                                     uint32_t s1, uint32_t s2, uint32_t s3,
+                                                     uint32_t out[4]) {
+  s0 ^= rk.w[0];
+  s1 ^= rk.w[1];
+  s2 ^= rk.w[2];
+  s3 ^= rk.w[3];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t t0 = te0[s0 >> 24] ^ ror32(te0[(s1 >> 16) & 0xff], 8) ^
+                        ror32(te0[(s2 >> 8) & 0xff], 16) ^ ror32(te0[s3 & 0xff], 24) ^ rk.w[4 * r];
+    const uint32_t t1 = te0[s1 >> 24] ^ ror32(te0[(s2 >> 16) & 0xff], 8) ^
+                        ror32(te0[(s3 >> 8) & 0xff], 16) ^ ror32(te0[s0 & 0xff], 24) ^
+                        rk.w[4 * r + 1];
+    const uint32_t t2 = te0[s2 >> 24] ^ ror32(te0[(s3 >> 16) & 0xff], 8) ^
+                        ror32(te0[(s0 >> 8) & 0xff], 16) ^ ror32(te0[s1 & 0xff], 24) ^
+                        rk.w[4 * r + 2];
+    const uint32_t t3 = te0[s3 >> 24] ^ ror32(te0[(s0 >> 16) & 0xff], 8) ^
+                        ror32(te0[(s1 >> 8) & 0xff], 16) ^ ror32(te0[s2 & 0xff], 24) ^
+                        rk.w[4 * r + 3];
+    s0 = t0;
+    s1 = t1;
+    s2 = t2;
+    s3 = t3;
+  }
+#define GVS_SB(x) ((te0[(x)] >> 8) & 0xffu)
+  out[0] = (GVS_SB(s0 >> 24) << 24 | GVS_SB((s1 >> 16) & 0xff) << 16 |
+            GVS_SB((s2 >> 8) & 0xff) << 8 | GVS_SB(s3 & 0xff)) ^ rk.w[40];
+  out[1] = (GVS_SB(s1 >> 24) << 24 | GVS_SB((s2 >> 16) & 0xff) << 16 |
+            GVS_SB((s3 >> 8) & 0xff) << 8 | GVS_SB(s0 & 0xff)) ^ rk.w[41];
+  out[2] = (GVS_SB(s2 >> 24) << 24 | GVS_SB((s3 >> 16) & 0xff) << 16 |
+            GVS_SB((s0 >> 8) & 0xff) << 8 | GVS_SB(s1 & 0xff)) ^ rk.w[42];
+  out[3] = (GVS_SB(s3 >> 24) << 24 | GVS_SB((s0 >> 16) & 0xff) << 16 |
+            GVS_SB((s1 >> 8) & 0xff) << 8 | GVS_SB(s2 & 0xff)) ^ rk.w[43];
+#undef GVS_SB
+}
+
+// keystream block j of (table, row, epoch) as four little-endian data words
+template <typename Tab>
+__host__ __device__ inline uint4 ctr_keystream(const AesRk& rk, const Tab& te0, uint32_t table,
+                                               uint64_t row, uint32_t epoch, uint32_t j) {
+  uint32_t o[4];
+  aes128_encrypt_words(rk, te0, bswap32((uint32_t)row), bswap32((uint32_t)(row >> 32)),
+                       bswap32(epoch), (table << 24) | j, o);
+  return make_uint4(bswap32(o[0]), bswap32(o[1]), bswap32(o[2]), bswap32(o[3]));
+}
+
+// --------------------------------------------------------------- BLAKE2b
+
+struct B2State {
+  uint64_t h[8];
+};
+
+__host__ __device__ inline uint64_t b2_rotr(uint64_t x, int r) { return (x >> r) | (x << (64 - r)); }
+
+__host__ __device__ inline void b2_iv(uint64_t iv[8]) {
+  iv[0] = 0x6a09e667f3bcc908ULL;
+  iv[1] = 0xbb67ae8584caa73bULL;
+  iv[2] = 0x3c6ef372fe94f82bULL;
+  iv[3] = 0xa54ff53a5f1d36f1ULL;
+  iv[4] = 0x510e527fade682d1ULL;
+  iv[5] = 0x9b05688c2b3e6c1fULL;
+  iv[6] = 0x1f83d9abfb41bd6bULL;
+  iv[7] = 0x5be0cd19137e2179ULL;
+}
+
+#define GVS_B2G(a, b, c, d, x, y)    \
+  do {                               \
+    v[a] = v[a] + v[b] + (x);        \
+    v[d] = b2_rotr(v[d] ^ v[a], 32); \
+    v[c] = v[c] + v[d];              \
+    v[b] = b2_rotr(v[b] ^ v[c], 24); \
+    v[a] = v[a] + v[b] + (y);        \
+    v[d] = b2_rotr(v[d] ^ v[a], 16); \
+    v[c] = v[c] + v[d];              \
+    v[b] = b2_rotr(v[b] ^ v[c], 63); \
+  } while (0)
+
+// RFC 7693 §3.2 compression F; t = byte offset after this block, last = final block
+__host__ __device__ inline void b2_compress(B2State& s, const uint64_t m[16], uint64_t t,
+                                            bool last) {
+  constexpr uint8_t SG[12][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+  uint64_t v[16], iv[8];
+  b2_iv(iv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] = s.h[i];
+    v[i + 8] = iv[i];
+  }
+  v[12] ^= t;
+  if (last) v[14] = ~v[14];
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    GVS_B2G(0, 4, 8, 12, m[SG[r][0]], m[SG[r][1]]);
+    GVS_B2G(1, 5, 9, 13, m[SG[r][2]], m[SG[r][3]]);
+    GVS_B2G(2, 6, 10, 14, m[SG[r][4]], m[SG[r][5]]);
+    GVS_B2G(3, 7, 11, 15, m[SG[r][6]], m[SG[r][7]]);
+    GVS_B2G(0, 5, 10, 15, m[SG[r][8]], m[SG[r][9]]);
+    GVS_B2G(1, 6, 11, 12, m[SG[r][10]], m[SG[r][11]]);
+    GVS_B2G(2, 7, 8, 13, m[SG[r][12]], m[SG[r][13]]);
+    GVS_B2G(3, 4, 9, 14, m[SG[r][14]], m[SG[r][15]]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.h[i] ^= v[i] ^ v[i + 8];
+}
+#undef GVS_B2G
+
+// initial state from the parameter block: digest length nn, key length kk,
+// sequential mode, personalisation (p0, p1) (RFC 7693 §2.5, BLAKE2 §2.8)
+__host__ __device__ inline B2State b2_init(uint32_t nn, uint32_t kk, uint64_t p0, uint64_t p1) {
+  B2State s;
+  b2_iv(s.h);
+  s.h[0] ^= 0x01010000ULL ^ ((uint64_t)kk << 8) ^ nn;
+  s.h[6] ^= p0;
+  s.h[7] ^= p1;
+  return s;
+}
+
+// leaf i of a row: BLAKE2b-128 of its 256 ciphertext bytes, person "gvs-leaf" | le64(i)
+constexpr uint64_t kLeafPerson0 = 0x6661656c2d737667ULL;  // "gvs-leaf" little-endian
+__host__ __device__ inline void leaf_digest(const uint64_t m[32], uint32_t i, uint64_t out[2]) {
+  B2State s = b2_init(16, 0, kLeafPerson0, (uint64_t)i);
+  b2_compress(s, m, 128, false);
+  b2_compress(s, m + 16, 256, true);
+  out[0] = s.h[0];
+  out[1] = s.h[1];
+}
+
+// tag from the state after the key block (keyed BLAKE2b-128, 32-byte key) and
+// the 96-byte header + leaves message
+__host__ __device__ inline void row_tag(const B2State& keyed, uint64_t row, uint32_t epoch,
+                                        uint32_t table, const uint64_t side[2],
+                                        const uint64_t leaves[8], uint64_t out[2]) {
+  uint64_t m[16];
+  m[0] = row;
+  m[1] = (uint64_t)epoch | ((uint64_t)table << 32);
+  m[2] = side[0];
+  m[3] = side[1];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m[4 + k] = leaves[k];
+#pragma unroll
+  for (int k = 12; k < 16; ++k) m[k] = 0;
+  B2State s = keyed;
+  b2_compress(s, m, 128 + 96, true);
+  out[0] = s.h[0];
+  out[1] = s.h[1];
+}
+
+// Everything a sealing kernel needs, passed by value.
+struct SealCtx {
+  AesRk rk;
+  B2State keyed;    // BLAKE2b-128 state after the MAC key block
+  uint32_t epoch;   // rows are read at `epoch`, written at `epoch + 1`
+  uint32_t on;      // authenticated-storage mode enabled
+};
+
+}  // namespace gvs

@@ -85,6 +85,9 @@ struct Engine {
   uint32_t* dslot = nullptr;
   uint32_t* bsum2 = nullptr;
   uint4* recv = nullptr;     // routed modes: S*C incoming request slots
+  uint4* mtag = nullptr;     // authenticated storage: N message-row tags
+  uint4* btag = nullptr;     //                        R mailbox-row tags
+  uint32_t epoch = 0;        // batches applied: rows are sealed at this epoch
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -117,6 +120,10 @@ struct gvs_handle {
   const char* mark_name[kMaxMarks] = {};
   int n_marks = 0;
   bool timed = false;
+  bool auth = false;         // GVS_FLAG_AUTH_STORAGE
+  bool poisoned = false;     // an integrity failure was seen
+  SealCtx sc{};              // storage keys (epoch filled per engine)
+  uint32_t* te = nullptr;    // AES table on the device
   int rpass_variant = 6;
   std::vector<void*> allocs;
   std::string err;
@@ -174,7 +181,7 @@ static int validate(const gvs_config* c) {
     return GVS_ERR_INVALID_ARG;
   if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << (kSeqBits - 1)))
     return GVS_ERR_INVALID_ARG;
-  if (c->flags != 0) return GVS_ERR_INVALID_ARG;
+  if (c->flags & ~GVS_FLAG_AUTH_STORAGE) return GVS_ERR_INVALID_ARG;
   if (c->rows_per_partition && (!is_pow2(c->rows_per_partition) ||
                                 c->rows_per_partition < (uint32_t)kTile ||
                                 c->rows_per_partition > (uint32_t)kRowsMax))
@@ -196,6 +203,102 @@ static uint32_t auto_capacity(uint32_t B, uint32_t S) {
   uint64_t c = (uint64_t)std::ceil(mu + 8.0 * std::sqrt(mu) + 64.0);
   c = (c + 63) / 64 * 64;
   return (uint32_t)(c < B ? c : B);
+}
+
+// ------------------------------------------------- authenticated storage (host)
+
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+  uint8_t p = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (b & 1) p ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return p;
+}
+
+// AES S-box from log/antilog tables of the generator 3 plus the affine map
+static void aes_sbox(uint8_t sb[256]) {
+  uint8_t lg[256] = {}, alg[256] = {};
+  uint8_t x = 1;
+  for (int i = 0; i < 255; ++i) {
+    alg[i] = x;
+    lg[x] = (uint8_t)i;
+    x = gf_mul(x, 3);
+  }
+  for (int v = 0; v < 256; ++v) {
+    uint8_t inv = v ? alg[(255 - lg[v]) % 255] : 0;
+    uint8_t s = inv, r = inv;
+    for (int k = 0; k < 4; ++k) {
+      r = (uint8_t)((r << 1) | (r >> 7));
+      s ^= r;
+    }
+    sb[v] = (uint8_t)(s ^ 0x63);
+  }
+}
+
+static void aes_tables(const uint8_t sb[256], uint32_t te0[256]) {
+  for (int v = 0; v < 256; ++v) {
+    const uint8_t s1 = sb[v], s2 = gf_mul(s1, 2), s3 = (uint8_t)(s2 ^ s1);
+    te0[v] = ((uint32_t)s2 << 24) | ((uint32_t)s1 << 16) | ((uint32_t)s1 << 8) | s3;
+  }
+}
+
+static void aes_expand(const uint8_t sb[256], const uint8_t key[16], AesRk& rk) {
+  for (int i = 0; i < 4; ++i)
+    rk.w[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
+              ((uint32_t)key[4 * i + 2] << 8) | key[4 * i + 3];
+  uint32_t rcon = 0x01000000u;
+  for (int i = 4; i < 44; ++i) {
+    uint32_t t = rk.w[i - 1];
+    if (i % 4 == 0) {
+      t = ((uint32_t)sb[(t >> 16) & 0xff] << 24) | ((uint32_t)sb[(t >> 8) & 0xff] << 16) |
+          ((uint32_t)sb[t & 0xff] << 8) | sb[t >> 24];
+      t ^= rcon;
+      rcon = (uint32_t)gf_mul((uint8_t)(rcon >> 24), 2) << 24;
+    }
+    rk.w[i] = rk.w[i - 4] ^ t;
+  }
+}
+
+static void b2_block(const uint8_t* p, size_t n, uint64_t m[16]) {
+  uint8_t b[128] = {};
+  std::memcpy(b, p, n);
+  for (int i = 0; i < 16; ++i) m[i] = ld64(b + 8 * i);
+}
+
+// keyed BLAKE2b (32-byte key) of a message shorter than one block
+static void b2_keyed_short(const uint8_t key[32], const char* msg, uint32_t nn, uint8_t* out) {
+  B2State s = b2_init(nn, 32, 0, 0);
+  uint64_t m[16];
+  b2_block(key, 32, m);
+  b2_compress(s, m, 128, false);
+  const size_t len = std::strlen(msg);
+  b2_block((const uint8_t*)msg, len, m);
+  b2_compress(s, m, 128 + len, true);
+  for (uint32_t i = 0; i < nn; ++i) out[i] = (uint8_t)(s.h[i / 8] >> (8 * (i % 8)));
+}
+
+// storage keys from the config secret: AES key, MAC key state
+static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256]) {
+  uint8_t sb[256], ak[16], mk[32];
+  aes_sbox(sb);
+  aes_tables(sb, te0);
+  b2_keyed_short(secret, "gvs storage aes", 16, ak);
+  b2_keyed_short(secret, "gvs storage mac", 32, mk);
+  aes_expand(sb, ak, sc.rk);
+  sc.keyed = b2_init(16, 32, 0, 0);
+  uint64_t m[16];
+  b2_block(mk, 32, m);
+  b2_compress(sc.keyed, m, 128, false);
+  sc.epoch = 0;
+  sc.on = 1;
+}
+
+static SealCtx seal_of(const gvs_handle* h, const Engine& e) {
+  SealCtx c = h->sc;
+  c.epoch = e.epoch;
+  return c;
 }
 
 static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
@@ -259,6 +362,10 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   A(dslot, B);
   A(bsum2, e.nblk);
   if (h->mode != kSingle) A(recv, (uint64_t)h->S * h->C * kSlotU4);
+  if (h->auth) {
+    A(mtag, e.N);
+    A(btag, e.R);
+  }
 #undef A
   hipStream_t s = h->stream;
   GVS_HIP(h, hipMemsetAsync(e.img + (uint64_t)B * 64, 0, E * 1024, s));
@@ -274,6 +381,15 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   sc.tail = e.N;
   GVS_HIP(h, hipMemcpyAsync(e.ring, ring.data(), ring.size() * 4, hipMemcpyHostToDevice, s));
   GVS_HIP(h, hipMemcpyAsync(e.scal, &sc, sizeof sc, hipMemcpyHostToDevice, s));
+  if (h->auth) {  // every row starts as a sealed all-zero row at epoch 0
+    e.epoch = 0;
+    const SealCtx c = seal_of(h, e);
+    hipLaunchKernelGGL(k_seal_init, dim3(1024), dim3(256), 0, s, c, (const uint32_t*)h->te,
+                       e.table, e.mtag, (uint4*)nullptr, 0u, e.N);
+    hipLaunchKernelGGL(k_seal_init, dim3(256), dim3(256), 0, s, c, (const uint32_t*)h->te,
+                       e.mbox, e.btag, e.side, 1u, e.R);
+    GVS_HIP(h, hipGetLastError());
+  }
   GVS_HIP(h, hipStreamSynchronize(s));
   return GVS_OK;
 }
@@ -304,6 +420,7 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
   h->cfg = *cfg;
   h->mode = mode;
   h->device = (int)cfg->device;
+  h->auth = (cfg->flags & GVS_FLAG_AUTH_STORAGE) != 0;
   h->S = cfg->shard_count ? cfg->shard_count : 1;
   h->Bsub = cfg->max_batch;
   if (mode == kRccl && cfg->shard_index >= h->S) {
@@ -334,6 +451,13 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
     return fail(GVS_ERR_DEVICE);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(GVS_ERR_DEVICE);
+  if (h->auth) {
+    uint32_t te0[256];
+    storage_ctx(cfg->secret_key, h->sc, te0);
+    if (int rc = dalloc_t(h, &h->te, 256)) return fail(rc);
+    if (hipMemcpy(h->te, te0, sizeof te0, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GVS_ERR_DEVICE);
+  }
 
   const uint32_t n_eng = mode == kLocal ? h->S : 1u;
   const uint32_t n_src = mode == kSingle ? 0u : (mode == kLocal ? h->S : 1u);
@@ -378,8 +502,11 @@ static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
   return GVS_OK;
 }
 
-static MArgs margs(const Engine& e) {
+static MArgs margs(const gvs_handle* h, const Engine& e) {
   MArgs a{};
+  a.sc = seal_of(h, e);
+  a.te = h->te;
+  a.btag = e.btag;
   a.keys = e.s1keys;
   a.qstart = e.qstart;
   a.mbox = e.mbox;
@@ -438,7 +565,10 @@ static int phase_a(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride,
   mark(h, "meta");
   if (int r = sort_keys<Key128, 4096>(h, e.s1keys, B)) return r;
   mark(h, "sort_s1");
-  hipLaunchKernelGGL(k_m1, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(e));
+  if (h->auth)
+    hipLaunchKernelGGL(k_m1<true>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  else
+    hipLaunchKernelGGL(k_m1<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
   mark(h, "m1");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
@@ -460,7 +590,14 @@ static void launch_rpass(gvs_handle* h, const Engine& e, uint32_t n) {
   a.W = e.W;
   a.S = e.S;
   a.null_blocks = kNullBlocks;
+  a.sc = seal_of(h, e);
+  a.te = h->te;
+  a.mtag = e.mtag;
   const dim3 g(e.W + kNullBlocks), b(256);
+  if (h->auth) {
+    hipLaunchKernelGGL((k_rpass<16, true, true, 2, true>), g, b, 0, s, a);
+    return;
+  }
   switch (h->rpass_variant) {
     case 0: hipLaunchKernelGGL((k_rpass<4, false, false, 1>), g, b, 0, s, a); break;
     case 1: hipLaunchKernelGGL((k_rpass<4, true, true, 1>), g, b, 0, s, a); break;
@@ -502,7 +639,10 @@ static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
   }
   mark(h, "post");
-  hipLaunchKernelGGL(k_m2, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(e));
+  if (h->auth)
+    hipLaunchKernelGGL(k_m2<true>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  else
+    hipLaunchKernelGGL(k_m2<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
   if (d_out && n)
     hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
   mark(h, "m2");
@@ -640,6 +780,12 @@ static int finish(gvs_handle* h) {
   GVS_HIP(h, hipMemcpyAsync(&e, &h->eng[0].scal->error, sizeof e, hipMemcpyDeviceToHost,
                             h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
+  if (e & 8u) {
+    h->poisoned = true;
+    h->err = "integrity failure: a stored row does not match its tag (authenticated storage)";
+    return GVS_ERR_INTEGRITY;
+  }
+  if (e & 2u) h->poisoned = true;  // M2 stopped half-way: tables inconsistent
   if (e & 4u) {
     h->err = "batch overflow: more than route_capacity requests of one source for one shard";
     return GVS_ERR_BATCH_OVERFLOW;
@@ -652,6 +798,7 @@ static int finish(gvs_handle* h) {
     h->err = "internal error flag " + std::to_string(e);
     return GVS_ERR_INTERNAL;
   }
+  for (auto& en : h->eng) en.epoch += 1;  // every row was rewritten at epoch + 1
   return GVS_OK;
 }
 
@@ -711,6 +858,7 @@ int gvs_create_sharded(const gvs_config* cfg, const uint8_t comm_id[GVS_COMM_ID_
 
 int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_response* out) {
   if (!h || (!reqs && n) || (!out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
   GVS_HIP(h, hipSetDevice(h->device));
   if (n)
     GVS_HIP(h, hipMemcpyAsync(h->in_stage, reqs, (size_t)n * sizeof(gvs_request),
@@ -724,6 +872,7 @@ int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_re
 
 int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void* d_out) {
   if (!h || (!d_reqs && n) || (!d_out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
   GVS_HIP(h, hipSetDevice(h->device));
   if (int r = run_batch(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
   return finish(h);
@@ -752,6 +901,7 @@ int gvs_get_stats(gvs_handle* h, gvs_stats* out) {
   out->shards = h->eng.size();
   out->route_capacity = h->C;
   out->shard_batch = h->Be;
+  out->epoch = h->eng[0].epoch;
   return GVS_OK;
 }
 
@@ -761,12 +911,22 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
   if (bytes < N * 1024 * h->eng.size()) return GVS_ERR_INVALID_ARG;
   std::vector<uint8_t> phys(N * 1024);
   uint8_t* dst = (uint8_t*)host_dst;
+  std::vector<uint32_t> te0(256);
+  SealCtx sc{};
+  if (h->auth) storage_ctx(h->cfg.secret_key, sc, te0.data());
   for (const auto& e : h->eng) {
     GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
     GVS_HIP(h, hipStreamSynchronize(h->stream));
     for (uint64_t sl = 0; sl < N; ++sl) {
       uint64_t row = (sl % e.W) * e.S + sl / e.W;
-      std::memcpy(dst + sl * 1024, phys.data() + row * 1024, 1024);
+      uint8_t* d = dst + sl * 1024;
+      std::memcpy(d, phys.data() + row * 1024, 1024);
+      if (h->auth)  // unseal (decrypt) at the current epoch
+        for (uint32_t j = 0; j < 64; ++j) {
+          const uint4 k = ctr_keystream(sc.rk, te0.data(), 0u, row, e.epoch, j);
+          const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+          for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
+        }
     }
     dst += N * 1024;
   }
@@ -810,5 +970,75 @@ int gvs_last_timings(gvs_handle* h, const char** names, float* ms, int cap) {
 }
 
 const char* gvs_last_error(gvs_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
+                         const uint8_t pt[1024], const uint8_t* side_pt, uint8_t ct[1024],
+                         uint8_t* side_ct, uint8_t tag[16]) {
+  if (!secret || !pt || !ct || !tag || table > 1 || (side_pt && !side_ct)) return GVS_ERR_INVALID_ARG;
+  SealCtx sc{};
+  uint32_t te0[256];
+  storage_ctx(secret, sc, te0);
+  auto xor_block = [&](const uint8_t* src, uint8_t* dst, uint32_t j) {
+    const uint4 k = ctr_keystream(sc.rk, te0, table, row, epoch, j);
+    const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+    for (int b = 0; b < 16; ++b) dst[b] = (uint8_t)(src[b] ^ (kw[b / 4] >> (8 * (b % 4))));
+  };
+  for (uint32_t j = 0; j < 64; ++j) xor_block(pt + 16 * j, ct + 16 * j, j);
+  uint64_t sd[2] = {0, 0};
+  if (side_pt) {
+    xor_block(side_pt, side_ct, 64);
+    sd[0] = ld64(side_ct);
+    sd[1] = ld64(side_ct + 8);
+  }
+  uint64_t leaves[8];
+  for (uint32_t i = 0; i < 4; ++i) {
+    uint64_t m[32];
+    for (int k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
+    leaf_digest(m, i, leaves + 2 * i);
+  }
+  uint64_t t[2];
+  row_tag(sc.keyed, row, epoch, table, sd, leaves, t);
+  for (int b = 0; b < 16; ++b) tag[b] = (uint8_t)(t[b / 8] >> (8 * (b % 8)));
+  return GVS_OK;
+}
+
+static int raw_region(gvs_handle* h, uint32_t shard, uint32_t region, void** base,
+                      uint64_t* size) {
+  if (shard >= h->eng.size()) return GVS_ERR_INVALID_ARG;
+  Engine& e = h->eng[shard];
+  switch (region) {
+    case 0: *base = e.table; *size = e.N * 1024; break;
+    case 1: *base = e.mbox; *size = e.R * 1024; break;
+    case 2: *base = e.side; *size = e.R * 16; break;
+    case 3: *base = e.mtag; *size = e.mtag ? e.N * 16 : 0; break;
+    case 4: *base = e.btag; *size = e.btag ? e.R * 16 : 0; break;
+    default: return GVS_ERR_INVALID_ARG;
+  }
+  return *base ? GVS_OK : GVS_ERR_INVALID_ARG;
+}
+
+int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset, void* dst,
+                 uint64_t bytes) {
+  if (!h || !dst) return GVS_ERR_INVALID_ARG;
+  void* base;
+  uint64_t size;
+  if (int r = raw_region(h, shard, region, &base, &size)) return r;
+  if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
+  GVS_HIP(h, hipMemcpyAsync(dst, (uint8_t*)base + offset, bytes, hipMemcpyDeviceToHost, h->stream));
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return GVS_OK;
+}
+
+int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset,
+                  const void* src, uint64_t bytes) {
+  if (!h || !src) return GVS_ERR_INVALID_ARG;
+  void* base;
+  uint64_t size;
+  if (int r = raw_region(h, shard, region, &base, &size)) return r;
+  if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
+  GVS_HIP(h, hipMemcpyAsync((uint8_t*)base + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return GVS_OK;
+}
 
 }  // extern "C"

@@ -20,6 +20,7 @@
 // data only inside a single workgroup.
 #pragma once
 #include "gvs_device.h"
+#include "gvs_seal_dev.h"
 
 namespace gvs {
 
@@ -297,6 +298,9 @@ struct MArgs {
   uint32_t Q, Sr, B, dummy_blocks;
   uint64_t N;
   KeyCtx kc;
+  SealCtx sc;          // authenticated storage (AUTH instantiations)
+  const uint32_t* te;  // AES table (256 words)
+  uint4* btag;         // R mailbox row tags
 };
 
 // packed per-op info kept in LDS: seq | class<<20 | sub<<22 | success<<23
@@ -430,11 +434,17 @@ __device__ inline void init_sink(GroupL* g, uint32_t ng, uint32_t start) {
   }
 }
 
-// Phase B shared: map occupied mailbox rows of the partition to groups.
+// Phase B shared: map occupied mailbox rows of the partition to groups (and
+// cache each row's occupied bit).  AUTH: side entries are decrypted here;
+// they are authenticated with their row in phase C.
+template <bool AUTH>
 __device__ inline void side_prepass(const MArgs& a, uint32_t q, GroupL* g, uint32_t ng,
-                                    int16_t* s_sg, uint32_t* s_occ) {
+                                    int16_t* s_sg, uint8_t* s_occb, uint32_t* s_occ,
+                                    const uint32_t* s_te) {
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
-    uint4 sd = a.side[(uint64_t)q * a.Sr + j];
+    const uint64_t row = (uint64_t)q * a.Sr + j;
+    uint4 sd = a.side[row];
+    if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
     uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
     const int k = occ ? find_group(g, ng, hi, w1 >> 23) : -1;
@@ -444,7 +454,20 @@ __device__ inline void side_prepass(const MArgs& a, uint32_t q, GroupL* g, uint3
       g[k].len = (uint32_t)(w1 >> 1) & 63u;
     }
     s_sg[j] = (int16_t)k;
+    s_occb[j] = occ ? 1 : 0;
   }
+}
+
+// AUTH, phase C: stage the side ciphertexts of rows j0 .. j0+kMU-1 and verify
+// and decrypt the chunk's rows; a mismatch fails the batch for good.
+template <int U>
+__device__ inline void m_unseal_chunk(const MArgs& a, const uint32_t* s_te, uint32_t q,
+                                      uint32_t j0, uint4 (&v)[U], uint4* st) {
+  const uint32_t lane = lane_id();
+  const uint64_t r0 = (uint64_t)q * a.Sr + j0;
+  if (lane < (uint32_t)U) st[U * 4 * kSegU4 + lane] = a.side[r0 + lane];
+  if (!wave_unseal<U>(a.sc, s_te, 1u, r0, v, a.btag, true, st) && lane == 0)
+    atomicOr(&a.scal->error, 8u);
 }
 
 // Wave-cooperative write of up to 64 M1Out records (one per lane): each store
@@ -522,12 +545,16 @@ __device__ void dummy_partition(const MArgs& a, uint32_t b) {
   }
 }
 
+template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __shared__ GroupL g[kGroupMax + 1];
   __shared__ uint32_t stash[kStash];
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint8_t s_occb[kSrMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
+  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar branches
   const uint32_t q = blockIdx.x;
@@ -535,6 +562,8 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
     dummy_partition<false>(a, q - a.Q);
     return;
   }
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
   // the wave's first chunk of rows is in flight during the group discovery
   const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
   uint4 va[kMU], vb[kMU];
@@ -551,7 +580,7 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   }
   init_sink(g, ng, start);
   __syncthreads();
-  side_prepass(a, q, g, ng, s_sg, &s_occ);
+  side_prepass<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
   __syncthreads();
 
   // Phase C: stream every mailbox row of the partition (read-only pass).  Rows
@@ -568,6 +597,7 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
       keep4(v[u]);  // every row is read, used or not
       mm |= (j0 + u < a.Sr && s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
     }
+    if (AUTH) m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
     mm = __builtin_amdgcn_readfirstlane(mm);
     bool dry = j0 == 0;
     while (mm || dry) {
@@ -834,8 +864,11 @@ struct RArgs {
   const uint4* img;
   uint4* resp;              // B internal slots of kRespSlot bytes
   RRes* rres;
-  const Scal* scal;
+  Scal* scal;
   uint32_t n, B, W, S, null_blocks;
+  SealCtx sc;               // authenticated storage (AUTH instantiations)
+  const uint32_t* te;       // AES table (256 words)
+  uint4* mtag;              // N row tags
 };
 
 __device__ inline void write_response(const RArgs& a, uint32_t seq, uint4 rec, uint32_t status) {
@@ -922,11 +955,13 @@ __device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, 
   }
 }
 
-template <int U, bool NTL, bool NTS, int MINW>
+template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false>
 __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t stash[kStash];
   __shared__ uint32_t s_first[kTile], s_cnt[kTile];
   __shared__ uint32_t s_tile[kRowsMax / kTile + 1];
+  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(U) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
@@ -952,6 +987,8 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   const uint32_t start = a.pstart[w], end = a.pstart[w + 1];
   const uint32_t cnt = end - start;
   const uint64_t rowbase = (uint64_t)w * a.S;
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(U) : 0u);
   // stash this partition's ops (each key read once): row offset << 20 | seq
   for (uint32_t k = tid; k < cnt && k < (uint32_t)kStash; k += 256) {
     const uint64_t key = a.rkeys[start + k];
@@ -988,6 +1025,11 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
+      const uint64_t r0 = rowbase + rb + j;  // physical row of v[0]
+      if (AUTH) {
+        if (!wave_unseal<U>(a.sc, s_te, 0u, r0, v, a.mtag, false, st) && lane == 0)
+          atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
+      }
       // rows of this chunk that have ops (wave-uniform); wave 0's first chunk
       // also runs the dry op, so the single copy of the apply code below is
       // executed by every workgroup whatever the batch holds (see r_apply)
@@ -1011,6 +1053,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
 #pragma unroll
         for (int uu = 0; uu < U; ++uu) v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
       }
+      if (AUTH) wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st);
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }
@@ -1183,11 +1226,15 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
   __syncthreads();
 }
 
+template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __shared__ GroupL g[kGroupMax + 1];
   __shared__ uint32_t stash[kStash];
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint8_t s_occb[kSrMax];
+  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   __shared__ int16_t s_place[kSrMax];
   __shared__ uint8_t s_flag[kSrMax];
   __shared__ uint16_t s_pfx[kSrMax + 1];
@@ -1203,6 +1250,8 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
     dummy_partition<true>(a, q - a.Q);
     return;
   }
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
   // the wave's first chunk of rows is in flight during the group discovery
   uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
   uint4* side = a.side + (uint64_t)q * a.Sr;
@@ -1217,7 +1266,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   }
   init_sink(g, ng, start);
   __syncthreads();
-  side_prepass(a, q, g, ng, s_sg, &s_occ);
+  side_prepass<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
   __syncthreads();
   // final lengths; pending = groups with no row that end non-empty (the sink
   // g[ng] gets fl = 0, flag 0)
@@ -1231,8 +1280,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __syncthreads();
   for (uint32_t j = tid; j < a.Sr; j += 256) {
     const int k = s_sg[j];
-    const uint4 sd = a.side[(uint64_t)q * a.Sr + j];
-    const bool occ = u4hi(sd) & 1u;
+    const bool occ = s_occb[j] != 0;
     s_flag[j] = (!occ || (k >= 0 && g[k].fl == 0)) ? 1 : 0;
   }
   __syncthreads();
@@ -1268,6 +1316,17 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
       sd[u] = in ? side[j0 + u] : make_uint4(0, 0, 0, 0);
       mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
     }
+    if (AUTH) {
+      // verify + decrypt the rows (side ciphertexts staged), then the side
+      // entries: lane u < kMU decrypts row u's and every lane takes them all
+      m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
+      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
+      uint4 mine = make_uint4(0, 0, 0, 0);
+      if (lane < (uint32_t)kMU)
+        mine = xor4(st[kMU * 4 * kSegU4 + lane], side_keystream(a.sc, s_te, r0 + lane, a.sc.epoch));
+#pragma unroll
+      for (int u = 0; u < kMU; ++u) sd[u] = shfl4(mine, u);
+    }
     mm = __builtin_amdgcn_readfirstlane(mm);
     bool dry = j0 == 0;
     while (mm || dry) {
@@ -1301,11 +1360,26 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
       }
       dry = false;
     }
+    if (AUTH) {
+      // new side entries: lane u < kMU encrypts row u's at epoch + 1 and
+      // stages it for the tag; then the rows are sealed at epoch + 1
+      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
+      const uint32_t ep = a.sc.epoch + 1u;
+      uint4 mine = sd[0];
+#pragma unroll
+      for (int u = 1; u < kMU; ++u) mine = sel4(lane == (uint32_t)u, sd[u], mine);
+      if (lane < (uint32_t)kMU) {
+        const uint4 ct = xor4(mine, side_keystream(a.sc, s_te, r0 + lane, ep));
+        st[kMU * 4 * kSegU4 + lane] = ct;
+        side[j0 + lane] = ct;
+      }
+      wave_seal<kMU>(a.sc, s_te, 1u, r0, ep, v, a.btag, true, st);
+    }
 #pragma unroll
     for (int u = 0; u < kMU; ++u) {
       if (j0 + u < a.Sr) {
         st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
-        if (lane == 0) side[j0 + u] = sd[u];
+        if (!AUTH && lane == 0) side[j0 + u] = sd[u];
       }
       va[u] = vb[u];
     }

@@ -21,7 +21,8 @@ EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
     "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
-    "gvs_comm_unique_id", "gvs_create_sharded",
+    "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_dump_raw",
+    "gvs_store_raw",
 )
 
 
@@ -57,6 +58,10 @@ def load_library(path=None):
     lib.gvs_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     lib.gvs_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
                                      ctypes.POINTER(ctypes.c_float), i32]
+    cp, u64 = ctypes.c_char_p, ctypes.c_uint64
+    lib.gvs_storage_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
+    lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
+    lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_last_error.restype = ctypes.c_char_p
     lib.gvs_version.restype = ctypes.c_char_p
@@ -140,6 +145,18 @@ class ObliviousStore:
         out = np.zeros(n, dtype=abi.RECORD_DTYPE)
         self._check(self.lib.gvs_dump_messages(self.h, out.ctypes.data, n * 1024))
         return out
+
+    def dump_raw(self, region, offset, nbytes, shard=0):
+        """Raw device bytes of one shard's region (abi.RAW_*): ciphertext in
+        authenticated mode.  Test use."""
+        out = np.zeros(nbytes, dtype=np.uint8)
+        self._check(self.lib.gvs_dump_raw(self.h, shard, region, offset, out.ctypes.data, nbytes))
+        return out
+
+    def store_raw(self, region, offset, data, shard=0):
+        """Overwrite raw device bytes (tamper tests of the authenticated mode)."""
+        buf = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+        self._check(self.lib.gvs_store_raw(self.h, shard, region, offset, buf.ctypes.data, len(buf)))
 
     def synchronize(self):
         self._check(self.lib.gvs_synchronize(self.h))

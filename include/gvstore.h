@@ -77,6 +77,11 @@ extern "C" {
                                        was exceeded; the batch was not applied */
 #define GVS_ERR_NO_DEVICE (-5)
 #define GVS_ERR_INTERNAL (-6)
+#define GVS_ERR_INTEGRITY (-7) /* authenticated storage: a stored row failed
+                                  its tag; the handle refuses further work */
+
+/* gvs_config.flags */
+#define GVS_FLAG_AUTH_STORAGE 1u /* AES-CTR + BLAKE2b sealed tables */
 
 /* ---- records ------------------------------------------------------------- */
 
@@ -126,7 +131,7 @@ typedef struct gvs_config {
   uint32_t device;              /* HIP device ordinal */
   uint8_t secret_key[32];       /* [0:16) id PRP key, [16:32) recipient PRF key;
                                    identical on every shard */
-  uint32_t flags;               /* reserved, must be 0 */
+  uint32_t flags;               /* GVS_FLAG_* */
   uint32_t rows_per_partition;  /* message rows per table-pass workgroup (power of
                                    two 256..4096); 0 = automatic */
   uint32_t shard_count;         /* S shards of the store (0 or 1 = unsharded) */
@@ -148,6 +153,7 @@ typedef struct gvs_stats {       /* summed over the handle's shards */
   uint64_t shards;              /* shards held by this handle */
   uint64_t route_capacity;      /* C (0 when unsharded) */
   uint64_t shard_batch;         /* requests each shard's pipeline processes per batch */
+  uint64_t epoch;               /* batches applied to the tables (sealing epoch) */
 } gvs_stats;
 
 typedef struct gvs_handle gvs_handle;
@@ -199,6 +205,23 @@ int gvs_get_stats(gvs_handle *h, gvs_stats *out);
 /* Copy the slot-addressed message table (N * 1024 bytes per shard, shards in
  * order) to host memory; test use. */
 int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
+
+/* Authenticated-storage format, host-side and device-free:
+ * seal one 1024-B row (and for table 1, the mailbox table, its 16-B side
+ * entry; side_pt = NULL for table 0) at `epoch` under the storage keys
+ * derived from `secret` (gvs_config.secret_key).  For offline verification
+ * of dumps and for tests. */
+int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
+                         const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
+                         uint8_t *side_ct, uint8_t tag[16]);
+
+/* Raw device regions of one shard, for tests of the storage format:
+ * 0 message table (physical rows), 1 mailbox table, 2 mailbox side entries,
+ * 3 message row tags, 4 mailbox row tags (3, 4: authenticated mode only). */
+int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset, void *dst,
+                 uint64_t bytes);
+int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset,
+                  const void *src, uint64_t bytes);
 
 /* Wait for all work on the handle's stream. */
 int gvs_synchronize(gvs_handle *h);

@@ -68,6 +68,12 @@ def lib():
             getattr(L, f).argtypes = [vp]
             getattr(L, f).restype = u64
         L.gvo_gen_batch.argtypes = [vp, ctypes.POINTER(GenParams), ctypes.POINTER(u64), vp, u32, u64]
+        cp = ctypes.c_char_p
+        L.gvo_aes128_expand.argtypes = [cp, cp]
+        L.gvo_aes128_encrypt.argtypes = [cp, cp, cp]
+        L.gvo_blake2b.argtypes = [cp, ctypes.c_size_t, cp, cp, ctypes.c_size_t, cp, ctypes.c_size_t]
+        L.gvo_storage_keys.argtypes = [cp, cp, cp]
+        L.gvo_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
         L.gvo_id_encode_shard.argtypes = [ctypes.c_char_p, u32, u32, u64, ctypes.c_char_p]
         L.gvo_id_decode_shard.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, u32,
                                           ctypes.POINTER(u32), ctypes.POINTER(u32),
@@ -138,6 +144,34 @@ def route(config, reqs):
 
 def route_capacity(batch, n_shards):
     return lib().gvo_route_capacity(batch, n_shards)
+
+
+def aes128_encrypt(key16: bytes, block16: bytes) -> bytes:
+    rk = ctypes.create_string_buffer(176)
+    lib().gvo_aes128_expand(key16, rk)
+    out = ctypes.create_string_buffer(16)
+    lib().gvo_aes128_encrypt(rk, block16, out)
+    return out.raw
+
+
+def blake2b(msg: bytes, digest_size=64, key=b"", person=None) -> bytes:
+    out = ctypes.create_string_buffer(digest_size)
+    lib().gvo_blake2b(key or None, len(key), person, msg, len(msg), out, digest_size)
+    return out.raw
+
+
+def storage_keys(secret32: bytes):
+    a, m = ctypes.create_string_buffer(16), ctypes.create_string_buffer(32)
+    lib().gvo_storage_keys(secret32, a, m)
+    return a.raw, m.raw
+
+
+def seal_row(secret32: bytes, table: int, row: int, epoch: int, pt: bytes, side_pt=None):
+    """-> (ct 1024 B, side ct 16 B or None, tag 16 B)"""
+    ct, sct, tag = (ctypes.create_string_buffer(1024), ctypes.create_string_buffer(16),
+                    ctypes.create_string_buffer(16))
+    lib().gvo_seal_row(secret32, table, row, epoch, pt, side_pt, ct, sct if side_pt else None, tag)
+    return ct.raw, (sct.raw if side_pt else None), tag.raw
 
 
 def identity(i: int) -> bytes:

@@ -99,6 +99,17 @@ uint64_t gvo_cluster_mailboxes(const gvo_cluster *c);
 void gvo_cluster_gen_batch(const gvo_cluster *c, const gvo_gen_params *p, uint64_t *rng,
                            gvs_request *reqs, uint32_t n, uint64_t op_base);
 
+/* Authenticated-storage format (gvs_seal.c): AES-128 per
+ * FIPS-197, BLAKE2b per RFC 7693, and the sealing of one stored row. */
+void gvo_aes128_expand(const uint8_t key[16], uint8_t rk[176]);
+void gvo_aes128_encrypt(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]);
+void gvo_blake2b(const uint8_t *key, size_t keylen, const uint8_t *person, const uint8_t *msg,
+                 size_t len, uint8_t *out, size_t outlen);
+void gvo_storage_keys(const uint8_t secret[32], uint8_t aes_key[16], uint8_t mac_key[32]);
+void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
+                  const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
+                  uint8_t *side_ct, uint8_t tag[16]);
+
 /* Path ORAM restatement of the reference's CPU path (gvs_pathoram.c): the
  * same handler semantics over three Path ORAMs; the timed CPU baseline. */
 typedef struct gvp_model gvp_model;

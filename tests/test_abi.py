@@ -36,7 +36,7 @@ def test_pod_sizes_match_header():
     assert "GVS_PAYLOAD_BYTES 936" in hdr and "GVS_MAILBOX_SLOTS 62" in hdr
     assert abi.REQUEST_DTYPE.itemsize == 1040 and abi.RESPONSE_DTYPE.itemsize == 1040
     assert ctypes.sizeof(abi.GvsConfig) == 8 + 4 * 4 + 32 + 4 + 28
-    assert ctypes.sizeof(abi.GvsStats) == 11 * 8
+    assert ctypes.sizeof(abi.GvsStats) == 12 * 8
 
 
 def test_config_init_and_version_without_gpu():
