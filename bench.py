@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--routed", action="store_true",
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
+    p.add_argument("--auth", action="store_true",
+                   help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
 
@@ -176,11 +178,12 @@ def main():
     N, B = 1 << a.log2n, a.batch
     if world > 1 or a.routed:
         # one shard per rank; the store's own RCCL communicator carries the data path
-        cfg = abi.make_config(N, max_batch=B, device=local, shard_count=world, shard_index=rank)
+        cfg = abi.make_config(N, max_batch=B, device=local, shard_count=world, shard_index=rank,
+                              auth_storage=a.auth)
         cid = gdist.broadcast_bytes(ri, comm_unique_id() if rank == 0 else None, device=dev)
         store = ObliviousStore(cfg, comm_id=cid)
     else:
-        cfg = abi.make_config(N, max_batch=B, device=local)
+        cfg = abi.make_config(N, max_batch=B, device=local, auth_storage=a.auth)
         store = ObliviousStore(cfg)
     shard_batch = store.stats()["shard_batch"]
     g = torch.Generator(device=dev)
@@ -224,7 +227,7 @@ def main():
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("log2n") == a.log2n and tj.get("batch") == B and world == 1:
+            if tj.get("log2n") == a.log2n and tj.get("batch") == B and world == 1 and not a.auth:
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -242,12 +245,13 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded on device): 75% prefill, 25/25/25/25 CRUD mix, 50% next-message reads/deletes",
-            "config": {"workload": f"C3: 2^{a.log2n} message capacity per GPU, {B}-request batches",
+            "config": {"workload": (f"C5 storage mode (AES-128-CTR + BLAKE2b sealed rows): " if a.auth else "C3: ")
+                       + f"2^{a.log2n} message capacity per GPU, {B}-request batches",
                        "msg_capacity": N, "batch": B,
                        "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,
                        "parallelism": f"shards{world}",
                        "route_capacity": store.stats()["route_capacity"],
-                       "shard_batch": shard_batch},
+                       "shard_batch": shard_batch, "auth_storage": bool(a.auth)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rpass (message-table pass)",

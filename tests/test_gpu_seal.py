@@ -1,0 +1,164 @@
+"""GPU: the authenticated-storage mode (GVS_FLAG_AUTH_STORAGE).
+
+* Responses, live counts and the (host-unsealed) message table stay bit-exact
+  with the oracle, which knows nothing about sealing: sealing must not change
+  what the store computes.
+* What sits in HBM is exactly the format of oracle/gvs_seal.c: every raw
+  message row, mailbox row, side entry and tag equals the oracle's sealing of
+  the plaintext at the store's current epoch.
+* Tampering with any stored byte, tag or side entry, or replaying an older
+  sealed row, fails the next batch with GVS_ERR_INTEGRITY, and the handle then
+  refuses further work.
+"""
+import numpy as np
+import pytest
+
+from grapevine_amd import abi
+from grapevine_amd.store import GvsError, ObliviousStore
+from oracle import ffi
+
+from parity import run_stream
+
+pytestmark = pytest.mark.gpu
+
+SECRET = bytes((0x67 + 31 * i) & 0xFF for i in range(32))
+
+
+def make_pair(n_msgs=4096, Q=16, Sr=32, B=1024):
+    cfg = abi.make_config(n_msgs, mailbox_partitions=Q, mailbox_partition_slots=Sr,
+                          max_batch=B, secret_key=SECRET, auth_storage=True)
+    return ObliviousStore(cfg), ffi.Model(cfg)
+
+
+def physical_row(st, slot):
+    W, S = st["msg_partitions"], st["msg_partition_slots"]
+    return (slot % W) * S + slot // W
+
+
+def unseal(table, row, epoch, ct, side_ct=None):
+    """Decrypt with the oracle's keystream (the sealing of a zero row)."""
+    z = ffi.seal_row(SECRET, table, row, epoch, bytes(1024), bytes(16) if side_ct is not None else None)
+    pt = bytes(np.frombuffer(ct, np.uint8) ^ np.frombuffer(z[0], np.uint8))
+    spt = bytes(np.frombuffer(side_ct, np.uint8) ^ np.frombuffer(z[1], np.uint8)) if side_ct is not None else None
+    return pt, spt
+
+
+def test_auth_mode_parity_stream():
+    store, model = make_pair()
+    model.seed(31)
+    seen = run_stream(store, model, ffi.gen_params(n_identities=300), batches=8, n=1024)
+    assert {0, 1, 2} <= set(seen), seen
+    assert store.stats()["epoch"] == 8
+
+
+def test_auth_mode_hot_recipient_and_capacity():
+    store, model = make_pair(n_msgs=512, Q=4, Sr=16, B=1024)
+    model.seed(32)
+    seen = run_stream(store, model, ffi.gen_params(create=60, read=15, update=10, delete=15,
+                                                   hot=40, n_identities=60), batches=6, n=1024)
+    assert seen[5] > 0 and seen[7] > 0, seen
+
+
+def test_stored_bytes_are_the_oracle_format():
+    store, model = make_pair()
+    model.seed(33)
+    run_stream(store, model, ffi.gen_params(n_identities=200), batches=3, n=1024)
+    st = store.stats()
+    ep = st["epoch"]
+    N = store.config.msg_capacity
+    want_tab = model.dump_messages()
+    raw = store.dump_raw(abi.RAW_MESSAGES, 0, N * 1024).reshape(N, 1024)
+    tags = store.dump_raw(abi.RAW_MSG_TAGS, 0, N * 16).reshape(N, 16)
+    rng = np.random.default_rng(0)
+    live = [s for s in range(N) if want_tab[s]["msg_id"].any()]
+    slots = sorted(set(rng.choice(live, 24, replace=False).tolist()) | {0, N - 1})
+    for s in slots:
+        r = physical_row(st, s)
+        ct, _, tag = ffi.seal_row(SECRET, 0, r, ep, want_tab[s:s + 1].tobytes())
+        assert raw[r].tobytes() == ct, f"slot {s} row {r}: ciphertext differs"
+        assert tags[r].tobytes() == tag, f"slot {s} row {r}: tag differs"
+    # mailbox rows: decrypt, re-seal with the oracle, compare bytes and tag
+    R = store.config.mailbox_partitions * store.config.mailbox_partition_slots
+    mb = store.dump_raw(abi.RAW_MAILBOXES, 0, R * 1024).reshape(R, 1024)
+    side = store.dump_raw(abi.RAW_SIDE, 0, R * 16).reshape(R, 16)
+    btag = store.dump_raw(abi.RAW_MBOX_TAGS, 0, R * 16).reshape(R, 16)
+    occupied = 0
+    for r in range(R):
+        pt, spt = unseal(1, r, ep, mb[r].tobytes(), side[r].tobytes())
+        occupied += spt[8] & 1
+        ct, sct, tag = ffi.seal_row(SECRET, 1, r, ep, pt, spt)
+        assert (mb[r].tobytes(), side[r].tobytes(), btag[r].tobytes()) == (ct, sct, tag), f"mailbox row {r}"
+    assert occupied == model.mailboxes
+
+
+def run_one(store, model, params, n=1024):
+    reqs = model.gen_batch(n, params)
+    return store.process_batch(reqs), model.process_batch(reqs)
+
+
+@pytest.mark.parametrize("region,offset", [
+    (abi.RAW_MESSAGES, 5 * 1024 + 700),   # a byte of a message row
+    (abi.RAW_MSG_TAGS, 77 * 16 + 3),      # a message tag
+    (abi.RAW_MAILBOXES, 9 * 1024 + 40),   # a mailbox row
+    (abi.RAW_SIDE, 3 * 16 + 1),           # a mailbox side entry
+    (abi.RAW_MBOX_TAGS, 200 * 16 + 15),   # a mailbox tag
+])
+def test_tamper_is_detected(region, offset):
+    store, model = make_pair()
+    model.seed(34)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    b = store.dump_raw(region, offset, 1)
+    store.store_raw(region, offset, bytes([int(b[0]) ^ 0x10]))
+    with pytest.raises(GvsError) as ei:
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY
+    with pytest.raises(GvsError) as ei:  # the handle stays dead
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY
+
+
+def test_replayed_row_is_detected():
+    store, model = make_pair()
+    model.seed(35)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    row = 123
+    old = store.dump_raw(abi.RAW_MESSAGES, row * 1024, 1024).tobytes()
+    old_tag = store.dump_raw(abi.RAW_MSG_TAGS, row * 16, 16).tobytes()
+    run_stream(store, model, params, batches=1, n=1024)  # every row re-sealed at a new epoch
+    store.store_raw(abi.RAW_MESSAGES, row * 1024, old)
+    store.store_raw(abi.RAW_MSG_TAGS, row * 16, old_tag)
+    with pytest.raises(GvsError) as ei:
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY
+
+
+def test_swapped_rows_are_detected():
+    store, model = make_pair()
+    model.seed(36)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    a = [store.dump_raw(abi.RAW_MESSAGES, r * 1024, 1024).tobytes() for r in (10, 11)]
+    t = [store.dump_raw(abi.RAW_MSG_TAGS, r * 16, 16).tobytes() for r in (10, 11)]
+    store.store_raw(abi.RAW_MESSAGES, 10 * 1024, a[1])
+    store.store_raw(abi.RAW_MSG_TAGS, 10 * 16, t[1])
+    store.store_raw(abi.RAW_MESSAGES, 11 * 1024, a[0])
+    store.store_raw(abi.RAW_MSG_TAGS, 11 * 16, t[0])
+    with pytest.raises(GvsError) as ei:
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY
+
+
+def test_sharded_local_auth_parity():
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024,
+                          secret_key=SECRET, auth_storage=True, shard_count=2)
+    store = ObliviousStore(cfg)
+    cl = ffi.Cluster(cfg)
+    cl.seed(37)
+    p = ffi.gen_params(n_identities=300)
+    for b in range(4):
+        reqs = cl.gen_batch(2048, p)
+        want = cl.process_batch(reqs)
+        got = store.process_batch(reqs)
+        assert got.tobytes() == want.tobytes(), f"batch {b}"
