@@ -25,13 +25,34 @@ struct AesRk {
   uint32_t w[44];  // expanded encryption key, big-endian words (FIPS-197 §5.2)
 };
 
-__host__ __device__ inline uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+__host__ __device__ inline uint32_t ror32(uint32_t x, int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(x, x, (uint32_t)r);
+#else
+  return (x >> r) | (x << (32 - r));
+#endif
+}
 __host__ __device__ inline uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96)
+__host__ __device__ inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 // te0[x] = S[x]*{02} | S[x] | S[x] | S[x]*{03} (big-endian bytes); the other
 // three round tables are byte rotations of it, S[x] = (te0[x] >> 8) & 0xff.
+// te_at(tab, s, k) = te0[byte k of s] (k = 3 is the most significant byte).
+// Host: a plain 256-word array.  Device: the LDS replicas of gvs_seal_dev.h.
+__host__ __device__ inline uint32_t te_at(const uint32_t* tab, uint32_t s, int k) {
+  return tab[(s >> (8 * k)) & 0xffu];
+}
+
 template <typename Tab>
 __host__ __device__ inline void aes128_encrypt_words(const AesRk& rk, const Tab& te0, uint32_t s0,
                                                      uint32_t s1, uint32_t s2, uint32_t s3,
@@ -42,31 +63,28 @@ __host__ __device__ inline void aes128_encrypt_words(const AesRk& rk, const Tab&
   s3 ^= rk.w[3];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    const uint32_t t0 = te0[s0 >> 24] ^ ror32(te0[(s1 >> 16) & 0xff], 8) ^
-                        ror32(te0[(s2 >> 8) & 0xff], 16) ^ ror32(te0[s3 & 0xff], 24) ^ rk.w[4 * r];
-    const uint32_t t1 = te0[s1 >> 24] ^ ror32(te0[(s2 >> 16) & 0xff], 8) ^
-                        ror32(te0[(s3 >> 8) & 0xff], 16) ^ ror32(te0[s0 & 0xff], 24) ^
-                        rk.w[4 * r + 1];
-    const uint32_t t2 = te0[s2 >> 24] ^ ror32(te0[(s3 >> 16) & 0xff], 8) ^
-                        ror32(te0[(s0 >> 8) & 0xff], 16) ^ ror32(te0[s1 & 0xff], 24) ^
-                        rk.w[4 * r + 2];
-    const uint32_t t3 = te0[s3 >> 24] ^ ror32(te0[(s0 >> 16) & 0xff], 8) ^
-                        ror32(te0[(s1 >> 8) & 0xff], 16) ^ ror32(te0[s2 & 0xff], 24) ^
-                        rk.w[4 * r + 3];
+    const uint32_t t0 = xor3(xor3(te_at(te0, s0, 3), ror32(te_at(te0, s1, 2), 8),
+                                  ror32(te_at(te0, s2, 1), 16)),
+                             ror32(te_at(te0, s3, 0), 24), rk.w[4 * r]);
+    const uint32_t t1 = xor3(xor3(te_at(te0, s1, 3), ror32(te_at(te0, s2, 2), 8),
+                                  ror32(te_at(te0, s3, 1), 16)),
+                             ror32(te_at(te0, s0, 0), 24), rk.w[4 * r + 1]);
+    const uint32_t t2 = xor3(xor3(te_at(te0, s2, 3), ror32(te_at(te0, s3, 2), 8),
+                                  ror32(te_at(te0, s0, 1), 16)),
+                             ror32(te_at(te0, s1, 0), 24), rk.w[4 * r + 2]);
+    const uint32_t t3 = xor3(xor3(te_at(te0, s3, 3), ror32(te_at(te0, s0, 2), 8),
+                                  ror32(te_at(te0, s1, 1), 16)),
+                             ror32(te_at(te0, s2, 0), 24), rk.w[4 * r + 3]);
     s0 = t0;
     s1 = t1;
     s2 = t2;
     s3 = t3;
   }
-#define GVS_SB(x) ((te0[(x)] >> 8) & 0xffu)
-  out[0] = (GVS_SB(s0 >> 24) << 24 | GVS_SB((s1 >> 16) & 0xff) << 16 |
-            GVS_SB((s2 >> 8) & 0xff) << 8 | GVS_SB(s3 & 0xff)) ^ rk.w[40];
-  out[1] = (GVS_SB(s1 >> 24) << 24 | GVS_SB((s2 >> 16) & 0xff) << 16 |
-            GVS_SB((s3 >> 8) & 0xff) << 8 | GVS_SB(s0 & 0xff)) ^ rk.w[41];
-  out[2] = (GVS_SB(s2 >> 24) << 24 | GVS_SB((s3 >> 16) & 0xff) << 16 |
-            GVS_SB((s0 >> 8) & 0xff) << 8 | GVS_SB(s1 & 0xff)) ^ rk.w[42];
-  out[3] = (GVS_SB(s3 >> 24) << 24 | GVS_SB((s0 >> 16) & 0xff) << 16 |
-            GVS_SB((s1 >> 8) & 0xff) << 8 | GVS_SB(s2 & 0xff)) ^ rk.w[43];
+#define GVS_SB(x, k) ((te_at(te0, (x), (k)) >> 8) & 0xffu)
+  out[0] = (GVS_SB(s0, 3) << 24 | GVS_SB(s1, 2) << 16 | GVS_SB(s2, 1) << 8 | GVS_SB(s3, 0)) ^ rk.w[40];
+  out[1] = (GVS_SB(s1, 3) << 24 | GVS_SB(s2, 2) << 16 | GVS_SB(s3, 1) << 8 | GVS_SB(s0, 0)) ^ rk.w[41];
+  out[2] = (GVS_SB(s2, 3) << 24 | GVS_SB(s3, 2) << 16 | GVS_SB(s0, 1) << 8 | GVS_SB(s1, 0)) ^ rk.w[42];
+  out[3] = (GVS_SB(s3, 3) << 24 | GVS_SB(s0, 2) << 16 | GVS_SB(s1, 1) << 8 | GVS_SB(s2, 0)) ^ rk.w[43];
 #undef GVS_SB
 }
 
@@ -86,7 +104,25 @@ struct B2State {
   uint64_t h[8];
 };
 
-__host__ __device__ inline uint64_t b2_rotr(uint64_t x, int r) { return (x >> r) | (x << (64 - r)); }
+// 64-bit rotate right by a constant; on the device two v_alignbit_b32 (a
+// rotate by 32 is a register swap)
+__host__ __device__ inline uint64_t b2_rotr(uint64_t x, int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (r >= 32) {
+    const uint32_t t = lo;
+    lo = hi;
+    hi = t;
+    r -= 32;
+  }
+  if (r == 0) return ((uint64_t)hi << 32) | lo;
+  const uint32_t nlo = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)r);
+  const uint32_t nhi = __builtin_amdgcn_alignbit(lo, hi, (uint32_t)r);
+  return ((uint64_t)nhi << 32) | nlo;
+#else
+  return (x >> r) | (x << (64 - r));
+#endif
+}
 
 __host__ __device__ inline void b2_iv(uint64_t iv[8]) {
   iv[0] = 0x6a09e667f3bcc908ULL;
@@ -111,10 +147,9 @@ __host__ __device__ inline void b2_iv(uint64_t iv[8]) {
     v[b] = b2_rotr(v[b] ^ v[c], 63); \
   } while (0)
 
-// RFC 7693 §3.2 compression F; t = byte offset after this block, last = final block
-__host__ __device__ inline void b2_compress(B2State& s, const uint64_t m[16], uint64_t t,
-                                            bool last) {
-  constexpr uint8_t SG[12][16] = {
+// message schedule sigma[r] (RFC 7693 §2.7); rounds 10 and 11 reuse rows 0, 1
+__host__ __device__ constexpr int b2_sigma(int r, int i) {
+  constexpr uint8_t S[10][16] = {
       {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
       {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
       {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
@@ -124,9 +159,28 @@ __host__ __device__ inline void b2_compress(B2State& s, const uint64_t m[16], ui
       {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
       {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
       {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
-      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
-      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+  return S[r % 10][i];
+}
+
+// One round with compile-time message indices: every m[] access is static,
+// so the message block stays in registers (a runtime index would make the
+// compiler move the array to scratch or LDS).
+template <int R>
+__host__ __device__ __attribute__((always_inline)) inline void b2_round(uint64_t (&v)[16], const uint64_t* m) {
+  GVS_B2G(0, 4, 8, 12, m[b2_sigma(R, 0)], m[b2_sigma(R, 1)]);
+  GVS_B2G(1, 5, 9, 13, m[b2_sigma(R, 2)], m[b2_sigma(R, 3)]);
+  GVS_B2G(2, 6, 10, 14, m[b2_sigma(R, 4)], m[b2_sigma(R, 5)]);
+  GVS_B2G(3, 7, 11, 15, m[b2_sigma(R, 6)], m[b2_sigma(R, 7)]);
+  GVS_B2G(0, 5, 10, 15, m[b2_sigma(R, 8)], m[b2_sigma(R, 9)]);
+  GVS_B2G(1, 6, 11, 12, m[b2_sigma(R, 10)], m[b2_sigma(R, 11)]);
+  GVS_B2G(2, 7, 8, 13, m[b2_sigma(R, 12)], m[b2_sigma(R, 13)]);
+  GVS_B2G(3, 4, 9, 14, m[b2_sigma(R, 14)], m[b2_sigma(R, 15)]);
+}
+
+// RFC 7693 §3.2 compression F; t = byte offset after this block, last = final block
+__host__ __device__ __attribute__((always_inline)) inline void b2_compress(B2State& s, const uint64_t m[16], uint64_t t,
+                                            bool last) {
   uint64_t v[16], iv[8];
   b2_iv(iv);
 #pragma unroll
@@ -136,17 +190,18 @@ __host__ __device__ inline void b2_compress(B2State& s, const uint64_t m[16], ui
   }
   v[12] ^= t;
   if (last) v[14] = ~v[14];
-#pragma unroll
-  for (int r = 0; r < 12; ++r) {
-    GVS_B2G(0, 4, 8, 12, m[SG[r][0]], m[SG[r][1]]);
-    GVS_B2G(1, 5, 9, 13, m[SG[r][2]], m[SG[r][3]]);
-    GVS_B2G(2, 6, 10, 14, m[SG[r][4]], m[SG[r][5]]);
-    GVS_B2G(3, 7, 11, 15, m[SG[r][6]], m[SG[r][7]]);
-    GVS_B2G(0, 5, 10, 15, m[SG[r][8]], m[SG[r][9]]);
-    GVS_B2G(1, 6, 11, 12, m[SG[r][10]], m[SG[r][11]]);
-    GVS_B2G(2, 7, 8, 13, m[SG[r][12]], m[SG[r][13]]);
-    GVS_B2G(3, 4, 9, 14, m[SG[r][14]], m[SG[r][15]]);
-  }
+  b2_round<0>(v, m);
+  b2_round<1>(v, m);
+  b2_round<2>(v, m);
+  b2_round<3>(v, m);
+  b2_round<4>(v, m);
+  b2_round<5>(v, m);
+  b2_round<6>(v, m);
+  b2_round<7>(v, m);
+  b2_round<8>(v, m);
+  b2_round<9>(v, m);
+  b2_round<10>(v, m);
+  b2_round<11>(v, m);
 #pragma unroll
   for (int i = 0; i < 8; ++i) s.h[i] ^= v[i] ^ v[i + 8];
 }
@@ -165,7 +220,7 @@ __host__ __device__ inline B2State b2_init(uint32_t nn, uint32_t kk, uint64_t p0
 
 // leaf i of a row: BLAKE2b-128 of its 256 ciphertext bytes, person "gvs-leaf" | le64(i)
 constexpr uint64_t kLeafPerson0 = 0x6661656c2d737667ULL;  // "gvs-leaf" little-endian
-__host__ __device__ inline void leaf_digest(const uint64_t m[32], uint32_t i, uint64_t out[2]) {
+__host__ __device__ __attribute__((always_inline)) inline void leaf_digest(const uint64_t m[32], uint32_t i, uint64_t out[2]) {
   B2State s = b2_init(16, 0, kLeafPerson0, (uint64_t)i);
   b2_compress(s, m, 128, false);
   b2_compress(s, m + 16, 256, true);
@@ -175,7 +230,7 @@ __host__ __device__ inline void leaf_digest(const uint64_t m[32], uint32_t i, ui
 
 // tag from the state after the key block (keyed BLAKE2b-128, 32-byte key) and
 // the 96-byte header + leaves message
-__host__ __device__ inline void row_tag(const B2State& keyed, uint64_t row, uint32_t epoch,
+__host__ __device__ __attribute__((always_inline)) inline void row_tag(const B2State& keyed, uint64_t row, uint32_t epoch,
                                         uint32_t table, const uint64_t side[2],
                                         const uint64_t leaves[8], uint64_t out[2]) {
   uint64_t m[16];

@@ -595,7 +595,7 @@ static void launch_rpass(gvs_handle* h, const Engine& e, uint32_t n) {
   a.mtag = e.mtag;
   const dim3 g(e.W + kNullBlocks), b(256);
   if (h->auth) {
-    hipLaunchKernelGGL((k_rpass<16, true, true, 2, true>), g, b, 0, s, a);
+    hipLaunchKernelGGL((k_rpass<16, true, true, 1, true>), g, b, 0, s, a);
     return;
   }
   switch (h->rpass_variant) {

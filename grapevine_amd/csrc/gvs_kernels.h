@@ -553,7 +553,7 @@ __global__ __launch_bounds__(256) void k_m1(MArgs a) {
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_empt;
-  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
   __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar branches
@@ -960,7 +960,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t stash[kStash];
   __shared__ uint32_t s_first[kTile], s_cnt[kTile];
   __shared__ uint32_t s_tile[kRowsMax / kTile + 1];
-  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
   __shared__ uint4 s_st[AUTH ? 4 * stage_u4(U) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(256) void k_m2(MArgs a) {
   __shared__ Key128 s_key[256];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
-  __shared__ uint32_t s_te[AUTH ? 256 : 1];
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
   __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   __shared__ int16_t s_place[kSrMax];
   __shared__ uint8_t s_flag[kSrMax];

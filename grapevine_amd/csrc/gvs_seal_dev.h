@@ -20,8 +20,47 @@ constexpr uint32_t kSegU4 = 17;  // 256-B leaf segment + 16 B padding, in uint4
 // LDS bytes per wave for U rows: 4 segments per row + U side slots
 __host__ __device__ constexpr uint32_t stage_u4(int U) { return (uint32_t)U * 4 * kSegU4 + (uint32_t)U; }
 
+// stage slot of block `lane` of row u: 256-B leaf segments padded by 16 B
+__device__ inline uint32_t stage_slot(int u, uint32_t lane) {
+  return ((uint32_t)u * 4 + (lane >> 4)) * kSegU4 + (lane & 15);
+}
+
+// order the wave's LDS stores before its later LDS loads (and vice versa)
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The AES table lives in LDS as 64 interleaved replicas: entry x of replica
+// r at byte x * 256 + 4 r.  Lane l reads replica l, so the 32 lanes of a
+// ds_read_b32 half-wave always hit 32 distinct banks whatever the (secret,
+// data-dependent) indices are: no bank conflicts, and no timing that depends
+// on the key or the plaintext through conflicts.  The table is 64 KiB-aligned,
+// which puts it at LDS address 0, so a lookup address is a single v_perm_b32:
+// byte 1 = the state byte, byte 0 = 4 l.
+constexpr uint32_t kTeRep = 64;
+constexpr uint32_t kTeWords = 256 * kTeRep;  // 64 KiB
+#define GVS_TE_LDS __shared__ __attribute__((aligned(65536))) uint32_t
+
 __device__ inline void load_te(uint32_t* s_te, const uint32_t* g_te) {
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_te[i] = g_te[i];
+  for (uint32_t i = threadIdx.x; i < kTeWords; i += blockDim.x) s_te[i] = g_te[i / kTeRep];
+}
+
+struct LdsTe {
+  const uint32_t* base;  // s_te (at LDS address 0)
+  uint32_t lane4;        // 4 * lane
+};
+
+__device__ inline LdsTe lds_te(const uint32_t* s_te) { return LdsTe{s_te, lane_id() * 4u}; }
+
+__device__ inline uint32_t te_at(const LdsTe& t, uint32_t s, int k) {
+  const uint32_t off = __builtin_amdgcn_perm(s, t.lane4, 0x0c0c0400u | ((uint32_t)(4 + k) << 8));
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.base) + off);
+}
+
+__device__ inline uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 
 __device__ inline uint64_t shfl_u64(uint64_t x, int src) {
@@ -29,17 +68,94 @@ __device__ inline uint64_t shfl_u64(uint64_t x, int src) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// Tag of row row0 + ur, ur = (lane >> 2) % U, over the ciphertext rows v[]
-// and (mailbox rows) side ciphertexts staged at st[U*4*kSegU4 + u].
+// AES-128 of two counter blocks at once (the device form of
+// aes128_encrypt_words): each round first issues all 32 table lookups of both
+// blocks, then combines them.  sched_barrier keeps the compiler from
+// interleaving loads and uses (which it does under register pressure, leaving
+// one LDS latency exposed per lookup).
+__device__ inline void aes128_encrypt2(const AesRk& rk, const LdsTe& te, uint32_t (&a)[4],
+                                       uint32_t (&b)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] ^= rk.w[i];
+    b[i] ^= rk.w[i];
+  }
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    uint32_t la[16], lb[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        la[4 * i + k] = te_at(te, a[(i + k) & 3], 3 - k);
+        lb[4 * i + k] = te_at(te, b[(i + k) & 3], 3 - k);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = xor3(xor3(la[4 * i], ror32(la[4 * i + 1], 8), ror32(la[4 * i + 2], 16)),
+                  ror32(la[4 * i + 3], 24), rk.w[4 * r + i]);
+      b[i] = xor3(xor3(lb[4 * i], ror32(lb[4 * i + 1], 8), ror32(lb[4 * i + 2], 16)),
+                  ror32(lb[4 * i + 3], 24), rk.w[4 * r + i]);
+    }
+  }
+  uint32_t la[16], lb[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      la[4 * i + k] = te_at(te, a[(i + k) & 3], 3 - k);
+      lb[4 * i + k] = te_at(te, b[(i + k) & 3], 3 - k);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // last round: S-box bytes (te0 byte 1) in place, then AddRoundKey
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = ((la[4 * i] >> 8 & 0xffu) << 24 | (la[4 * i + 1] >> 8 & 0xffu) << 16 |
+            (la[4 * i + 2] >> 8 & 0xffu) << 8 | (la[4 * i + 3] >> 8 & 0xffu)) ^ rk.w[40 + i];
+    b[i] = ((lb[4 * i] >> 8 & 0xffu) << 24 | (lb[4 * i + 1] >> 8 & 0xffu) << 16 |
+            (lb[4 * i + 2] >> 8 & 0xffu) << 8 | (lb[4 * i + 3] >> 8 & 0xffu)) ^ rk.w[40 + i];
+  }
+}
+
+// keystream blocks j of rows ra and rb (same table, epoch) as little-endian words
+__device__ inline void ctr_keystream2(const AesRk& rk, const LdsTe& te, uint32_t table,
+                                      uint64_t ra, uint64_t rb, uint32_t epoch, uint32_t j,
+                                      uint4& ka, uint4& kb) {
+  uint32_t a[4] = {bswap32((uint32_t)ra), bswap32((uint32_t)(ra >> 32)), bswap32(epoch),
+                   (table << 24) | j};
+  uint32_t b[4] = {bswap32((uint32_t)rb), bswap32((uint32_t)(rb >> 32)), bswap32(epoch),
+                   (table << 24) | j};
+  aes128_encrypt2(rk, te, a, b);
+  ka = make_uint4(bswap32(a[0]), bswap32(a[1]), bswap32(a[2]), bswap32(a[3]));
+  kb = make_uint4(bswap32(b[0]), bswap32(b[1]), bswap32(b[2]), bswap32(b[3]));
+}
+
 template <int U>
-__device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0, uint32_t epoch,
-                                 const uint4 (&v)[U], bool with_side, uint4* st, uint64_t out[2]) {
+__device__ inline void stage_rows(const uint4 (&v)[U], uint4* st) {
   const uint32_t lane = lane_id();
 #pragma unroll
-  for (int u = 0; u < U; ++u) st[(u * 4 + (lane >> 4)) * kSegU4 + (lane & 15)] = v[u];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int u = 0; u < U; ++u) st[stage_slot(u, lane)] = v[u];
+  wave_lds_sync();
+}
+
+template <int U>
+__device__ inline void unstage_rows(uint4 (&v)[U], const uint4* st) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = st[stage_slot(u, lane)];
+  wave_lds_sync();
+}
+
+// Tag of row row0 + ur, ur = (lane >> 2) % U, over the ciphertext rows
+// already in the stage and (mailbox rows) side ciphertexts staged at
+// st[U*4*kSegU4 + u].
+template <int U>
+__device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0, uint32_t epoch,
+                                 bool with_side, const uint4* st, uint64_t out[2]) {
+  const uint32_t lane = lane_id();
   const uint32_t ur = (lane >> 2) % (uint32_t)U, leaf = lane & 3;
   uint64_t m[32];
   const uint4* seg = st + (ur * 4 + leaf) * kSegU4;
@@ -65,21 +181,28 @@ __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0
     sd[1] = u4hi(x);
   }
   row_tag(c.keyed, row0 + ur, epoch, table, sd, lv, out);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();  // the stage is reused by the caller
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// XOR the CTR keystream of (table, row0 + u, epoch) block `lane` into v[u]
+// XOR the CTR keystream of (table, row0 + u, epoch) block `lane` into the
+// staged rows, in place.  A rolled loop (one copy of the AES code, two
+// independent blocks per step); the rows are not held in registers meanwhile,
+// which leaves the AES lookups room to be issued back to back.
 template <int U>
-__device__ inline void wave_ctr(const SealCtx& c, const uint32_t* s_te, uint32_t table,
-                                uint64_t row0, uint32_t epoch, uint4 (&v)[U]) {
+__device__ inline void stage_ctr(const SealCtx& c, const uint32_t* s_te, uint32_t table,
+                                 uint64_t row0, uint32_t epoch, uint4* st) {
+  static_assert(U % 2 == 0, "rows come in pairs");
   const uint32_t lane = lane_id();
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint4 k = ctr_keystream(c.rk, s_te, table, row0 + u, epoch, lane);
-    v[u] = make_uint4(v[u].x ^ k.x, v[u].y ^ k.y, v[u].z ^ k.z, v[u].w ^ k.w);
+  const LdsTe te = lds_te(s_te);
+#pragma unroll 1
+  for (int u = 0; u < U; u += 2) {
+    uint4 k0, k1;
+    ctr_keystream2(c.rk, te, table, row0 + u, row0 + u + 1, epoch, lane, k0, k1);
+    uint4* p0 = st + stage_slot(u, lane);
+    uint4* p1 = st + stage_slot(u + 1, lane);
+    *p0 = xor4(*p0, k0);
+    *p1 = xor4(*p1, k1);
   }
+  wave_lds_sync();
 }
 
 // Verify and decrypt U rows read at c.epoch.  `tags` is the table's tag
@@ -89,12 +212,14 @@ template <int U>
 __device__ inline bool wave_unseal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                    uint64_t row0, uint4 (&v)[U], const uint4* tags, bool with_side,
                                    uint4* st) {
+  stage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, c.epoch, v, with_side, st, t);
+  wave_tags<U>(c, table, row0, c.epoch, with_side, st, t);
   const uint32_t ur = (lane_id() >> 2) % (uint32_t)U;
   const uint4 want = tags[row0 + ur];
   const bool bad = u4lo(want) != t[0] || u4hi(want) != t[1];
-  wave_ctr<U>(c, s_te, table, row0, c.epoch, v);
+  stage_ctr<U>(c, s_te, table, row0, c.epoch, st);
+  unstage_rows<U>(v, st);
   return __ballot(bad) == 0ull;
 }
 
@@ -104,9 +229,12 @@ template <int U>
 __device__ inline void wave_seal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                  uint64_t row0, uint32_t ep, uint4 (&v)[U], uint4* tags,
                                  bool with_side, uint4* st) {
-  wave_ctr<U>(c, s_te, table, row0, ep, v);
+  stage_rows<U>(v, st);
+  stage_ctr<U>(c, s_te, table, row0, ep, st);
+  unstage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, ep, v, with_side, st, t);
+  wave_tags<U>(c, table, row0, ep, with_side, st, t);
+  wave_lds_sync();  // the stage is reused by the caller
   const uint32_t lane = lane_id();
   if ((lane & 3u) == 0 && (lane >> 2) < (uint32_t)U)
     tags[row0 + (lane >> 2)] = make_uint4((uint32_t)t[0], (uint32_t)(t[0] >> 32), (uint32_t)t[1],
@@ -116,12 +244,9 @@ __device__ inline void wave_seal(const SealCtx& c, const uint32_t* s_te, uint32_
 // Keystream block 64 (the mailbox side entry) of `row` at `ep`.
 __device__ inline uint4 side_keystream(const SealCtx& c, const uint32_t* s_te, uint64_t row,
                                        uint32_t ep) {
-  return ctr_keystream(c.rk, s_te, 1u, row, ep, 64u);
+  return ctr_keystream(c.rk, lds_te(s_te), 1u, row, ep, 64u);
 }
 
-__device__ inline uint4 xor4(uint4 a, uint4 b) {
-  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
-}
 
 // Seal freshly initialised (all-zero) rows of a table at epoch 0; one wave
 // per 16 rows, grid-stride.  side != nullptr: mailbox table (+ side array).
@@ -129,7 +254,7 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
                                                    uint4* tags, uint4* side, uint32_t table,
                                                    uint64_t n_rows) {
   constexpr int U = 16;
-  __shared__ uint32_t s_te[256];
+  GVS_TE_LDS s_te[kTeWords];
   __shared__ uint4 s_st[4 * stage_u4(U)];
   load_te(s_te, g_te);
   __syncthreads();
