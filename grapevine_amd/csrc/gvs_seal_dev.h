@@ -68,20 +68,24 @@ __device__ inline uint64_t shfl_u64(uint64_t x, int src) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// AES-128 of two counter blocks at once (the device form of
-// aes128_encrypt_words): each round first issues all 32 table lookups of both
-// blocks, then combines them.  sched_barrier keeps the compiler from
-// interleaving loads and uses (which it does under register pressure, leaving
-// one LDS latency exposed per lookup).
-__device__ inline void aes128_encrypt2(const AesRk& rk, const LdsTe& te, uint32_t (&a)[4],
-                                       uint32_t (&b)[4]) {
+// S-box bytes of four lookups (byte 1 of each te0 entry) packed big-endian:
+// three v_perm_b32
+__device__ inline uint32_t sbox_pack(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3) {
+  const uint32_t hi = __builtin_amdgcn_perm(l0, l1, 0x05010c0cu);  // l0.b1 | l1.b1 | 0 | 0
+  const uint32_t lo = __builtin_amdgcn_perm(l2, l3, 0x0c0c0501u);  // 0 | 0 | l2.b1 | l3.b1
+  return hi | lo;
+}
+
+// AES-128 rounds R0..10 of two blocks at once (the device form of
+// aes128_encrypt_words; a[], b[] hold the state entering round R0).  Each
+// round first issues all 32 table lookups of both blocks, then combines them:
+// sched_barrier keeps the compiler from interleaving loads and uses (which it
+// does under register pressure, leaving one LDS latency exposed per lookup).
+template <int R0>
+__device__ inline void aes128_rounds2(const AesRk& rk, const LdsTe& te, uint32_t (&a)[4],
+                                      uint32_t (&b)[4]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    a[i] ^= rk.w[i];
-    b[i] ^= rk.w[i];
-  }
-#pragma unroll
-  for (int r = 1; r < 10; ++r) {
+  for (int r = R0; r < 10; ++r) {
     uint32_t la[16], lb[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -110,25 +114,53 @@ __device__ inline void aes128_encrypt2(const AesRk& rk, const LdsTe& te, uint32_
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  // last round: S-box bytes (te0 byte 1) in place, then AddRoundKey
+  // last round: SubBytes + ShiftRows (S-box = te0 byte 1), AddRoundKey
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    a[i] = ((la[4 * i] >> 8 & 0xffu) << 24 | (la[4 * i + 1] >> 8 & 0xffu) << 16 |
-            (la[4 * i + 2] >> 8 & 0xffu) << 8 | (la[4 * i + 3] >> 8 & 0xffu)) ^ rk.w[40 + i];
-    b[i] = ((lb[4 * i] >> 8 & 0xffu) << 24 | (lb[4 * i + 1] >> 8 & 0xffu) << 16 |
-            (lb[4 * i + 2] >> 8 & 0xffu) << 8 | (lb[4 * i + 3] >> 8 & 0xffu)) ^ rk.w[40 + i];
+    a[i] = sbox_pack(la[4 * i], la[4 * i + 1], la[4 * i + 2], la[4 * i + 3]) ^ rk.w[40 + i];
+    b[i] = sbox_pack(lb[4 * i], lb[4 * i + 1], lb[4 * i + 2], lb[4 * i + 3]) ^ rk.w[40 + i];
   }
 }
 
-// keystream blocks j of rows ra and rb (same table, epoch) as little-endian words
-__device__ inline void ctr_keystream2(const AesRk& rk, const LdsTe& te, uint32_t table,
-                                      uint64_t ra, uint64_t rb, uint32_t epoch, uint32_t j,
-                                      uint4& ka, uint4& kb) {
-  uint32_t a[4] = {bswap32((uint32_t)ra), bswap32((uint32_t)(ra >> 32)), bswap32(epoch),
-                   (table << 24) | j};
-  uint32_t b[4] = {bswap32((uint32_t)rb), bswap32((uint32_t)(rb >> 32)), bswap32(epoch),
-                   (table << 24) | j};
-  aes128_encrypt2(rk, te, a, b);
+// Counter blocks of one lane over a chunk of rows row0 .. row0 + U - 1 (U
+// divides 256, row0 a multiple of U) differ only in the low byte of the row,
+// which AES round 1 reads once (the byte-3 lookup of word 0).  Round 1 is
+// therefore computed once per chunk without that term; per block it costs one
+// lookup (ctr_round1_finish).
+struct CtrRound1 {
+  uint32_t t[4];  // round-1 output, t[0] still missing T0[x0.b3]
+  uint32_t x0b3;  // byte 3 of x0 = bswap(row0 lo) ^ rk0, for the low row byte
+};
+
+__device__ inline CtrRound1 ctr_round1_chunk(const AesRk& rk, const LdsTe& te, uint32_t table,
+                                             uint64_t row0, uint32_t epoch, uint32_t j) {
+  const uint32_t x0 = bswap32((uint32_t)row0) ^ rk.w[0];
+  const uint32_t x1 = bswap32((uint32_t)(row0 >> 32)) ^ rk.w[1];
+  const uint32_t x2 = bswap32(epoch) ^ rk.w[2];
+  const uint32_t x3 = ((table << 24) | j) ^ rk.w[3];
+  const uint32_t x[4] = {x0, x1, x2, x3};
+  uint32_t l[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) l[4 * i + k] = (i == 0 && k == 0) ? 0u : te_at(te, x[(i + k) & 3], 3 - k);
+  CtrRound1 c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    c.t[i] = xor3(xor3(l[4 * i], ror32(l[4 * i + 1], 8), ror32(l[4 * i + 2], 16)),
+                  ror32(l[4 * i + 3], 24), rk.w[4 + i]);
+  c.x0b3 = x0 >> 24;
+  return c;
+}
+
+// keystream blocks j of rows row0 + u and row0 + u + 1 as little-endian words
+__device__ inline void ctr_keystream2(const AesRk& rk, const LdsTe& te, const CtrRound1& c1,
+                                      uint32_t u, uint4& ka, uint4& kb) {
+  const uint32_t ta = te_at(te, (c1.x0b3 ^ u) << 24, 3);
+  const uint32_t tb = te_at(te, (c1.x0b3 ^ (u + 1)) << 24, 3);
+  uint32_t a[4] = {c1.t[0] ^ ta, c1.t[1], c1.t[2], c1.t[3]};
+  uint32_t b[4] = {c1.t[0] ^ tb, c1.t[1], c1.t[2], c1.t[3]};
+  aes128_rounds2<2>(rk, te, a, b);
   ka = make_uint4(bswap32(a[0]), bswap32(a[1]), bswap32(a[2]), bswap32(a[3]));
   kb = make_uint4(bswap32(b[0]), bswap32(b[1]), bswap32(b[2]), bswap32(b[3]));
 }
@@ -190,13 +222,14 @@ __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0
 template <int U>
 __device__ inline void stage_ctr(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                  uint64_t row0, uint32_t epoch, uint4* st) {
-  static_assert(U % 2 == 0, "rows come in pairs");
+  static_assert(U % 2 == 0 && 256 % U == 0, "rows come in pairs; a chunk stays in one 256-row block");
   const uint32_t lane = lane_id();
   const LdsTe te = lds_te(s_te);
+  const CtrRound1 c1 = ctr_round1_chunk(c.rk, te, table, row0, epoch, lane);
 #pragma unroll 1
   for (int u = 0; u < U; u += 2) {
     uint4 k0, k1;
-    ctr_keystream2(c.rk, te, table, row0 + u, row0 + u + 1, epoch, lane, k0, k1);
+    ctr_keystream2(c.rk, te, c1, (uint32_t)u, k0, k1);
     uint4* p0 = st + stage_slot(u, lane);
     uint4* p1 = st + stage_slot(u + 1, lane);
     *p0 = xor4(*p0, k0);

@@ -1,7 +1,8 @@
 """Data-independence of the engine (north_star obliviousness contract,
 api/proto/grapevine.proto:120-122): for batches of the same size, the kernel
 launch sequence, the grid/workgroup sizes and the HBM byte counters
-(rocprofv3 FETCH_SIZE, WRITE_SIZE) must not depend on the request mix.
+(rocprofv3 FETCH_SIZE, WRITE_SIZE) must not depend on the request mix, with and
+without authenticated storage.
 
 Each mix runs tools/oblivious_probe.py under rocprofv3 in a child process
 (one --kernel-trace run, one --pmc run per counter; counters are never
@@ -22,12 +23,12 @@ PROBE = os.path.join(ROOT, "tools", "oblivious_probe.py")
 MIXES = ["main", "all_create", "all_miss_read", "hot_next", "deletes"]
 
 
-def rocprof(args, mix, outdir):
+def rocprof(args, mix, outdir, auth=False):
     if shutil.which("rocprofv3") is None:
         pytest.skip("rocprofv3 not available")
     os.makedirs(outdir, exist_ok=True)
     cmd = ["rocprofv3"] + args + ["-d", outdir, "-o", "run", "--output-format", "csv", "--",
-                                  sys.executable, PROBE, mix]
+                                  sys.executable, PROBE, mix] + (["--auth"] if auth else [])
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
@@ -50,12 +51,12 @@ def short(name):
     return name.split("(")[0].replace("void ", "").replace("gvs::", "")
 
 
-@pytest.fixture(scope="module")
-def traces(tmp_path_factory):
+@pytest.fixture(scope="module", params=[False, True], ids=["plain", "auth"])
+def traces(request, tmp_path_factory):
     base = tmp_path_factory.mktemp("obl")
     out = {}
     for mix in MIXES:
-        d = rocprof(["--kernel-trace"], mix, str(base / f"kt_{mix}"))
+        d = rocprof(["--kernel-trace"], mix, str(base / f"kt_{mix}"), auth=request.param)
         rows = gvs_rows(os.path.join(d, "**", "*kernel_trace.csv"))
         out[mix] = [(short(r["Kernel_Name"]), r.get("Grid_Size", r.get("Grid_Size_X")),
                      r.get("Workgroup_Size", r.get("Workgroup_Size_X"))) for r in rows]
@@ -70,18 +71,24 @@ def test_launch_sequence_and_grids_identical(traces):
 
 
 def split_batches(vals):
-    out, cur = [], []
+    """Per-batch lists of (kernel, value); launches before the first batch
+    (k_seal_init at store creation) are dropped."""
+    out, cur = [], None
     for k, v in vals:
-        if k == "k_copy" and cur:
-            out.append(cur)
+        if k == "k_copy":
+            if cur:
+                out.append(cur)
             cur = []
-        cur.append((k, v))
-    out.append(cur)
+        if cur is not None:
+            cur.append((k, v))
+    if cur:
+        out.append(cur)
     return out
 
 
+@pytest.mark.parametrize("auth", [False, True], ids=["plain", "auth"])
 @pytest.mark.parametrize("counter", ["FETCH_SIZE", "WRITE_SIZE"])
-def test_hbm_bytes_identical(counter, tmp_path):
+def test_hbm_bytes_identical(counter, auth, tmp_path):
     """Per kernel, the byte counter of every measured batch of every mix must
     equal main's within the counter's own run-to-run noise: the spread of one
     prefill batch (identical in every process) across the processes (floor:
@@ -89,7 +96,7 @@ def test_hbm_bytes_identical(counter, tmp_path):
     is not under program control (obliviousness)."""
     per_mix = {}
     for mix in MIXES:
-        d = rocprof(["--pmc", counter], mix, str(tmp_path / f"{counter}_{mix}"))
+        d = rocprof(["--pmc", counter], mix, str(tmp_path / f"{counter}_{mix}"), auth=auth)
         rows = gvs_rows(os.path.join(d, "**", "*counter_collection.csv"))
         vals = [(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
                 if r.get("Counter_Name", counter) == counter]
@@ -114,7 +121,8 @@ def test_hbm_bytes_identical(counter, tmp_path):
                 bad.append((k, mix, dev, tol))
         lines.append(" ".join(row))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", f"oblivious_{counter}.txt"), "w") as f:
+    tag = "_auth" if auth else ""
+    with open(os.path.join(ROOT, "gpurun_out", f"oblivious_{counter}{tag}.txt"), "w") as f:
         for mix, bs in per_mix.items():
             f.write(f"{mix}: " + " ".join(f"{k}={v:.0f}" for b in bs for k, v in b) + "\n")
         f.write("\n".join(lines) + "\n")

@@ -29,8 +29,9 @@ def main():
     p.add_argument("--log2n", type=int, default=20)
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--batches", type=int, default=3)
+    p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
     a = p.parse_args()
-    cfg = abi.make_config(1 << a.log2n, max_batch=a.batch)
+    cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth)
     store = ObliviousStore(cfg)
     model = ffi.Model(cfg)
     model.seed(77)
