@@ -253,6 +253,19 @@ __device__ inline void keep4(uint4& x) {
 
 // c ? x : y per component through a mask the optimiser cannot turn back into
 // an indexed access (which would move a register array to scratch)
+// c ? x : y as mask arithmetic the compiler cannot turn into a branch
+__device__ inline uint32_t selu32(bool c, uint32_t x, uint32_t y) {
+  uint32_t m = 0u - (uint32_t)c;
+  asm volatile("" : "+v"(m));
+  return (x & m) | (y & ~m);
+}
+__device__ inline uint64_t selu64(bool c, uint64_t x, uint64_t y) {
+  uint32_t m = 0u - (uint32_t)c;
+  asm volatile("" : "+v"(m));
+  const uint64_t mm = ((uint64_t)m << 32) | m;
+  return (x & mm) | (y & ~mm);
+}
+
 __device__ inline uint4 sel4(uint32_t c, uint4 x, uint4 y) {
   uint32_t m = 0u - c;
   asm volatile("" : "+v"(m));

@@ -488,15 +488,32 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
 
 // ------------------------------------------------------------------ pipeline
 
-template <typename K, int LMAX>
-static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
-  const uint32_t L = n < (uint32_t)LMAX ? n : (uint32_t)LMAX;
-  hipStream_t s = h->stream;
-  hipLaunchKernelGGL((k_bitonic_local<K, LMAX>), dim3(n / L), dim3(1024), 0, s, d, L, 0u, 1);
+// Bitonic sort of n keys (n a power of two >= 1024): tiles of L = 1024 E keys
+// sorted in registers/LDS, then for each larger merge level the global steps
+// (two per launch) and the tile-local finish.
+template <typename K, int E>
+static void sort_tiles(hipStream_t s, K* d, uint32_t n) {
+  constexpr uint32_t L = 1024u * E;
+  hipLaunchKernelGGL((k_bitonic_tile<K, E>), dim3(n / L), dim3(1024), 0, s, d, 0u, 1);
   for (uint32_t k = 2 * L; k <= n; k <<= 1) {
-    for (uint32_t j = k >> 1; j >= L; j >>= 1)
+    uint32_t j = k >> 1;
+    for (; j >= 2 * L; j >>= 2)  // two steps per launch while both are global
+      hipLaunchKernelGGL(k_bitonic_global2<K>, dim3((n / 4 + 255) / 256), dim3(256), 0, s, d, n, k, j);
+    if (j >= L)
       hipLaunchKernelGGL(k_bitonic_global<K>, dim3((n / 2 + 255) / 256), dim3(256), 0, s, d, n, k, j);
-    hipLaunchKernelGGL((k_bitonic_local<K, LMAX>), dim3(n / L), dim3(1024), 0, s, d, L, k, 0);
+    hipLaunchKernelGGL((k_bitonic_tile<K, E>), dim3(n / L), dim3(1024), 0, s, d, k, 0);
+  }
+}
+
+template <typename K, int EMAX>
+static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
+  if (n < 1024 || !is_pow2(n)) return GVS_ERR_INTERNAL;
+  const uint32_t e = n / 1024 < (uint32_t)EMAX ? n / 1024 : (uint32_t)EMAX;
+  switch (e) {
+    case 1: sort_tiles<K, 1>(h->stream, d, n); break;
+    case 2: sort_tiles<K, 2>(h->stream, d, n); break;
+    case 4: sort_tiles<K, (EMAX < 4 ? EMAX : 4)>(h->stream, d, n); break;
+    default: sort_tiles<K, EMAX>(h->stream, d, n); break;
   }
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
@@ -563,7 +580,7 @@ static int phase_a(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride,
     hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
   }
   mark(h, "meta");
-  if (int r = sort_keys<Key128, 4096>(h, e.s1keys, B)) return r;
+  if (int r = sort_keys<Key128, 4>(h, e.s1keys, B)) return r;
   mark(h, "sort_s1");
   if (h->auth)
     hipLaunchKernelGGL(k_m1<true>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
@@ -628,7 +645,7 @@ static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.pcount, e.pstart, e.W + 1);
   }
   mark(h, "alloc");
-  if (int r = sort_keys<uint64_t, 8192>(h, e.rkeys, B)) return r;
+  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
   mark(h, "sort_r");
   launch_rpass(h, e, n);
   mark(h, "rpass");

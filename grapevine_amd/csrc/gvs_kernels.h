@@ -37,34 +37,126 @@ __device__ inline bool key_lt<Key128>(const Key128& a, const Key128& b) {
   return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo);
 }
 
-// Sorts (full=1) or finishes a merge level k (full=0) inside tiles of L keys.
-template <typename K, int LMAX>
-__global__ __launch_bounds__(1024) void k_bitonic_local(K* data, uint32_t L, uint32_t kmerge,
-                                                        int full) {
-  __shared__ K s[LMAX];
+// c ? a : b per component (a select of whole structs goes through scratch)
+__device__ inline uint64_t key_sel(bool c, uint64_t a, uint64_t b) { return c ? a : b; }
+__device__ inline Key128 key_sel(bool c, const Key128& a, const Key128& b) {
+  return Key128{c ? a.hi : b.hi, c ? a.lo : b.lo};
+}
+
+__device__ inline uint64_t shfl_xor_key(uint64_t a, uint32_t m) {
+  const uint32_t lo = __shfl_xor((uint32_t)a, (int)m), hi = __shfl_xor((uint32_t)(a >> 32), (int)m);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ inline Key128 shfl_xor_key(const Key128& a, uint32_t m) {
+  return Key128{shfl_xor_key(a.hi, m), shfl_xor_key(a.lo, m)};
+}
+
+// compare-exchange of one element with its partner's copy: keep the smaller
+// key if this element is the lower one of an ascending pair (or the upper
+// one of a descending pair), else the larger
+template <typename K>
+__device__ inline K cmpex_keep(const K& mine, const K& other, bool keep_min) {
+  const bool lt = key_lt(other, mine);
+  return key_sel(lt == keep_min, other, mine);
+}
+
+// Bitonic sort inside tiles of L = 1024 * E keys (full = 1), or the last
+// steps j = L/2 .. 1 of merge level kmerge (full = 0).  Thread t holds keys
+// t*E .. t*E + E - 1 in registers: steps j < E are register compare-exchanges,
+// steps E <= j < 64 E exchange with lane t ^ (j / E) by shuffles, and only
+// steps j >= 64 E go through LDS with a barrier each (Key128, 4096-key tiles:
+// 10 of the 78 steps of a full tile sort).  The sequence of operations does
+// not depend on the keys (a sorting network).
+template <typename K, int E>
+__global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge, int full) {
+  constexpr uint32_t L = 1024u * E;
+  __shared__ K s[L];
+  const uint32_t t = threadIdx.x, lane = lane_id();
   const uint32_t base = blockIdx.x * L;
-  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) s[i] = data[base + i];
-  __syncthreads();
-  uint32_t k_begin = full ? 2u : kmerge, k_end = full ? L : kmerge;
-  for (uint32_t k = k_begin; k <= k_end; k <<= 1) {
-    uint32_t j0 = full ? (k >> 1) : (L >> 1);
-    for (uint32_t j = j0; j > 0; j >>= 1) {
-      for (uint32_t p = threadIdx.x; p < (L >> 1); p += blockDim.x) {
-        uint32_t i = ((p / j) * 2u * j) + (p % j);
-        uint32_t pj = i + j;
-        bool asc = (((base + i) & k) == 0u);
-        K a = s[i], b = s[pj];
-        bool sw = asc ? key_lt(b, a) : key_lt(a, b);
-        if (sw) {
-          s[i] = b;
-          s[pj] = a;
+  K r[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) r[e] = data[base + t * E + e];
+  const uint32_t k_lo = full ? 2u : kmerge, k_hi = full ? L : kmerge;
+  for (uint32_t k = k_lo; k <= k_hi; k <<= 1) {
+    const uint32_t j_top = full ? (k >> 1) : (L >> 1);
+    // steps through LDS
+    if (j_top >= 64u * E) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) s[t * E + e] = r[e];
+      __syncthreads();
+      for (uint32_t j = j_top; j >= 64u * E; j >>= 1) {
+        for (uint32_t p = t; p < (L >> 1); p += 1024u) {
+          const uint32_t i = ((p / j) * 2u * j) + (p % j);
+          const bool asc = ((base + i) & k) == 0u;
+          const K a = s[i], b = s[i + j];
+          const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+          s[i] = key_sel(sw, b, a);
+          s[i + j] = key_sel(sw, a, b);
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) r[e] = s[t * E + e];
+      __syncthreads();  // s is rewritten by the next level
+    }
+    // steps across lanes
+    for (uint32_t m = min(j_top, 32u * E) / E; m >= 1u; m >>= 1) {
+      const bool lower = (lane & m) == 0u;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bool asc = ((base + t * E + e) & k) == 0u;
+        r[e] = cmpex_keep(r[e], shfl_xor_key(r[e], m), lower == asc);
+      }
+    }
+    // steps inside the thread's registers
+#pragma unroll
+    for (uint32_t j = E / 2; j >= 1u; j >>= 1) {
+      if (j <= j_top) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if ((e & j) == 0u) {
+            const bool asc = ((base + t * E + e) & k) == 0u;
+            const K a = r[e], b = r[e | j];
+            const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+            r[e] = key_sel(sw, b, a);
+            r[e | j] = key_sel(sw, a, b);
+          }
         }
       }
-      __syncthreads();
     }
-    if (!full) break;
   }
-  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) data[base + i] = s[i];
+#pragma unroll
+  for (int e = 0; e < E; ++e) data[base + t * E + e] = r[e];
+}
+
+// Two steps (j, j/2) of merge level k over the whole array: each thread owns
+// the four keys i0, i0 + j/2, i0 + j, i0 + 3j/2.
+template <typename K>
+__global__ __launch_bounds__(256) void k_bitonic_global2(K* data, uint32_t n, uint32_t k,
+                                                         uint32_t j) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (n >> 2)) return;
+  const uint32_t h = j >> 1;
+  // a group of 2j indices holds h quadruples x0, x0 + h, x0 + j, x0 + j + h
+  const uint32_t g = p / h, o = p % h;
+  const uint32_t x0 = g * 2u * j + o;  // bits h and j of x0 are zero
+  const uint32_t x1 = x0 + h, x2 = x0 + j, x3 = x0 + j + h;
+  const bool asc = (x0 & k) == 0u;
+  K v0 = data[x0], v1 = data[x1], v2 = data[x2], v3 = data[x3];
+  auto cx = [&](K& a, K& b) {
+    const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+    const K ta = a;
+    a = key_sel(sw, b, a);
+    b = key_sel(sw, ta, b);
+  };
+  cx(v0, v2);
+  cx(v1, v3);
+  cx(v0, v1);
+  cx(v2, v3);
+  data[x0] = v0;
+  data[x1] = v1;
+  data[x2] = v2;
+  data[x3] = v3;
 }
 
 template <typename K>
@@ -186,52 +278,56 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   const bool id_zero = !nz4(c0);
   const bool auth_zero = !nz4(c1) && !nz4(c2);
   const bool rcpt_zero = !nz4(c3) && !nz4(c4);
-  uint32_t kind = 0xFFFFFFFFu, pre = kPending, cls = 3, sub = 0;
-  uint4 xa = c3, xb = c4;  // mailbox key: recipient, or auth for next ops
-  if (i >= a.n) {
-    kind = KIND_PAD;
-    pre = 0;
-  } else if (type < 1u || type > 4u || auth_zero || (type == 3u && id_zero)) {
-    kind = KIND_HARD;  // grapevine.proto:57-64, :95 fail-fast
-    pre = 0;
-  } else if (type == 1u) {
-    kind = KIND_CREATE;
-    if (rcpt_zero) pre = 4;  // INVALID_RECIPIENT, grapevine.proto:72
-    else cls = 1;
-  } else if ((type == 2u || type == 4u) && id_zero) {
-    kind = type == 2u ? KIND_NEXT_READ : KIND_NEXT_DEL;
-    cls = 0;
-    sub = type == 4u ? 1u : 0u;
-    xa = c1;
-    xb = c2;
-  }
+  // Classification without branches: every op runs the same instructions
+  // (a skipped branch would leave its code lines unfetched, and instruction
+  // fetch shows up in FETCH_SIZE; DESIGN.md §3 rule 6).  Conditions combine
+  // with bitwise operators (no short-circuit control flow) and every select
+  // chooses between values already computed.
+  const bool pad = i >= a.n;
+  const bool hard = (type < 1u) | (type > 4u) | auth_zero | ((type == 3u) & id_zero);
+  const bool create = type == 1u;
+  const bool next = ((type == 2u) | (type == 4u)) & id_zero;
   const uint32_t dec = id_decode(a.kc, u4lo(c0), u4hi(c0), a.N);  // every op: fixed work
-  if (kind == 0xFFFFFFFFu) {
-    const uint32_t s = dec;
-    kind = type == 2u ? KIND_READ : (type == 3u ? KIND_UPDATE : KIND_DELETE);
-    o.slot = s;
-    if (s == kNone) pre = 2;  // NOT_FOUND: the id names no slot
-    else if (kind == KIND_DELETE && !rcpt_zero) cls = 2;
-  }
+  const bool nodec = dec == kNone;
+  const uint32_t byid_kind =
+      selu32(type == 2u, KIND_READ, selu32(type == 3u, KIND_UPDATE, KIND_DELETE));
+  const uint32_t next_kind = selu32(type == 2u, KIND_NEXT_READ, KIND_NEXT_DEL);
+  const bool fail = pad | hard;
+  const bool byid = !fail & !create & !next;
+  uint32_t kind = selu32(next, next_kind, byid_kind);
+  kind = selu32(create, KIND_CREATE, kind);
+  kind = selu32(hard, KIND_HARD, kind);
+  kind = selu32(pad, KIND_PAD, kind);
+  // grapevine.proto:57-64, :95 fail-fast; :72 INVALID_RECIPIENT; NOT_FOUND
+  // when the id names no slot
+  uint32_t pre = selu32(byid & nodec, 2u, kPending);
+  pre = selu32(create, selu32(rcpt_zero, 4u, kPending), pre);
+  pre = selu32(fail, 0u, pre);
+  uint32_t cls = selu32((byid_kind == KIND_DELETE) & !nodec & !rcpt_zero, 2u, 3u);
+  cls = selu32(next, 0u, cls);
+  cls = selu32(create, selu32(rcpt_zero, 3u, 1u), cls);
+  cls = selu32(fail, 3u, cls);
+  const uint32_t sub = (uint32_t)(next & (type == 4u));
+  o.slot = selu32(byid, dec, kNone);
+  const uint4 xa = sel4(next, c1, c3), xb = sel4(next, c2, c4);  // mailbox key: recipient, or auth
   o.x[0] = xa.x; o.x[1] = xa.y; o.x[2] = xa.z; o.x[3] = xa.w;
   o.x[4] = xb.x; o.x[5] = xb.y; o.x[6] = xb.z; o.x[7] = xb.w;
   Key128 key;
-  uint32_t q = a.Q;
+  uint32_t q;
   {
     // the PRF runs for every op (fixed work); only participants use it
     const uint64_t x[4] = {u4lo(xa), u4hi(xa), u4lo(xb), u4hi(xb)};
     uint64_t hi, lo;
     recipient_hash(a.kc, x, hi, lo);
-    if (cls < 3) {
-      o.h_hi = hi;
-      o.h_lo = lo;
-      q = a.logQ ? (uint32_t)(hi >> (64 - a.logQ)) : 0u;
-      key.hi = hi;
-      key.lo = s1_lo(lo, cls, i, sub);
-    } else {
-      key.hi = ~0ull;
-      key.lo = (~0ull << 21) | ((uint64_t)i << 1);
-    }
+    const bool part = cls < 3u;
+    const uint32_t q_part = a.logQ ? (uint32_t)(hi >> (64 - a.logQ)) : 0u;
+    const uint64_t lo_part = s1_lo(lo, cls, i, sub);
+    const uint64_t lo_none = (~0ull << 21) | ((uint64_t)i << 1);
+    o.h_hi = selu64(part, hi, 0ull);
+    o.h_lo = selu64(part, lo, 0ull);
+    q = selu32(part, q_part, a.Q);
+    key.hi = selu64(part, hi, ~0ull);
+    key.lo = selu64(part, lo_part, lo_none);
   }
   o.kind = kind;
   o.pre_status = pre;
