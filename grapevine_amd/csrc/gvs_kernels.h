@@ -789,7 +789,12 @@ struct AllocArgs {
   KeyCtx kc;
 };
 
-// seq-order compact flags (coalesced, fixed) + per-block counts
+constexpr uint32_t kWinGroup = 8;      // blocks per allocation-window refill
+constexpr uint32_t kWinRing = 16384;  // LDS window ring: one group + one chunk fits
+
+// seq-order compact flags (coalesced, fixed) + per-block counts; pflag holds
+// bit 0 pop, bit 1 mailbox-ok create, bits 2..11 / 12..21 their in-block
+// exclusive prefixes
 __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
   __shared__ uint32_t s_w[16];
   if (a.scal->error) return;
@@ -798,11 +803,11 @@ __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
   const uint32_t kind = a.kinds[i];
   const bool pop = (m1.flags & CF_POP) != 0u;
   const bool s = (m1.flags & CF_MBOX_OK) != 0u && kind == KIND_CREATE;
-  a.pflag[i] = (pop ? 1u : 0u) | (s ? 2u : 0u);
   a.pslot[i] = m1.slot;
   uint32_t tp, ts;
-  (void)block1024_prefix(pop, s_w, &tp);
-  (void)block1024_prefix(s, s_w, &ts);
+  const uint32_t pp = block1024_prefix(pop, s_w, &tp);
+  const uint32_t ps = block1024_prefix(s, s_w, &ts);
+  a.pflag[i] = (pop ? 1u : 0u) | (s ? 2u : 0u) | (pp << 2) | (ps << 12);
   if (threadIdx.x == 0) {
     a.bsum[2 * blockIdx.x] = tp;
     a.bsum[2 * blockIdx.x + 1] = ts;
@@ -816,7 +821,7 @@ __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
 __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   __shared__ uint32_t s_w[16];
   __shared__ uint32_t s_off[2][1024];
-  __shared__ uint32_t s_win[2048];
+  __shared__ uint32_t s_win[kWinRing];
   const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
   // block offsets (nblk <= 1024)
@@ -837,42 +842,41 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   const uint64_t count1 = sc->count - pops;
   const uint64_t room = a.N - count1;
   const uint64_t m = scnt < room ? scnt : room;
-  // (1) pops -> ring
+  // (1) pops -> ring.  In-block prefixes come from k_alloc_sum (pflag bits
+  // 2..11), so the blocks are independent: no barrier, loads in flight
+  // together.
   for (uint32_t c = 0; c < a.nblk; ++c) {
     const uint32_t i = c * 1024 + tid;
     const uint32_t f = a.pflag[i], slot = a.pslot[i];
     const bool pop = f & 1u;
-    uint32_t tot;
-    const uint32_t pre = block1024_prefix(pop, s_w, &tot);
-    const uint32_t P = (c ? s_off[0][c - 1] : 0u) + pre;
+    const uint32_t P = (c ? s_off[0][c - 1] : 0u) + ((f >> 2) & 1023u);
     const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
     a.ring[(tail0 + pos) % a.ring_size] = pop ? slot : kNone;
   }
   __threadfence_block();
   __syncthreads();
-  // (2) allocation window, streamed in order through a 2048-entry LDS ring
+  // (2) allocation window [head, head + B), read in order in 1024-entry
+  // chunks through an LDS ring; groups of 8 blocks (8192 ops) share one
+  // refill and two barriers
   uint32_t loaded = 0;  // window entries loaded so far (multiple of 1024)
-  for (uint32_t c = 0; c < a.nblk; ++c) {
-    const uint32_t i = c * 1024 + tid;
-    const bool s = a.pflag[i] & 2u;
-    uint32_t tot;
-    const uint32_t pre = block1024_prefix(s, s_w, &tot);
-    const uint32_t S0 = c ? s_off[1][c - 1] : 0u;
-    const uint32_t Si = S0 + pre;
-    const uint32_t need = (uint32_t)min((uint64_t)(S0 + tot), m);
-    while (loaded < need) {  // uniform across the block
-      s_win[(loaded + tid) & 2047u] = a.ring[(head0 + loaded + tid) % a.ring_size];
-      loaded += 1024;
-      __syncthreads();
-    }
-    const bool success = s && (uint64_t)Si < m;
-    a.cslot[i] = success ? s_win[Si & 2047u] : kNone;
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += kWinGroup) {
+    const uint32_t c1 = min(c0 + kWinGroup, a.nblk);
+    const uint32_t need = (uint32_t)min((uint64_t)s_off[1][c1 - 1], m);
+    for (; loaded < need; loaded += 1024)  // uniform across the block
+      s_win[(loaded + tid) & (kWinRing - 1u)] = a.ring[(head0 + loaded + tid) % a.ring_size];
     __syncthreads();
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t i = c * 1024 + tid;
+      const uint32_t f = a.pflag[i];
+      const uint32_t Si = (c ? s_off[1][c - 1] : 0u) + ((f >> 12) & 1023u);
+      const bool success = (f & 2u) && (uint64_t)Si < m;
+      a.cslot[i] = success ? s_win[Si & (kWinRing - 1u)] : kNone;
+    }
+    __syncthreads();  // the next refill overwrites the ring
   }
-  while (loaded < a.B) {  // read the rest of the window: fixed B entries per batch
+  for (; loaded < a.B; loaded += 1024) {  // read the rest of the window: fixed B entries per batch
     const uint32_t v = a.ring[(head0 + loaded + tid) % a.ring_size];
     asm volatile("" ::"v"(v));
-    loaded += 1024;
   }
   if (tid == 0) {
     sc->pops = pops;
@@ -1178,10 +1182,10 @@ __global__ __launch_bounds__(1024) void k_post_sum(PostArgs a) {
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const uint32_t st = a.rres[i].status, slot = a.rop[i].slot;
   const bool d = a.kinds[i] == KIND_DELETE && st == 1u;
-  a.dflag[i] = d ? 1u : 0u;
   a.dslot[i] = slot;
   uint32_t tot;
-  (void)block1024_prefix(d, s_w, &tot);
+  const uint32_t pre = block1024_prefix(d, s_w, &tot);
+  a.dflag[i] = (d ? 1u : 0u) | (pre << 1);  // flag + in-block exclusive prefix
   if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
 }
 
@@ -1204,11 +1208,10 @@ __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
   const uint64_t tail = sc->tail0 + sc->pops;
   for (uint32_t c = 0; c < a.nblk; ++c) {
     const uint32_t i = c * 1024 + tid;
-    const bool d = a.dflag[i] != 0u;
+    const uint32_t f = a.dflag[i];
+    const bool d = f & 1u;
     const uint32_t slot = a.dslot[i];
-    uint32_t tot;
-    const uint32_t pre = block1024_prefix(d, s_w, &tot);
-    const uint32_t P = (c ? s_off[c - 1] : 0u) + pre;
+    const uint32_t P = (c ? s_off[c - 1] : 0u) + (f >> 1);  // no barrier: blocks independent
     const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
     a.ring[(tail + pos) % a.ring_size] = d ? slot : kNone;
   }
