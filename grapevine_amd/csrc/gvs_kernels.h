@@ -845,13 +845,24 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   // (1) pops -> ring.  In-block prefixes come from k_alloc_sum (pflag bits
   // 2..11), so the blocks are independent: no barrier, loads in flight
   // together.
-  for (uint32_t c = 0; c < a.nblk; ++c) {
-    const uint32_t i = c * 1024 + tid;
-    const uint32_t f = a.pflag[i], slot = a.pslot[i];
-    const bool pop = f & 1u;
-    const uint32_t P = (c ? s_off[0][c - 1] : 0u) + ((f >> 2) & 1023u);
-    const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
-    a.ring[(tail0 + pos) % a.ring_size] = pop ? slot : kNone;
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += kWinGroup) {
+    uint32_t f[kWinGroup], slot[kWinGroup];  // loads of 8 blocks in flight together
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t i = (c0 + u) * 1024 + tid;
+      f[u] = c0 + u < a.nblk ? a.pflag[i] : 0u;
+      slot[u] = c0 + u < a.nblk ? a.pslot[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t c = c0 + u, i = c * 1024 + tid;
+      if (c < a.nblk) {
+        const bool pop = f[u] & 1u;
+        const uint32_t P = (c ? s_off[0][c - 1] : 0u) + ((f[u] >> 2) & 1023u);
+        const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
+        a.ring[(tail0 + pos) % a.ring_size] = pop ? slot[u] : kNone;
+      }
+    }
   }
   __threadfence_block();
   __syncthreads();
@@ -865,12 +876,17 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
     for (; loaded < need; loaded += 1024)  // uniform across the block
       s_win[(loaded + tid) & (kWinRing - 1u)] = a.ring[(head0 + loaded + tid) % a.ring_size];
     __syncthreads();
-    for (uint32_t c = c0; c < c1; ++c) {
-      const uint32_t i = c * 1024 + tid;
-      const uint32_t f = a.pflag[i];
-      const uint32_t Si = (c ? s_off[1][c - 1] : 0u) + ((f >> 12) & 1023u);
-      const bool success = (f & 2u) && (uint64_t)Si < m;
-      a.cslot[i] = success ? s_win[Si & (kWinRing - 1u)] : kNone;
+    uint32_t f[kWinGroup];
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) f[u] = c0 + u < c1 ? a.pflag[(c0 + u) * 1024 + tid] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t c = c0 + u, i = c * 1024 + tid;
+      if (c < c1) {
+        const uint32_t Si = (c ? s_off[1][c - 1] : 0u) + ((f[u] >> 12) & 1023u);
+        const bool success = (f[u] & 2u) && (uint64_t)Si < m;
+        a.cslot[i] = success ? s_win[Si & (kWinRing - 1u)] : kNone;
+      }
     }
     __syncthreads();  // the next refill overwrites the ring
   }
@@ -1206,14 +1222,24 @@ __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
   const uint32_t nd = s_off[1023];
   Scal* sc = a.scal;
   const uint64_t tail = sc->tail0 + sc->pops;
-  for (uint32_t c = 0; c < a.nblk; ++c) {
-    const uint32_t i = c * 1024 + tid;
-    const uint32_t f = a.dflag[i];
-    const bool d = f & 1u;
-    const uint32_t slot = a.dslot[i];
-    const uint32_t P = (c ? s_off[c - 1] : 0u) + (f >> 1);  // no barrier: blocks independent
-    const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
-    a.ring[(tail + pos) % a.ring_size] = d ? slot : kNone;
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += 8) {  // no barrier: blocks are independent
+    uint32_t f[8], slot[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t i = (c0 + u) * 1024 + tid;
+      f[u] = c0 + u < a.nblk ? a.dflag[i] : 0u;
+      slot[u] = c0 + u < a.nblk ? a.dslot[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t c = c0 + u, i = c * 1024 + tid;
+      if (c < a.nblk) {
+        const bool d = f[u] & 1u;
+        const uint32_t P = (c ? s_off[c - 1] : 0u) + (f[u] >> 1);
+        const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
+        a.ring[(tail + pos) % a.ring_size] = d ? slot[u] : kNone;
+      }
+    }
   }
   if (tid == 0) {
     sc->nd = nd;
