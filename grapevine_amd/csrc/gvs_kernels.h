@@ -873,8 +873,19 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   for (uint32_t c0 = 0; c0 < a.nblk; c0 += kWinGroup) {
     const uint32_t c1 = min(c0 + kWinGroup, a.nblk);
     const uint32_t need = (uint32_t)min((uint64_t)s_off[1][c1 - 1], m);
-    for (; loaded < need; loaded += 1024)  // uniform across the block
-      s_win[(loaded + tid) & (kWinRing - 1u)] = a.ring[(head0 + loaded + tid) % a.ring_size];
+    // refill: up to kWinGroup + 1 chunks, all loads issued before the stores
+    uint32_t w[kWinGroup + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= kWinGroup; ++k) {
+      const uint32_t pos = loaded + k * 1024;
+      w[k] = pos < need ? a.ring[(head0 + pos + tid) % a.ring_size] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k <= kWinGroup; ++k) {
+      const uint32_t pos = loaded + k * 1024;
+      if (pos < need) s_win[(pos + tid) & (kWinRing - 1u)] = w[k];
+    }
+    while (loaded < need) loaded += 1024;  // uniform across the block
     __syncthreads();
     uint32_t f[kWinGroup];
 #pragma unroll
@@ -890,9 +901,16 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
     }
     __syncthreads();  // the next refill overwrites the ring
   }
-  for (; loaded < a.B; loaded += 1024) {  // read the rest of the window: fixed B entries per batch
-    const uint32_t v = a.ring[(head0 + loaded + tid) % a.ring_size];
-    asm volatile("" ::"v"(v));
+  // read the rest of the window (fixed B entries per batch), 8 chunks in flight
+  for (; loaded < a.B; loaded += 8 * 1024) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t pos = loaded + k * 1024;
+      v[k] = pos < a.B ? a.ring[(head0 + pos + tid) % a.ring_size] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) asm volatile("" ::"v"(v[k]));
   }
   if (tid == 0) {
     sc->pops = pops;
