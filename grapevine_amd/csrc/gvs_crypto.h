@@ -9,10 +9,18 @@
 //   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
 //                       (standard CTR, counter in the last two bytes)
 //   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
-//   leaf_i = BLAKE2b-128(ct[256i, 256i+256), person = "gvs-leaf" | le64(i))
-//   tag = BLAKE2b-128(key = mac_key, le64(row) | le32(e) | le32(table)
-//                     | side_ct (or 16 zero bytes) | leaf_0 .. leaf_3)
-// The tag binds row, table and epoch, so a replayed or moved row fails.
+//   L_i  = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table),
+//                      ct[256i, 256i+256))                       i = 0..3
+//   H    = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+//                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
+//   tag  = H ^ L_0 ^ L_1 ^ L_2 ^ L_3
+// An XOR-MAC with a counter term (Bellare-Guerin-Rogaway's XMACC): H is the
+// PRF of a value that is never sealed twice, (row, e, table), and the L_i are
+// PRFs of index-separated blocks.  The tag binds row, table and epoch, so a
+// replayed, moved or spliced row fails.  The key block of each keyed hash
+// depends only on (key, person): its state is computed once (SealCtx), so a
+// leaf costs two compressions and the header one; the header depends on no
+// row data, so the message pass computes it for 64 rows at a time.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -189,7 +197,7 @@ __host__ __device__ __attribute__((always_inline)) inline void b2_compress(B2Sta
     v[i + 8] = iv[i];
   }
   v[12] ^= t;
-  if (last) v[14] = ~v[14];
+  v[14] ^= last ? ~0ull : 0ull;  // a select: `last` may differ across lanes
   b2_round<0>(v, m);
   b2_round<1>(v, m);
   b2_round<2>(v, m);
@@ -218,32 +226,56 @@ __host__ __device__ inline B2State b2_init(uint32_t nn, uint32_t kk, uint64_t p0
   return s;
 }
 
-// leaf i of a row: BLAKE2b-128 of its 256 ciphertext bytes, person "gvs-leaf" | le64(i)
 constexpr uint64_t kLeafPerson0 = 0x6661656c2d737667ULL;  // "gvs-leaf" little-endian
-__host__ __device__ __attribute__((always_inline)) inline void leaf_digest(const uint64_t m[32], uint32_t i, uint64_t out[2]) {
-  B2State s = b2_init(16, 0, kLeafPerson0, (uint64_t)i);
+constexpr uint64_t kHeadPerson0 = 0x646165682d737667ULL;  // "gvs-head" little-endian
+
+// state of keyed BLAKE2b-128 (32-byte key) with personalisation (p0, p1)
+// after its key block
+__host__ __device__ inline B2State b2_keyed_state(const uint8_t key[32], uint64_t p0, uint64_t p1) {
+  B2State s = b2_init(16, 32, p0, p1);
+  uint64_t m[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint64_t w = 0;
+    if (k < 4)
+      for (int b = 7; b >= 0; --b) w = (w << 8) | key[8 * k + b];
+    m[k] = w;
+  }
   b2_compress(s, m, 128, false);
-  b2_compress(s, m + 16, 256, true);
+  return s;
+}
+
+// L_i over one 256-byte leaf (m = its 32 little-endian words), from the
+// keyed state of leaf i
+__host__ __device__ __attribute__((always_inline)) inline void leaf_prf(const B2State& k,
+                                                                       const uint64_t m[32],
+                                                                       uint64_t out[2]) {
+  B2State s = k;
+  b2_compress(s, m, 128 + 128, false);
+  b2_compress(s, m + 16, 128 + 256, true);
   out[0] = s.h[0];
   out[1] = s.h[1];
 }
 
-// tag from the state after the key block (keyed BLAKE2b-128, 32-byte key) and
-// the 96-byte header + leaves message
-__host__ __device__ __attribute__((always_inline)) inline void row_tag(const B2State& keyed, uint64_t row, uint32_t epoch,
-                                        uint32_t table, const uint64_t side[2],
-                                        const uint64_t leaves[8], uint64_t out[2]) {
-  uint64_t m[16];
+// the 32-byte header message block
+__host__ __device__ inline void header_block(uint64_t row, uint32_t epoch, uint32_t table,
+                                             const uint64_t side[2], uint64_t m[16]) {
   m[0] = row;
   m[1] = (uint64_t)epoch | ((uint64_t)table << 32);
   m[2] = side[0];
   m[3] = side[1];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) m[4 + k] = leaves[k];
-#pragma unroll
-  for (int k = 12; k < 16; ++k) m[k] = 0;
-  B2State s = keyed;
-  b2_compress(s, m, 128 + 96, true);
+  for (int k = 4; k < 16; ++k) m[k] = 0;
+}
+
+// H of one row
+__host__ __device__ __attribute__((always_inline)) inline void header_prf(
+    const B2State& k, uint64_t row, uint32_t epoch, uint32_t table, const uint64_t side[2],
+    uint64_t out[2]) {
+  uint64_t m[16];
+  header_block(row, epoch, table, side, m);
+  B2State s = k;
+  b2_compress(s, m, 128 + 32, true);
   out[0] = s.h[0];
   out[1] = s.h[1];
 }
@@ -251,9 +283,10 @@ __host__ __device__ __attribute__((always_inline)) inline void row_tag(const B2S
 // Everything a sealing kernel needs, passed by value.
 struct SealCtx {
   AesRk rk;
-  B2State keyed;    // BLAKE2b-128 state after the MAC key block
-  uint32_t epoch;   // rows are read at `epoch`, written at `epoch + 1`
-  uint32_t on;      // authenticated-storage mode enabled
+  B2State leafk[2][4];  // keyed states after the key block: [table][leaf]
+  B2State headk;        // keyed state of the header PRF
+  uint32_t epoch;       // rows are read at `epoch`, written at `epoch + 1`
+  uint32_t on;          // authenticated-storage mode enabled
 };
 
 }  // namespace gvs

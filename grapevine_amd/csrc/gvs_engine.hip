@@ -287,10 +287,10 @@ static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256]
   b2_keyed_short(secret, "gvs storage aes", 16, ak);
   b2_keyed_short(secret, "gvs storage mac", 32, mk);
   aes_expand(sb, ak, sc.rk);
-  sc.keyed = b2_init(16, 32, 0, 0);
-  uint64_t m[16];
-  b2_block(mk, 32, m);
-  b2_compress(sc.keyed, m, 128, false);
+  for (uint32_t t = 0; t < 2; ++t)
+    for (uint32_t i = 0; i < 4; ++i)
+      sc.leafk[t][i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i | ((uint64_t)t << 32));
+  sc.headk = b2_keyed_state(mk, kHeadPerson0, 0);
   sc.epoch = 0;
   sc.on = 1;
 }
@@ -1007,14 +1007,15 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
     sd[0] = ld64(side_ct);
     sd[1] = ld64(side_ct + 8);
   }
-  uint64_t leaves[8];
-  for (uint32_t i = 0; i < 4; ++i) {
-    uint64_t m[32];
-    for (int k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
-    leaf_digest(m, i, leaves + 2 * i);
-  }
   uint64_t t[2];
-  row_tag(sc.keyed, row, epoch, table, sd, leaves, t);
+  header_prf(sc.headk, row, epoch, table, sd, t);
+  for (uint32_t i = 0; i < 4; ++i) {
+    uint64_t m[32], l[2];
+    for (int k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
+    leaf_prf(sc.leafk[table][i], m, l);
+    t[0] ^= l[0];
+    t[1] ^= l[1];
+  }
   for (int b = 0; b < 16; ++b) tag[b] = (uint8_t)(t[b / 8] >> (8 * (b % 8)));
   return GVS_OK;
 }

@@ -1155,13 +1155,23 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
     }
     __syncthreads();
     const uint32_t rb = t * kTile + wave * 64;
+    // AUTH: the header PRF of the wave's 64 rows at both epochs, one row per
+    // lane (it depends on no row data); each chunk takes its rows' by shuffle
+    uint64_t hv[2] = {0, 0}, hs[2] = {0, 0};
+    if (AUTH) {
+      const uint64_t z[2] = {0, 0};
+      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch, 0u, z, hv);
+      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch + 1u, 0u, z, hs);
+    }
     for (uint32_t j = 0; j < 64; j += U) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
       const uint64_t r0 = rowbase + rb + j;  // physical row of v[0]
+      const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));  // lane holding the header
       if (AUTH) {
-        if (!wave_unseal<U>(a.sc, s_te, 0u, r0, v, a.mtag, false, st) && lane == 0)
+        const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
+        if (!wave_unseal<U>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
           atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
       }
       // rows of this chunk that have ops (wave-uniform); wave 0's first chunk
@@ -1187,7 +1197,10 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
 #pragma unroll
         for (int uu = 0; uu < U; ++uu) v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
       }
-      if (AUTH) wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st);
+      if (AUTH) {
+        const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
+        wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }

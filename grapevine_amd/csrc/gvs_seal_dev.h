@@ -181,12 +181,28 @@ __device__ inline void unstage_rows(uint4 (&v)[U], const uint4* st) {
   wave_lds_sync();
 }
 
+// c ? a : b for a whole BLAKE2b state (per-lane selects)
+__device__ inline B2State b2_sel(bool c, const B2State& a, const B2State& b) {
+  B2State r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.h[i] = c ? a.h[i] : b.h[i];
+  return r;
+}
+
 // Tag of row row0 + ur, ur = (lane >> 2) % U, over the ciphertext rows
-// already in the stage and (mailbox rows) side ciphertexts staged at
-// st[U*4*kSegU4 + u].
+// already in the stage: tag = H ^ L_0 ^ .. ^ L_3 (gvs_crypto.h).  Lane L
+// computes leaf L & 3 of row ur; the quad XORs its four leaves by shuffles.
+//  * U <= 8 (mailbox passes, side entries staged at st[U*4*kSegU4 + u]):
+//    lanes 32 + u compute H of row u in the same instructions (their first
+//    compression takes the header block instead of leaf data), so the header
+//    costs no extra time.  Valid in lanes < 4U.
+//  * U = 16 (message pass): every lane hashes a leaf; `hdr` is H of the
+//    lane's row, computed by the caller (for 64 rows at once).
 template <int U>
 __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0, uint32_t epoch,
-                                 bool with_side, const uint4* st, uint64_t out[2]) {
+                                 bool with_side, const uint4* st, const uint64_t* hdr,
+                                 uint64_t out[2]) {
+  constexpr bool kInlineHdr = U <= 8;
   const uint32_t lane = lane_id();
   const uint32_t ur = (lane >> 2) % (uint32_t)U, leaf = lane & 3;
   uint64_t m[32];
@@ -197,22 +213,46 @@ __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0
     m[2 * k] = u4lo(x);
     m[2 * k + 1] = u4hi(x);
   }
-  uint64_t d[2];
-  leaf_digest(m, leaf, d);
-  uint64_t lv[8];
+  uint64_t res[2];
+  if (kInlineHdr) {
+    const bool hl = lane >= 32;
+    const uint32_t hrow = (lane - 32) % (uint32_t)U;
+    uint64_t sd[2] = {0, 0};
+    if (with_side) {
+      const uint4 x = st[U * 4 * kSegU4 + hrow];
+      sd[0] = u4lo(x);
+      sd[1] = u4hi(x);
+    }
+    uint64_t hb[16];
+    header_block(row0 + hrow, epoch, table, sd, hb);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int src = (int)((lane & ~3u) | (uint32_t)k);
-    lv[2 * k] = shfl_u64(d[0], src);
-    lv[2 * k + 1] = shfl_u64(d[1], src);
+    for (int k = 0; k < 16; ++k) hb[k] = hl ? hb[k] : m[k];
+    B2State s = b2_sel(hl, c.headk, c.leafk[table & 1][0]);
+#pragma unroll
+    for (uint32_t i = 1; i < 4; ++i) s = b2_sel(!hl && leaf == i, c.leafk[table & 1][i], s);
+    b2_compress(s, hb, hl ? 128 + 32 : 128 + 128, hl);
+    const uint64_t h0 = s.h[0], h1 = s.h[1];
+    b2_compress(s, m + 16, 128 + 256, true);
+    res[0] = hl ? h0 : s.h[0];
+    res[1] = hl ? h1 : s.h[1];
+  } else {
+    B2State s = c.leafk[table & 1][0];
+#pragma unroll
+    for (uint32_t i = 1; i < 4; ++i) s = b2_sel(leaf == i, c.leafk[table & 1][i], s);
+    leaf_prf(s, m, res);
   }
-  uint64_t sd[2] = {0, 0};
-  if (with_side) {
-    const uint4 x = st[U * 4 * kSegU4 + ur];
-    sd[0] = u4lo(x);
-    sd[1] = u4hi(x);
+  // H of the lane's row: taken before the quad reduction below, which would
+  // fold four rows' headers together in the header lanes
+  uint64_t h[2];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) h[w] = kInlineHdr ? shfl_u64(res[w], (int)(32 + ur)) : hdr[w];
+  // XOR of the row's four leaves (lanes 4ur .. 4ur + 3), then H
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    res[w] ^= shfl_u64(res[w], (int)(lane ^ 1u));
+    res[w] ^= shfl_u64(res[w], (int)(lane ^ 2u));
+    out[w] = res[w] ^ h[w];
   }
-  row_tag(c.keyed, row0 + ur, epoch, table, sd, lv, out);
 }
 
 // XOR the CTR keystream of (table, row0 + u, epoch) block `lane` into the
@@ -244,13 +284,13 @@ __device__ inline void stage_ctr(const SealCtx& c, const uint32_t* s_te, uint32_
 template <int U>
 __device__ inline bool wave_unseal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                    uint64_t row0, uint4 (&v)[U], const uint4* tags, bool with_side,
-                                   uint4* st) {
+                                   uint4* st, const uint64_t* hdr = nullptr) {
   stage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, c.epoch, with_side, st, t);
-  const uint32_t ur = (lane_id() >> 2) % (uint32_t)U;
+  wave_tags<U>(c, table, row0, c.epoch, with_side, st, hdr, t);
+  const uint32_t lane = lane_id(), ur = (lane >> 2) % (uint32_t)U;
   const uint4 want = tags[row0 + ur];
-  const bool bad = u4lo(want) != t[0] || u4hi(want) != t[1];
+  const bool bad = lane < 4u * U && (u4lo(want) != t[0] || u4hi(want) != t[1]);
   stage_ctr<U>(c, s_te, table, row0, c.epoch, st);
   unstage_rows<U>(v, st);
   return __ballot(bad) == 0ull;
@@ -261,12 +301,12 @@ __device__ inline bool wave_unseal(const SealCtx& c, const uint32_t* s_te, uint3
 template <int U>
 __device__ inline void wave_seal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                  uint64_t row0, uint32_t ep, uint4 (&v)[U], uint4* tags,
-                                 bool with_side, uint4* st) {
+                                 bool with_side, uint4* st, const uint64_t* hdr = nullptr) {
   stage_rows<U>(v, st);
   stage_ctr<U>(c, s_te, table, row0, ep, st);
   unstage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, ep, with_side, st, t);
+  wave_tags<U>(c, table, row0, ep, with_side, st, hdr, t);
   wave_lds_sync();  // the stage is reused by the caller
   const uint32_t lane = lane_id();
   if ((lane & 3u) == 0 && (lane >> 2) < (uint32_t)U)
@@ -304,8 +344,16 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
         side[r0 + lane] = sct;
         st[U * 4 * kSegU4 + lane] = sct;
       }
+      wave_lds_sync();
     }
-    wave_seal<U>(c, s_te, table, r0, 0u, v, tags, side != nullptr, st);
+    uint64_t sd[2] = {0, 0}, hdr[2];
+    if (side) {
+      const uint4 x = st[U * 4 * kSegU4 + ((lane >> 2) % U)];
+      sd[0] = u4lo(x);
+      sd[1] = u4hi(x);
+    }
+    header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);  // one-time: no amortising
+    wave_seal<U>(c, s_te, table, r0, 0u, v, tags, side != nullptr, st, hdr);
 #pragma unroll
     for (int u = 0; u < U; ++u) rows[(r0 + u) * 64 + lane] = v[u];
   }

@@ -225,9 +225,12 @@ static void put_le(uint8_t *p, uint64_t v, int n) {
   for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
 }
 
-/* Seal one row: ct = pt ^ AES-CTR keystream, tag = keyed BLAKE2b-128 over
- * (row, epoch, table, side ct, 4 leaf digests).  side_pt may be NULL
- * (message rows); then side_ct is not written and 16 zero bytes are MACed. */
+/* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ L_0 ^ .. ^ L_3 with
+ *   L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table), leaf i)
+ *   H   = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+ *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
+ * side_pt may be NULL (message rows); then side_ct is not written and 16 zero
+ * bytes stand in for it. */
 void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
                   const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
                   uint8_t *side_ct, uint8_t tag[16]) {
@@ -248,16 +251,18 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
     uint8_t *dst = j < 64 ? ct + 16 * j : side_ct;
     for (int k = 0; k < 16; ++k) dst[k] = (uint8_t)(src[k] ^ ks[k]);
   }
-  uint8_t msg[96];
-  memset(msg, 0, sizeof msg);
-  put_le(msg, row, 8);
-  put_le(msg + 8, epoch, 4);
-  put_le(msg + 12, table, 4);
-  if (side_pt) memcpy(msg + 16, side_ct, 16);
+  uint8_t hdr[32], head_person[16] = {'g', 'v', 's', '-', 'h', 'e', 'a', 'd'};
+  memset(hdr, 0, sizeof hdr);
+  put_le(hdr, row, 8);
+  put_le(hdr + 8, epoch, 4);
+  put_le(hdr + 12, table, 4);
+  if (side_pt) memcpy(hdr + 16, side_ct, 16);
+  gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
   for (uint32_t i = 0; i < 4; ++i) {
-    uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'};
-    put_le(person + 8, i, 8);
-    gvo_blake2b(NULL, 0, person, ct + 256 * i, 256, msg + 32 + 16 * i, 16);
+    uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'}, l[16];
+    put_le(person + 8, i, 4);
+    put_le(person + 12, table, 4);
+    gvo_blake2b(mk, 32, person, ct + 256 * i, 256, l, 16);
+    for (int k = 0; k < 16; ++k) tag[k] ^= l[k];
   }
-  gvo_blake2b(mk, 32, NULL, msg, 96, tag, 16);
 }

@@ -7,7 +7,7 @@ Three independent implementations must agree:
   * the product library's host-side implementation (gvs_storage_seal_row,
     the same gvs_crypto.h code the gfx950 kernels run).
 Known-answer vectors: FIPS-197 Appendix C.1, SP 800-38A F.5.1, RFC 7693
-Appendix A."""
+Appendix A.  Tag: H ^ L_0 ^ .. ^ L_3 (XOR-MAC with a counter term, gvs_crypto.h)."""
 import ctypes
 import hashlib
 import shutil
@@ -49,12 +49,15 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
     for k, r in enumerate(rows):
         ct = bytes(np.frombuffer(pts[k], np.uint8) ^ ks[k, :1024])
         sct = bytes(np.frombuffer(side_pts[k], np.uint8) ^ ks[k, 1024:]) if side_pts is not None else None
-        msg = r.to_bytes(8, "little") + epoch.to_bytes(4, "little") + table.to_bytes(4, "little")
-        msg += sct if sct is not None else bytes(16)
+        hdr = r.to_bytes(8, "little") + epoch.to_bytes(4, "little") + table.to_bytes(4, "little")
+        hdr += sct if sct is not None else bytes(16)
+        tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
+                                             person=b"gvs-head" + bytes(8)).digest(), "little")
         for i in range(4):
-            person = b"gvs-leaf" + i.to_bytes(8, "little")
-            msg += hashlib.blake2b(ct[256 * i:256 * i + 256], digest_size=16, person=person).digest()
-        out.append((ct, sct, hashlib.blake2b(msg, key=mk, digest_size=16).digest()))
+            person = b"gvs-leaf" + i.to_bytes(4, "little") + table.to_bytes(4, "little")
+            tag ^= int.from_bytes(hashlib.blake2b(ct[256 * i:256 * i + 256], key=mk, digest_size=16,
+                                                  person=person).digest(), "little")
+        out.append((ct, sct, tag.to_bytes(16, "little")))
     return out
 
 
