@@ -78,7 +78,8 @@ class GvsConfig(ctypes.Structure):
         ("shard_count", ctypes.c_uint32),
         ("shard_index", ctypes.c_uint32),
         ("route_capacity", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 3),
+        ("expiry_per_batch", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 
@@ -98,12 +99,13 @@ RAW_MESSAGES, RAW_MAILBOXES, RAW_SIDE, RAW_MSG_TAGS, RAW_MBOX_TAGS = range(5)
 
 def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,
                 max_batch=None, device=0, secret_key=None, shard_count=0, shard_index=0,
-                route_capacity=0, rows_per_partition=0, auth_storage=False):
+                route_capacity=0, rows_per_partition=0, auth_storage=False, expiry_per_batch=0):
     """Config mirroring gvs_config_init's defaults (R = N/16 mailboxes per shard)."""
     cfg = GvsConfig()
     cfg.shard_count = shard_count
     cfg.shard_index = shard_index
     cfg.route_capacity = route_capacity
+    cfg.expiry_per_batch = expiry_per_batch
     cfg.rows_per_partition = rows_per_partition
     cfg.flags = FLAG_AUTH_STORAGE if auth_storage else 0
     cfg.msg_capacity = msg_capacity

@@ -88,6 +88,9 @@ struct Engine {
   uint4* mtag = nullptr;     // authenticated storage: N message-row tags
   uint4* btag = nullptr;     //                        R mailbox-row tags
   uint32_t epoch = 0;        // batches applied: rows are sealed at this epoch
+  // expiry sweep: X = cfg.expiry_per_batch ops at [B - X, B)
+  uint32_t X = 0, xk = 1, xep = 0;
+  uint4* xbuf = nullptr;     // X records of 128 B, written by the message pass
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -125,6 +128,7 @@ struct gvs_handle {
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
   int rpass_variant = 6;
+  uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   std::vector<void*> allocs;
   std::string err;
 };
@@ -188,8 +192,12 @@ static int validate(const gvs_config* c) {
     return GVS_ERR_INVALID_ARG;
   if (c->shard_count > kShardsMax) return GVS_ERR_INVALID_ARG;
   if (c->route_capacity > c->max_batch) return GVS_ERR_INVALID_ARG;
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < 2; ++i)
     if (c->reserved[i] != 0) return GVS_ERR_INVALID_ARG;
+  if (c->expiry_per_batch &&
+      (!is_pow2(c->expiry_per_batch) || c->expiry_per_batch > c->max_batch / 2 ||
+       c->shard_count > 1))
+    return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
 
@@ -323,6 +331,15 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   e.nblk = B / 1024;
   e.ring_size = e.N + B;
   if (e.W + 1 > (uint32_t)kBinsMax) return GVS_ERR_INVALID_ARG;
+  // expiry sweep: X records per batch; workgroups w = epoch (mod xk) record
+  // xep each (X >= W: every workgroup, X / W each; X < W: one each, a rotating
+  // 1/xk of the workgroups)
+  e.X = cfg->expiry_per_batch;
+  if (e.X) {
+    e.xep = e.X >= e.W ? e.X / e.W : 1u;
+    e.xk = e.X >= e.W ? 1u : e.W / e.X;
+    if (e.xep > kXepMax) return GVS_ERR_INVALID_ARG;
+  }
   e.kc.pk0 = ld64(cfg->secret_key);
   e.kc.pk1 = ld64(cfg->secret_key + 8);
   e.kc.hk0 = ld64(cfg->secret_key + 16);
@@ -362,6 +379,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   A(dslot, B);
   A(bsum2, e.nblk);
   if (h->mode != kSingle) A(recv, (uint64_t)h->S * h->C * kSlotU4);
+  if (e.X) A(xbuf, (uint64_t)e.X * 8);
   if (h->auth) {
     A(mtag, e.N);
     A(btag, e.R);
@@ -373,6 +391,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.table, 0, e.N * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
+  if (e.X) GVS_HIP(h, hipMemsetAsync(e.xbuf, 0, (uint64_t)e.X * 128, s));
   // free ring = slots 0..N-1 in order; scalars
   std::vector<uint32_t> ring(e.ring_size, kNone);
   for (uint64_t i = 0; i < e.N; ++i) ring[i] = (uint32_t)i;
@@ -572,10 +591,13 @@ static int phase_a(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride,
   const uint32_t B = e.B;
   GVS_HIP(h, hipMemsetAsync(e.qcount, 0, (e.Q + 1) * sizeof(uint32_t), s));
   GVS_HIP(h, hipMemsetAsync(e.pcount, 0, (e.W + 1) * sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types);
+  const uint32_t xbase = B - e.X;
+  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
+                     (const uint4*)e.xbuf, xbase);
   mark(h, "copy");
   {
-    MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, e.qcount, n, B, e.Q, e.logQ, e.N, e.kc};
+    MetaArgs a{e.img, e.types, e.ops,  e.kinds, e.s1keys, e.qcount, n,
+               B,     e.Q,     e.logQ, e.N,     e.kc,     xbase};
     hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
   }
@@ -610,6 +632,13 @@ static void launch_rpass(gvs_handle* h, const Engine& e, uint32_t n) {
   a.sc = seal_of(h, e);
   a.te = h->te;
   a.mtag = e.mtag;
+  a.xbase = e.B - e.X;
+  a.xon = e.X ? 1u : 0u;
+  a.xk = e.xk;
+  a.xrot = e.epoch % e.xk;
+  a.xep = e.xep;
+  a.cutoff = h->cutoff;
+  a.xbuf = e.xbuf;
   const dim3 g(e.W + kNullBlocks), b(256);
   if (h->auth) {
     hipLaunchKernelGGL((k_rpass<16, true, true, 1, true>), g, b, 0, s, a);
@@ -820,7 +849,7 @@ static int finish(gvs_handle* h) {
 }
 
 static uint32_t max_submit(const gvs_handle* h) {
-  return h->Bsub * (h->mode == kLocal ? h->S : 1u);
+  return h->Bsub * (h->mode == kLocal ? h->S : 1u) - h->eng[0].X;
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -893,6 +922,12 @@ int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void
   GVS_HIP(h, hipSetDevice(h->device));
   if (int r = run_batch(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
   return finish(h);
+}
+
+int gvs_set_expiry_cutoff(gvs_handle* h, uint64_t cutoff) {
+  if (!h) return GVS_ERR_INVALID_ARG;
+  h->cutoff = cutoff;
+  return GVS_OK;
 }
 
 int gvs_access(gvs_handle* h, const gvs_request* req, gvs_response* out) {

@@ -233,20 +233,35 @@ __device__ inline void hist_flush(uint32_t* s_hist, uint32_t nbins, uint32_t* g_
 // One wave per request: 64 x 16 B of image + the type word.  Rows >= n are
 // padding (zero image, type 0).  `stride` is the input record pitch in 16-B
 // units: 65 for the caller's gvs_request array, 72 for routed slots.
+//
+// Rows >= xbase (expiry sweep on) are the expiry deletes the
+// previous message pass recorded: record k = i - xbase becomes a DELETE image
+// of msg id with auth = recipient = the stored recipient, internal type
+// kTypeExpire if the record is valid, else padding.
+constexpr uint32_t kTypeExpire = 0x45585031u;  // never a valid request_type
 __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint32_t stride,
                                               uint32_t n, uint32_t B, uint4* __restrict__ img,
-                                              uint32_t* __restrict__ types) {
+                                              uint32_t* __restrict__ types, const uint4* xbuf,
+                                              uint32_t xbase) {
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t lane = lane_id();
   if (i >= B) return;
   uint4 v = make_uint4(0, 0, 0, 0);
-  if (i < n) v = in[(uint64_t)i * stride + lane];
-  img[(uint64_t)i * 64 + lane] = v;
-  if (lane == 0) {
-    uint32_t t = 0;
-    if (i < n) t = in[(uint64_t)i * stride + 64].x;
-    types[i] = t;
+  uint32_t t = 0;
+  if (i >= xbase) {
+    // lanes 0..5 <- record words id, rcpt lo, rcpt hi, rcpt lo, rcpt hi, valid
+    const uint32_t src = lane == 0 ? 0u : (lane < 5 ? 2u - (lane & 1u) : 3u);
+    const uint4* rec = xbuf + (uint64_t)(i - xbase) * 8;
+    const uint4 x = rec[src];
+    t = __shfl(x.x, 5) ? kTypeExpire : 0u;
+    if (lane < 5) v = x;
+    if (lane == 5) v = make_uint4(1u, 0, 0, 0);  // nonzero server time (response unused)
+  } else {
+    if (i < n) v = in[(uint64_t)i * stride + lane];
+    if (i < n && lane == 0) t = in[(uint64_t)i * stride + 64].x;
   }
+  img[(uint64_t)i * 64 + lane] = v;
+  if (lane == 0) types[i] = t;
 }
 
 // ------------------------------------------------------------------ k_meta
@@ -261,6 +276,7 @@ struct MetaArgs {
   uint32_t n, B, Q, logQ;
   uint64_t N;
   KeyCtx kc;
+  uint32_t xbase;  // ops >= xbase: expiry deletes (type kTypeExpire) or padding
 };
 
 __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
@@ -270,7 +286,9 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4* row = a.img + (uint64_t)i * 64;
   uint4 c0 = row[0], c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4], c5 = row[5];
-  const uint32_t type = a.types[i];
+  const uint32_t raw = a.types[i];
+  const bool is_x = i >= a.xbase;
+  const uint32_t type = selu32(is_x & (raw == kTypeExpire), 4u, raw);  // DELETE
   OpState o = {};
   o.id[0] = c0.x; o.id[1] = c0.y; o.id[2] = c0.z; o.id[3] = c0.w;
   o.ts = u4lo(c5);
@@ -283,7 +301,7 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   // fetch shows up in FETCH_SIZE; DESIGN.md §3 rule 6).  Conditions combine
   // with bitwise operators (no short-circuit control flow) and every select
   // chooses between values already computed.
-  const bool pad = i >= a.n;
+  const bool pad = (is_x & (raw != kTypeExpire)) | (!is_x & (i >= a.n));
   const bool hard = (type < 1u) | (type > 4u) | auth_zero | ((type == 3u) & id_zero);
   const bool create = type == 1u;
   const bool next = ((type == 2u) | (type == 4u)) & id_zero;
@@ -1003,7 +1021,16 @@ struct RArgs {
   SealCtx sc;               // authenticated storage (AUTH instantiations)
   const uint32_t* te;       // AES table (256 words)
   uint4* mtag;              // N row tags
+  // expiry sweep: ops with seq >= xbase are expiry deletes
+  // (succeed only if the row's timestamp < cutoff); with xon, workgroups
+  // w = xrot (mod xk) record their partition's first xep expired rows after
+  // the batch's ops into xbuf[(w / xk) * xep ..], one 128-B record each
+  uint32_t xbase, xon, xk, xrot, xep;
+  uint64_t cutoff;
+  uint4* xbuf;
 };
+
+constexpr uint32_t kXepMax = 8;  // expiry records per workgroup (one store instruction)
 
 __device__ inline void write_response(const RArgs& a, uint32_t seq, uint4 rec, uint32_t status) {
   const uint32_t lane = lane_id();
@@ -1073,7 +1100,11 @@ __device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, 
     // (grapevine.proto:84,97,107) and then the recipient (:99-101,:110-112)
     const uint32_t st_next = (exists && rid_match) ? 1u : 8u;
     const uint32_t st_create = exists ? 8u : 1u;
-    const bool found = exists && id_match && auth_ok;
+    // expiry deletes (seq >= xbase) also need the row's timestamp (lane 5,
+    // low 8 B) below the cutoff: a row updated since its sweep is kept
+    const uint64_t row_ts = ((uint64_t)__shfl(cur.y, 5) << 32) | __shfl(cur.x, 5);
+    const bool fresh = seq >= a.xbase && !(row_ts < a.cutoff);
+    const bool found = exists && id_match && auth_ok && !fresh;
     const uint32_t st_byid = !found ? 2u : ((kind != KIND_READ && !rcpt_ok) ? 4u : 1u);
     const uint32_t status = is_next ? st_next : (is_create ? st_create : st_byid);
     const bool ok = status == 1u;
@@ -1089,6 +1120,53 @@ __device__ inline void r_apply(const RArgs& a, uint4& v, const uint32_t* stash, 
   }
 }
 
+// Expiry sweep, per chunk of U rows after their ops: rows that hold a message
+// (nonzero id, lane 0) with timestamp (lane 5) < cutoff are appended, in row
+// order, to the wave's LDS list (id, recipient lo, recipient hi); entries past
+// xep go to a spare slot.  Branch-free and on-die only.  Returns the count.
+template <int U>
+__device__ inline uint32_t x_detect(const RArgs& a, const uint4 (&v)[U], uint4* buf, uint32_t xc) {
+  const uint32_t lane = lane_id();
+  const uint32_t part = lane == 0 ? 0u : lane - 2u;  // lanes 0, 3, 4 -> list words 0, 1, 2
+  const bool writer = lane == 0 || lane == 3 || lane == 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t ts = ((uint64_t)v[u].y << 32) | v[u].x;
+    const uint64_t m_old = __ballot(lane == 5 && ts < a.cutoff);
+    const uint64_t m_msg = __ballot(lane == 0 && nz4(v[u]));
+    const uint32_t hit = (uint32_t)((m_old >> 5) & m_msg & 1ull);
+    const uint32_t slot = min(xc, a.xep);
+    if (writer) buf[slot * 3 + part] = v[u];
+    xc += hit;
+  }
+  return xc;
+}
+
+// After a tile: append the waves' lists (wave order = row order) to the
+// partition's list s_xp of up to xep entries; s_xt is its length.  Threads
+// < 3 xep each fill one word with selects; the caller syncs, then thread 0
+// stores the returned length.
+__device__ inline uint32_t x_merge(const RArgs& a, const uint4* s_xw, const uint32_t* s_xc,
+                                   uint4* s_xp, uint32_t tot) {
+  const uint32_t tid = threadIdx.x, cap = a.xep;
+  uint32_t add = 0;
+  if (tid < 3 * cap) {
+    const uint32_t k = tid / 3, c = tid % 3;
+    uint32_t off = k - tot, src = kNone;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t cw = min(s_xc[w], cap);
+      const bool take = k >= tot && src == kNone && off < cw;
+      src = selu32(take, ((uint32_t)w * (kXepMax + 1) + off) * 3 + c, src);
+      off -= cw;
+    }
+    if (src != kNone) s_xp[k * 3 + c] = s_xw[src];
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) add += min(s_xc[w], cap);
+  return min(tot + add, cap);
+}
+
 template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false>
 __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t stash[kStash];
@@ -1096,6 +1174,9 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
   __shared__ uint32_t s_tile[kRowsMax / kTile + 1];
   GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
   __shared__ uint4 s_st[AUTH ? 4 * stage_u4(U) : 1];
+  __shared__ uint4 s_xw[4 * (kXepMax + 1) * 3];  // expiry: per-wave lists of a tile
+  __shared__ uint4 s_xp[kXepMax * 3];            //         the partition's list
+  __shared__ uint32_t s_xc[4], s_xt;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
@@ -1147,7 +1228,9 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
     const uint32_t lo = s_tile[t], hi = s_tile[t + 1];
     s_cnt[tid] = 0;
     s_first[tid] = 0xFFFFFFFFu;
+    if (t == 0 && tid == 0) s_xt = 0;
     __syncthreads();
+    uint32_t xc = 0;  // expiry: this wave's hits in this tile
     for (uint32_t k = lo + tid; k < hi; k += 256) {
       const uint32_t o = (r_op_at(a, stash, start, k, rowbase) >> 20) - t * kTile;
       atomicAdd(&s_cnt[o], 1u);
@@ -1197,6 +1280,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
 #pragma unroll
         for (int uu = 0; uu < U; ++uu) v[uu] = sel4((bit >> uu) & 1u, cur, v[uu]);
       }
+      if (a.xon) xc = x_detect<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc);
       if (AUTH) {
         const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
         wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
@@ -1204,7 +1288,25 @@ __global__ __launch_bounds__(256, MINW) void k_rpass(RArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }
+    if (lane == 0) s_xc[wave] = xc;
     __syncthreads();
+    if (a.xon) {
+      const uint32_t tot = x_merge(a, s_xw, s_xc, s_xp, s_xt);
+      __syncthreads();
+      if (tid == 0) s_xt = tot;
+    }
+  }
+  if (a.xon && w % a.xk == a.xrot) {
+    // the partition's expiry records: 8 lanes per 128-B record (id, recipient,
+    // valid word, zeros), all written by one store instruction of wave 0
+    __syncthreads();
+    if (wave == 0 && lane < 8 * a.xep) {
+      const uint32_t k = lane >> 3, part8 = lane & 7;
+      const bool valid = k < s_xt;
+      uint4 val = make_uint4(part8 == 3 && valid ? 1u : 0u, 0, 0, 0);
+      if (part8 < 3) val = valid ? s_xp[k * 3 + part8] : make_uint4(0, 0, 0, 0);
+      a.xbuf[((uint64_t)(w / a.xk) * a.xep + k) * 8 + part8] = val;
+    }
   }
 }
 

@@ -22,7 +22,7 @@ EXPORTED = (
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
     "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_dump_raw",
-    "gvs_store_raw",
+    "gvs_store_raw", "gvs_set_expiry_cutoff",
 )
 
 
@@ -63,6 +63,7 @@ def load_library(path=None):
     lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
     lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
     lib.gvs_last_error.argtypes = [vp]
+    lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p
     lib.gvs_version.restype = ctypes.c_char_p
     for name in EXPORTED:
@@ -163,6 +164,10 @@ class ObliviousStore:
 
     def set_option(self, key, value):
         self._check(self.lib.gvs_set_option(self.h, key.encode(), int(value)))
+
+    def set_expiry_cutoff(self, cutoff):
+        """Messages with timestamp < cutoff expire (gvs_set_expiry_cutoff)."""
+        self._check(self.lib.gvs_set_expiry_cutoff(self.h, int(cutoff)))
 
     def set_timing(self, on=True):
         self._check(self.lib.gvs_set_timing(self.h, 1 if on else 0))

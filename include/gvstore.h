@@ -138,7 +138,11 @@ typedef struct gvs_config {
   uint32_t shard_index;         /* this process's shard (gvs_create_sharded) */
   uint32_t route_capacity;      /* C: request slots per (source, shard) pair and
                                    batch; 0 = automatic */
-  uint32_t reserved[3];         /* must be 0 */
+  uint32_t expiry_per_batch;    /* X: expiry-sweep deletes per batch;
+                                   0 = off, else a power of two <= max_batch / 2,
+                                   unsharded stores only.  Callers then submit at
+                                   most max_batch - X requests per batch. */
+  uint32_t reserved[2];         /* must be 0 */
 } gvs_config;
 
 typedef struct gvs_stats {       /* summed over the handle's shards */
@@ -196,6 +200,15 @@ int gvs_process_batch(gvs_handle *h, const gvs_request *reqs, uint32_t n,
  * benchmark so that the timed region excludes PCIe. */
 int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
                              void *d_out);
+
+/* Message expiry (README.md:86-99: the untrusted host supplies the time and
+ * the expiry period).  From the next batch on, messages whose timestamp is
+ * < cutoff expire: each batch's message pass records up to X of them (fixed
+ * per workgroup), and the following batch deletes them, if still
+ * older than its cutoff, through X trailing delete slots: the message row, its
+ * mailbox entry and its slot are freed as by a recipient's DELETE.  0 = none.
+ * Requires gvs_config.expiry_per_batch > 0 for any effect. */
+int gvs_set_expiry_cutoff(gvs_handle *h, uint64_t cutoff);
 
 /* Single-request shim in the shape of ObliviousHashMap::access_and_insert. */
 int gvs_access(gvs_handle *h, const gvs_request *req, gvs_response *out);

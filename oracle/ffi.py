@@ -51,6 +51,7 @@ def lib():
         L.gvo_process_batch.argtypes = [vp, vp, u32, vp]
         L.gvo_process_batch.restype = ctypes.c_int
         L.gvo_apply_one.argtypes = [vp, vp, vp]
+        L.gvo_set_expiry_cutoff.argtypes = [vp, u64]
         for f in ("gvo_messages", "gvo_mailboxes", "gvo_creation_counter", "gvo_state_digest"):
             getattr(L, f).argtypes = [vp]
             getattr(L, f).restype = u64
@@ -210,6 +211,9 @@ class Model:
         if rc != 0:
             raise ValueError(f"oracle rejected batch: {rc}")
         return out
+
+    def set_expiry_cutoff(self, cutoff):
+        self.L.gvo_set_expiry_cutoff(self.m, int(cutoff))
 
     def apply_one(self, req):
         r = np.ascontiguousarray(np.asarray(req, dtype=abi.REQUEST_DTYPE).reshape(1))

@@ -164,6 +164,10 @@ struct gvo_model {
   uint32_t *live;  /* live slots */
   int64_t *live_pos;
   uint64_t n_live;
+  /* expiry sweep */
+  uint32_t X, W, S, xk, xep;
+  uint64_t cutoff, batches;
+  struct expiry_rec { uint8_t valid, id[16], rcpt[32]; } *xp; /* X pending deletes */
 };
 
 static int is_zero(const uint8_t *p, size_t n) {
@@ -208,6 +212,28 @@ gvo_model *gvo_create(const gvs_config *cfg) {
   }
   m->head = 0;
   m->tail = m->N;
+  /* message-table partitions of the engine (gvs_engine.hip engine_init): the
+   * expiry sweep's selection rule is defined over them [D] */
+  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : m->N / 16384;
+  if (S < 256) S = 256;
+  if (S > 4096) S = 4096;
+  if (S > m->N) S = m->N;
+  m->S = (uint32_t)S;
+  m->W = (uint32_t)(m->N / S);
+  m->X = cfg->expiry_per_batch;
+  if (m->X) {
+    if (!is_pow2(m->X) || m->X > m->B / 2) {
+      gvo_destroy(m);
+      return NULL;
+    }
+    m->xep = m->X >= m->W ? m->X / m->W : 1;
+    m->xk = m->X >= m->W ? 1 : m->W / m->X;
+    m->xp = calloc(m->X, sizeof *m->xp);
+    if (!m->xp || m->xep > 8) { /* at most 8 records per partition and batch */
+      gvo_destroy(m);
+      return NULL;
+    }
+  }
   return m;
 }
 
@@ -219,6 +245,7 @@ void gvo_destroy(gvo_model *m) {
   free(m->pcount);
   free(m->live);
   free(m->live_pos);
+  free(m->xp);
   free(m);
 }
 
@@ -457,12 +484,58 @@ static int batch_class(const gvs_request *rq) {
   return 2;
 }
 
+void gvo_set_expiry_cutoff(gvo_model *m, uint64_t cutoff) { m->cutoff = cutoff; }
+
+/* Expiry delete k of a batch: the message recorded by the
+ * previous batch's sweep is deleted as by its recipient, if it still exists
+ * and its timestamp is still < cutoff (an UPDATE since then keeps it). */
+static void do_expire(gvo_model *m, const struct expiry_rec *x) {
+  if (!x->valid) return;
+  gvs_record *r = lookup(m, x->id, NULL);
+  if (!r || !(r->timestamp < m->cutoff)) return;
+  gvs_request rq;
+  gvs_response o;
+  memset(&rq, 0, sizeof rq);
+  memcpy(rq.msg_id, x->id, 16);
+  memcpy(rq.auth_identity, x->rcpt, 32);
+  memcpy(rq.recipient, x->rcpt, 32);
+  rq.request_type = GVS_REQUEST_DELETE;
+  do_delete(m, &rq, &o);
+}
+
+/* The sweep after a batch [D]: partitions w = batches (mod xk) each record
+ * their first xep messages with timestamp < cutoff, in slot order within the
+ * partition (slot s is in partition s mod W at offset s div W), at
+ * xp[(w / xk) * xep ..]; unused entries are invalid. */
+static void expiry_sweep(gvo_model *m) {
+  memset(m->xp, 0, m->X * sizeof *m->xp);
+  for (uint32_t w = m->batches % m->xk; w < m->W; w += m->xk) {
+    uint32_t c = 0;
+    struct expiry_rec *dst = m->xp + (uint64_t)(w / m->xk) * m->xep;
+    for (uint64_t o = 0; o < m->S && c < m->xep; ++o) {
+      const gvs_record *r = &m->table[o * m->W + w];
+      if (is_zero(r->msg_id, 16) || !(r->timestamp < m->cutoff)) continue;
+      dst[c].valid = 1;
+      memcpy(dst[c].id, r->msg_id, 16);
+      memcpy(dst[c].rcpt, r->recipient, 32);
+      c++;
+    }
+  }
+}
+
 int gvo_process_batch(gvo_model *m, const gvs_request *reqs, uint32_t n,
                       gvs_response *out) {
-  if (n > m->B) return GVS_ERR_INVALID_ARG;
+  if (n > m->B - m->X) return GVS_ERR_INVALID_ARG;
   for (int cls = 0; cls < 3; ++cls)
     for (uint32_t i = 0; i < n; ++i)
       if (batch_class(&reqs[i]) == cls) gvo_apply_one(m, &reqs[i], &out[i]);
+  if (m->X) {
+    /* the expiry deletes occupy the batch's last X slots: by-id class, after
+     * every request */
+    for (uint32_t k = 0; k < m->X; ++k) do_expire(m, &m->xp[k]);
+    expiry_sweep(m);
+  }
+  m->batches++;
   return GVS_OK;
 }
 

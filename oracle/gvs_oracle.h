@@ -60,6 +60,8 @@ void gvo_destroy(gvo_model *m);
 /* Apply a batch in the engine's linearisation order; responses in request order. */
 int gvo_process_batch(gvo_model *m, const gvs_request *reqs, uint32_t n,
                       gvs_response *out);
+/* Expiry sweep (gvs_set_expiry_cutoff). */
+void gvo_set_expiry_cutoff(gvo_model *m, uint64_t cutoff);
 /* The plain sequential handler on one request (no batch reordering). */
 void gvo_apply_one(gvo_model *m, const gvs_request *req, gvs_response *out);
 
