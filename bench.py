@@ -44,6 +44,9 @@ def parse():
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
+    p.add_argument("--expiry", type=int, default=0,
+                   help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
+                        "batch - X requests and every prefilled message is past the cutoff")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return p.parse_args()
 
@@ -80,14 +83,14 @@ def gen_batches(torch, dev, B, count, known, pool, g, ts0):
     return out
 
 
-def prefill(torch, store, dev, B, target, pool, g, ts0):
+def prefill(torch, store, dev, B, target, pool, g, ts0, per_batch=None):
     """Fill the store with `target` creates through the normal pipeline; returns
     (id, sender, recipient) of every created message (device tensor n x 80)."""
     known = []
     done = 0
     d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
     while done < target:
-        n = min(B, target - done)
+        n = min(per_batch or B, target - done)
         r = torch.empty((n, 1040), dtype=torch.uint8, device=dev)
         r[:, :1024] = torch.randint(0, 256, (n, 1024), dtype=torch.uint8, device=dev, generator=g)
         r[:, 1024:] = 0
@@ -183,27 +186,32 @@ def main():
         cid = gdist.broadcast_bytes(ri, comm_unique_id() if rank == 0 else None, device=dev)
         store = ObliviousStore(cfg, comm_id=cid)
     else:
-        cfg = abi.make_config(N, max_batch=B, device=local, auth_storage=a.auth)
+        cfg = abi.make_config(N, max_batch=B, device=local, auth_storage=a.auth,
+                              expiry_per_batch=a.expiry)
         store = ObliviousStore(cfg)
     shard_batch = store.stats()["shard_batch"]
     g = torch.Generator(device=dev)
     g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
     pool[:, 0] |= 1
-    known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000)
+    known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000,
+                    per_batch=B - a.expiry)
     batches = gen_batches(torch, dev, B, a.warmup + a.steps, known, pool, g, 1_800_000_000)
     d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
+    nreq = B - a.expiry  # requests per batch (the expiry deletes take the last X slots)
+    if a.expiry:
+        store.set_expiry_cutoff(1_750_000_000)  # every prefilled message has expired
     store.set_timing(True)
     torch.cuda.synchronize(dev)
     for i in range(a.warmup):
-        store.process_batch_device(batches[i].data_ptr(), B, d_out.data_ptr())
+        store.process_batch_device(batches[i].data_ptr(), nreq, d_out.data_ptr())
     torch.cuda.synchronize(dev)
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stage = {}
     for i in range(a.steps):
-        store.process_batch_device(batches[a.warmup + i].data_ptr(), B, d_out.data_ptr())
+        store.process_batch_device(batches[a.warmup + i].data_ptr(), nreq, d_out.data_ptr())
         for k, v in store.last_timings().items():
             stage[k] = stage.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
@@ -215,7 +223,7 @@ def main():
     statuses = torch.bincount(d_out[:, 1024].to(torch.int64), minlength=9)[:9].tolist()
 
     if rank == 0:
-        total = world * B * a.steps
+        total = world * nreq * a.steps
         rpass_ms = stage_ms.get("rpass", float("nan"))
         # algorithmic bytes of one message-table pass: every row
         # read + written, every op's request image read and response written
@@ -251,7 +259,8 @@ def main():
                        "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,
                        "parallelism": f"shards{world}",
                        "route_capacity": store.stats()["route_capacity"],
-                       "shard_batch": shard_batch, "auth_storage": bool(a.auth)},
+                       "shard_batch": shard_batch, "auth_storage": bool(a.auth),
+                       "expiry_per_batch": a.expiry},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rpass (message-table pass)",

@@ -837,7 +837,6 @@ __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
 // [head, head+B) is read in order, exactly once, and its first m entries are
 // handed to the successful creates in seq order (TOO_MANY_MESSAGES cutoff).
 __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
-  __shared__ uint32_t s_w[16];
   __shared__ uint32_t s_off[2][1024];
   __shared__ uint32_t s_win[kWinRing];
   const uint32_t tid = threadIdx.x;
@@ -1340,7 +1339,6 @@ __global__ __launch_bounds__(1024) void k_post_sum(PostArgs a) {
 
 // one workgroup: by-id deletes -> free ring in seq order; commit scalars
 __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
-  __shared__ uint32_t s_w[16];
   __shared__ uint32_t s_off[1024];
   const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
