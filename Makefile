@@ -1,22 +1,27 @@
-# Top-level build: the product library (gfx950 HIP) and the CPU oracle (tests only).
+# Top-level build: the product library (gfx950 HIP), the same engine with the
+# test hooks of include/gvstore_test.h, and the CPU oracle (tests only).
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 
 LIB := grapevine_amd/libgvstore.so
+TESTLIB := grapevine_amd/libgvstore_test.so
 SRCS := grapevine_amd/csrc/gvs_engine.hip
-HDRS := grapevine_amd/csrc/gvs_kernels.h grapevine_amd/csrc/gvs_device.h grapevine_amd/csrc/gvs_route.h grapevine_amd/csrc/gvs_crypto.h grapevine_amd/csrc/gvs_seal_dev.h include/gvstore.h
+HDRS := $(wildcard grapevine_amd/csrc/*.h) include/gvstore.h include/gvstore_test.h
 
-all: $(LIB) oracle
+all: $(LIB) $(TESTLIB) oracle
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
+
+$(TESTLIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DGVS_TEST_HOOKS -shared -o $@ $(SRCS) -lrccl
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(TESTLIB)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

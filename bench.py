@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--batch", type=int, default=65536)
     p.add_argument("--fill", type=float, default=0.75)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
-    p.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline instances (host threads)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline instances (host threads); 0 = this process's CPU share")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--routed", action="store_true",
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
@@ -108,16 +109,100 @@ def prefill(torch, store, dev, B, target, pool, g, ts0, per_batch=None):
     return torch.cat(known)
 
 
+def check_batch(torch, r, o):
+    """Properties every response of one batch must have, checked
+    on the device after the timed region: a successful CREATE echoes the
+    request with a fresh nonzero id; a successful by-id op returns the record of
+    the id it named, an UPDATE with the request's payload and time; every
+    successful response names the caller as sender or recipient (the recipient,
+    for next-message ops); a failure carries nothing but the request's time.
+    Returns (violations, creates ok, deletes ok)."""
+    typ = r[:, 1024:1028].contiguous().view(torch.int32).flatten()
+    st = o[:, 1024:1028].contiguous().view(torch.int32).flatten()
+    ok = st == 1
+    mid_zero = (r[:, 0:16] == 0).all(1)
+    auth, rrcpt = r[:, 16:48], r[:, 48:80]
+    osnd, orcpt = o[:, 16:48], o[:, 48:80]
+    eq = lambda a, b: (a == b).all(1)
+    bad = torch.zeros_like(ok)
+    cre = ok & (typ == 1)
+    bad |= cre & ~(eq(osnd, auth) & eq(orcpt, rrcpt) & eq(o[:, 80:1024], r[:, 80:1024]) &
+                   ~(o[:, 0:16] == 0).all(1))
+    byid = ok & (typ != 1) & ~mid_zero
+    bad |= byid & ~eq(o[:, 0:16], r[:, 0:16])
+    bad |= byid & ~(eq(osnd, auth) | eq(orcpt, auth))
+    upd = ok & (typ == 3)
+    bad |= upd & ~eq(o[:, 80:1024], r[:, 80:1024])
+    nxt = ok & ((typ == 2) | (typ == 4)) & mid_zero
+    bad |= nxt & ~eq(orcpt, auth)
+    fail = (st >= 2) & (st <= 7)
+    bad |= fail & ~((o[:, 0:80] == 0).all(1) & eq(o[:, 80:88], r[:, 80:88]) & (o[:, 88:1024] == 0).all(1))
+    bad |= (st < 0) | (st > 7)
+    dels = ok & (typ == 4)
+    return int(bad.sum()), int(cre.sum()), int(dels.sum())
+
+
+def host_cpu():
+    """CPU model, the machine's logical CPUs and this process's CPU share."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    # the GPU box runs one GPU's share of the host (OMP_NUM_THREADS = 16 there):
+    # os.cpu_count() reports the whole machine, so the share caps the workers
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or affinity
+    return {"model": model, "logical_cpus": os.cpu_count(), "affinity": affinity,
+            "share": min(share, affinity)}
+
+
+def c1_single_thread():
+    """BASELINE config 1 as specified: the CPU reference path restated
+    (oracle/gvs_pathoram.c), 2^16 message capacity, a seeded 10K
+    create/read/delete mix (40/40/20, half of the reads and deletes by id, half
+    next-message), on one thread.  Returns requests/s."""
+    from grapevine_amd import abi
+    from oracle import ffi
+    cfg = abi.make_config(1 << 16)
+    seq, oram = ffi.Model(cfg), ffi.PathOramModel(cfg)
+    seq.seed(0x6772617065 + 1)
+    mix = ffi.gen_params(create=40, read=40, update=0, delete=20, nxt=50, n_identities=1 << 12)
+    left, ops, t = 10000, 0, 0.0
+    while left:
+        r = seq.gen_batch(min(left, cfg.max_batch), mix)
+        t0 = time.perf_counter()
+        oram.process_batch(r)
+        t += time.perf_counter() - t0
+        seq.process_batch(r)
+        ops += len(r)
+        left -= len(r)
+    oram.close()
+    seq.close()
+    return ops / t
+
+
 def cpu_baseline(budget_s, threads):
     """The reference's CPU path, restated: the grapevine handler over Path ORAM
     (oracle/gvs_pathoram.c, Z = 4, recursive position map, 4 ORAM accesses per
     request), cross-checked bit-for-bit against the sequential model in
-    tests/test_pathoram.py.  One independent instance per host thread (the
-    reference's maps are single-owner, &mut self); each is prefilled through
-    its own accesses and then times the C3 mix for ~budget_s."""
+    tests/test_pathoram.py.  One independent instance per host thread of this
+    process's CPU share (the reference's maps are single-owner, &mut self);
+    each is prefilled through its own accesses and then times the C3 mix for
+    ~budget_s.  Also times BASELINE config 1 itself on one thread."""
     import threading
     from grapevine_amd import abi
     from oracle import ffi
+    cpu = host_cpu()
+    threads = threads or cpu["share"]
+    c1 = c1_single_thread()
     log2n = 20
     cfg = abi.make_config(1 << log2n, max_batch=65536)
     mix = ffi.gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=0, bad_auth=0,
@@ -152,10 +237,16 @@ def cpu_baseline(budget_s, threads):
     ops = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": ops / wall, "unit": "req/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
+            "cpu_share": cpu["share"],
+            "c1_single_thread_req_s": c1,
             "sample": f"Path ORAM restatement of the reference CPU path (oracle/gvs_pathoram.c), "
                       f"2^{log2n} capacity (tree height reduced from C3's 2^24 to bound memory), "
-                      f"{threads} independent instances on {threads} host threads, C3 mix, "
-                      f"{ops} requests in {wall:.1f}s; per-instance rate {ops / wall / threads:.0f} req/s"}
+                      f"{threads} independent instances on {threads} host threads "
+                      f"(this process's CPU share of {cpu['logical_cpus']} logical CPUs), C3 mix, "
+                      f"{ops} requests in {wall:.1f}s; per-instance rate {ops / wall / threads:.0f} req/s; "
+                      f"BASELINE config 1 (2^16, seeded 10K 40/40/20 create/read/delete) on one "
+                      f"thread: {c1:.0f} req/s"}
 
 
 def main():
@@ -198,6 +289,7 @@ def main():
                     per_batch=B - a.expiry)
     batches = gen_batches(torch, dev, B, a.warmup + a.steps, known, pool, g, 1_800_000_000)
     d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
+    d_outs = [torch.empty((B, 1040), dtype=torch.uint8, device=dev) for _ in range(a.steps)]
     nreq = B - a.expiry  # requests per batch (the expiry deletes take the last X slots)
     if a.expiry:
         store.set_expiry_cutoff(1_750_000_000)  # every prefilled message has expired
@@ -206,12 +298,13 @@ def main():
     for i in range(a.warmup):
         store.process_batch_device(batches[i].data_ptr(), nreq, d_out.data_ptr())
     torch.cuda.synchronize(dev)
+    msgs_before = store.stats()["messages"]
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     stage = {}
     for i in range(a.steps):
-        store.process_batch_device(batches[a.warmup + i].data_ptr(), nreq, d_out.data_ptr())
+        store.process_batch_device(batches[a.warmup + i].data_ptr(), nreq, d_outs[i].data_ptr())
         for k, v in store.last_timings().items():
             stage[k] = stage.get(k, 0.0) + v
     torch.cuda.synchronize(dev)
@@ -220,7 +313,18 @@ def main():
     elapsed = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
     stage_ms = {k: v / a.steps for k, v in stage.items()}
     st = store.stats()
+    d_out = d_outs[-1]
     statuses = torch.bincount(d_out[:, 1024].to(torch.int64), minlength=9)[:9].tolist()
+    # response properties of every timed batch, and message conservation
+    viol, n_cre, n_del = 0, 0, 0
+    for i in range(a.steps):
+        v, c, d = check_batch(torch, batches[a.warmup + i][:nreq], d_outs[i][:nreq])
+        viol, n_cre, n_del = viol + v, n_cre + c, n_del + d
+    expired = msgs_before + n_cre - n_del - st["messages"]
+    checks = {"batches": a.steps, "violations": viol, "creates_ok": n_cre, "deletes_ok": n_del,
+              "messages_before": msgs_before, "messages_after": st["messages"],
+              "conserved": expired == 0 if not a.expiry else expired >= 0,
+              "expired": expired}
 
     if rank == 0:
         total = world * nreq * a.steps
@@ -266,6 +370,7 @@ def main():
                          "kernel": "k_rpass (message-table pass)",
                          "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms},
             "cpu_baseline": cpu,
+            "checks": checks,
             "stage_ms": stage_ms,
             "store": {"messages": st["messages"], "mailboxes": st["mailboxes"],
                       "last_batch_status_hist": statuses},

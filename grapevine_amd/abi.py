@@ -38,6 +38,8 @@ GVS_ERR_OUT_OF_MEMORY = -3
 GVS_ERR_BATCH_OVERFLOW = -4
 GVS_ERR_NO_DEVICE = -5
 GVS_ERR_INTERNAL = -6
+GVS_ERR_INTEGRITY = -7
+GVS_ERR_EPOCH_EXHAUSTED = -8
 
 RECORD_DTYPE = np.dtype([
     ("msg_id", "u1", 16),

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/gvstore.h"
+#include "../../include/gvstore_test.h"
 #include "gvs_kernels.h"
 #include "gvs_route.h"
 
@@ -37,6 +38,11 @@ constexpr int kNullBlocks = 32;   // R-pass blocks for ops that touch no row
 constexpr int kDummyBlocks = 32;  // M-pass blocks for ops that touch no mailbox
 constexpr int kMaxMarks = 24;
 constexpr uint64_t kExtra = 64;   // per-op records after the B real ones (record B = dry dummy)
+// Authenticated storage binds every sealed row to a 32-bit epoch (one per
+// batch).  A store refuses work well before the epoch could wrap, since a
+// wrapped epoch would reuse CTR keystream and accept replayed rows
+// (gvs_crypto.h); the caller then rebuilds the store under a fresh key.
+constexpr uint32_t kEpochLimit = 0xFFFFFF00u;
 
 enum Mode { kSingle, kLocal, kRccl };
 
@@ -446,6 +452,13 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
     delete h;
     return GVS_ERR_INVALID_ARG;
   }
+  // the expiry sweep's deletes occupy the last X slots of a shard pipeline's
+  // batch; routed pipelines fill those slots with the routed requests
+  // (gvs_create_sharded accepts shard_count 1), so expiry is single-mode only
+  if (mode != kSingle && cfg->expiry_per_batch) {
+    delete h;
+    return GVS_ERR_INVALID_ARG;
+  }
   if (mode == kSingle) {
     h->C = 0;
     h->Be = h->Bsub;
@@ -848,6 +861,14 @@ static int finish(gvs_handle* h) {
   return GVS_OK;
 }
 
+static int check_epoch(gvs_handle* h) {
+  if (h->auth && h->eng[0].epoch >= kEpochLimit) {
+    h->err = "storage epoch exhausted: rebuild the store under a fresh secret_key";
+    return GVS_ERR_EPOCH_EXHAUSTED;
+  }
+  return GVS_OK;
+}
+
 static uint32_t max_submit(const gvs_handle* h) {
   return h->Bsub * (h->mode == kLocal ? h->S : 1u) - h->eng[0].X;
 }
@@ -905,6 +926,7 @@ int gvs_create_sharded(const gvs_config* cfg, const uint8_t comm_id[GVS_COMM_ID_
 int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_response* out) {
   if (!h || (!reqs && n) || (!out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   if (n)
     GVS_HIP(h, hipMemcpyAsync(h->in_stage, reqs, (size_t)n * sizeof(gvs_request),
@@ -919,6 +941,7 @@ int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_re
 int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void* d_out) {
   if (!h || (!d_reqs && n) || (!d_out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   if (int r = run_batch(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
   return finish(h);
@@ -954,34 +977,6 @@ int gvs_get_stats(gvs_handle* h, gvs_stats* out) {
   out->route_capacity = h->C;
   out->shard_batch = h->Be;
   out->epoch = h->eng[0].epoch;
-  return GVS_OK;
-}
-
-int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
-  if (!h || !host_dst) return GVS_ERR_INVALID_ARG;
-  const uint64_t N = h->eng[0].N;
-  if (bytes < N * 1024 * h->eng.size()) return GVS_ERR_INVALID_ARG;
-  std::vector<uint8_t> phys(N * 1024);
-  uint8_t* dst = (uint8_t*)host_dst;
-  std::vector<uint32_t> te0(256);
-  SealCtx sc{};
-  if (h->auth) storage_ctx(h->cfg.secret_key, sc, te0.data());
-  for (const auto& e : h->eng) {
-    GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
-    GVS_HIP(h, hipStreamSynchronize(h->stream));
-    for (uint64_t sl = 0; sl < N; ++sl) {
-      uint64_t row = (sl % e.W) * e.S + sl / e.W;
-      uint8_t* d = dst + sl * 1024;
-      std::memcpy(d, phys.data() + row * 1024, 1024);
-      if (h->auth)  // unseal (decrypt) at the current epoch
-        for (uint32_t j = 0; j < 64; ++j) {
-          const uint4 k = ctr_keystream(sc.rk, te0.data(), 0u, row, e.epoch, j);
-          const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-          for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
-        }
-    }
-    dst += N * 1024;
-  }
   return GVS_OK;
 }
 
@@ -1055,6 +1050,35 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
   return GVS_OK;
 }
 
+#ifdef GVS_TEST_HOOKS
+int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
+  if (!h || !host_dst) return GVS_ERR_INVALID_ARG;
+  const uint64_t N = h->eng[0].N;
+  if (bytes < N * 1024 * h->eng.size()) return GVS_ERR_INVALID_ARG;
+  std::vector<uint8_t> phys(N * 1024);
+  uint8_t* dst = (uint8_t*)host_dst;
+  std::vector<uint32_t> te0(256);
+  SealCtx sc{};
+  if (h->auth) storage_ctx(h->cfg.secret_key, sc, te0.data());
+  for (const auto& e : h->eng) {
+    GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
+    GVS_HIP(h, hipStreamSynchronize(h->stream));
+    for (uint64_t sl = 0; sl < N; ++sl) {
+      uint64_t row = (sl % e.W) * e.S + sl / e.W;
+      uint8_t* d = dst + sl * 1024;
+      std::memcpy(d, phys.data() + row * 1024, 1024);
+      if (h->auth)  // unseal (decrypt) at the current epoch
+        for (uint32_t j = 0; j < 64; ++j) {
+          const uint4 k = ctr_keystream(sc.rk, te0.data(), 0u, row, e.epoch, j);
+          const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+          for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
+        }
+    }
+    dst += N * 1024;
+  }
+  return GVS_OK;
+}
+
 static int raw_region(gvs_handle* h, uint32_t shard, uint32_t region, void** base,
                       uint64_t* size) {
   if (shard >= h->eng.size()) return GVS_ERR_INVALID_ARG;
@@ -1093,5 +1117,7 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   return GVS_OK;
 }
+
+#endif  // GVS_TEST_HOOKS
 
 }  // extern "C"

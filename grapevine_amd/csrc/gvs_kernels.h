@@ -167,12 +167,12 @@ __global__ __launch_bounds__(256) void k_bitonic_global(K* data, uint32_t n, uin
   uint32_t i = ((p / j) * 2u * j) + (p % j);
   uint32_t pj = i + j;
   bool asc = ((i & k) == 0u);
-  K a = data[i], b = data[pj];
-  bool sw = asc ? key_lt(b, a) : key_lt(a, b);
-  if (sw) {
-    data[i] = b;
-    data[pj] = a;
-  }
+  const K a = data[i], b = data[pj];
+  const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+  // both keys are stored whatever the comparison says: a store only on a
+  // swap would make the written bytes depend on the key order
+  data[i] = key_sel(sw, b, a);
+  data[pj] = key_sel(sw, a, b);
 }
 
 // ------------------------------------------------------------ block helpers

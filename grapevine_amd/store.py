@@ -15,15 +15,24 @@ import numpy as np
 from . import abi
 
 _LIB = None
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgvstore.so")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+# The production library exports include/gvstore.h only; the test build adds
+# the hooks of include/gvstore_test.h (dumps, raw stores).  Tests select it
+# with GVS_TEST_HOOKS=1 (tests/conftest.py).
+_LIB_PATH = os.path.join(_HERE, "libgvstore.so")
+_TEST_LIB_PATH = os.path.join(_HERE, "libgvstore_test.so")
 
 EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
-    "gvs_process_batch_device", "gvs_access", "gvs_get_stats", "gvs_dump_messages",
+    "gvs_process_batch_device", "gvs_access", "gvs_get_stats",
     "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
-    "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_dump_raw",
-    "gvs_store_raw", "gvs_set_expiry_cutoff",
+    "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
 )
+TEST_EXPORTED = ("gvs_dump_messages", "gvs_dump_raw", "gvs_store_raw")
+
+
+def test_hooks_enabled():
+    return os.environ.get("GVS_TEST_HOOKS") == "1"
 
 
 class GvsError(RuntimeError):
@@ -37,10 +46,11 @@ def load_library(path=None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or _LIB_PATH
+    p = path or (_TEST_LIB_PATH if test_hooks_enabled() else _LIB_PATH)
     if not os.path.exists(p):
-        raise RuntimeError(f"libgvstore.so not built at {p}; run `make` (HIP extension missing)")
+        raise RuntimeError(f"{os.path.basename(p)} not built at {p}; run `make` (HIP extension missing)")
     lib = ctypes.CDLL(p)
+    hooks = hasattr(lib, "gvs_dump_raw")
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.gvs_config_init.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.c_uint64]
     lib.gvs_create.argtypes = [ctypes.POINTER(abi.GvsConfig), ctypes.POINTER(vp)]
@@ -52,7 +62,6 @@ def load_library(path=None):
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
     lib.gvs_access.argtypes = [vp, vp, vp]
     lib.gvs_get_stats.argtypes = [vp, ctypes.POINTER(abi.GvsStats)]
-    lib.gvs_dump_messages.argtypes = [vp, vp, ctypes.c_uint64]
     lib.gvs_synchronize.argtypes = [vp]
     lib.gvs_set_timing.argtypes = [vp, i32]
     lib.gvs_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
@@ -60,13 +69,15 @@ def load_library(path=None):
                                      ctypes.POINTER(ctypes.c_float), i32]
     cp, u64 = ctypes.c_char_p, ctypes.c_uint64
     lib.gvs_storage_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
-    lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
-    lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
+    if hooks:
+        lib.gvs_dump_messages.argtypes = [vp, vp, ctypes.c_uint64]
+        lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
+        lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p
     lib.gvs_version.restype = ctypes.c_char_p
-    for name in EXPORTED:
+    for name in EXPORTED + (TEST_EXPORTED if hooks else ()):
         if name not in ("gvs_last_error", "gvs_version"):
             getattr(lib, name).restype = i32
     if path is None:

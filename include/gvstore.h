@@ -79,6 +79,10 @@ extern "C" {
 #define GVS_ERR_INTERNAL (-6)
 #define GVS_ERR_INTEGRITY (-7) /* authenticated storage: a stored row failed
                                   its tag; the handle refuses further work */
+#define GVS_ERR_EPOCH_EXHAUSTED (-8) /* authenticated storage: 2^32 - 256 batches
+                                        applied; rows are bound to a 32-bit epoch,
+                                        so the store must be rebuilt under a fresh
+                                        secret_key before it could wrap */
 
 /* gvs_config.flags */
 #define GVS_FLAG_AUTH_STORAGE 1u /* AES-CTR + BLAKE2b sealed tables */
@@ -215,10 +219,6 @@ int gvs_access(gvs_handle *h, const gvs_request *req, gvs_response *out);
 
 int gvs_get_stats(gvs_handle *h, gvs_stats *out);
 
-/* Copy the slot-addressed message table (N * 1024 bytes per shard, shards in
- * order) to host memory; test use. */
-int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
-
 /* Authenticated-storage format, host-side and device-free:
  * seal one 1024-B row (and for table 1, the mailbox table, its 16-B side
  * entry; side_pt = NULL for table 0) at `epoch` under the storage keys
@@ -227,14 +227,6 @@ int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
 int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
                          const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
                          uint8_t *side_ct, uint8_t tag[16]);
-
-/* Raw device regions of one shard, for tests of the storage format:
- * 0 message table (physical rows), 1 mailbox table, 2 mailbox side entries,
- * 3 message row tags, 4 mailbox row tags (3, 4: authenticated mode only). */
-int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset, void *dst,
-                 uint64_t bytes);
-int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset,
-                  const void *src, uint64_t bytes);
 
 /* Wait for all work on the handle's stream. */
 int gvs_synchronize(gvs_handle *h);

@@ -1,0 +1,32 @@
+/*
+ * gvstore_test.h — test hooks of libgvstore_test.so (the same engine built
+ * with -DGVS_TEST_HOOKS).  They read or overwrite a store's device state
+ * (decrypting it in authenticated mode), so the production library
+ * libgvstore.so does not export them: an enclave binds only include/gvstore.h.
+ */
+#ifndef GVSTORE_TEST_H
+#define GVSTORE_TEST_H
+
+#include "gvstore.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Copy the slot-addressed message table (N * 1024 bytes per shard, shards in
+ * order) to host memory; test use. */
+int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
+
+/* Raw device regions of one shard, for tests of the storage format:
+ * 0 message table (physical rows), 1 mailbox table, 2 mailbox side entries,
+ * 3 message row tags, 4 mailbox row tags (3, 4: authenticated mode only). */
+int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset, void *dst,
+                 uint64_t bytes);
+int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset,
+                  const void *src, uint64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GVSTORE_TEST_H */

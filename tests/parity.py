@@ -33,10 +33,12 @@ def diff_responses(got, want, reqs, limit=8):
     return out
 
 
-def diff_tables(got, want, limit=5):
+def diff_tables(got, want, limit=5, chunk=1 << 18):
     g = got.view(np.uint8).reshape(len(got), -1)
     w = want.view(np.uint8).reshape(len(want), -1)
-    bad = np.nonzero((g != w).any(axis=1))[0]
+    # chunked: a C3 table is 16 GiB, a whole-array comparison would add 16 GiB
+    bad = np.concatenate([np.nonzero((g[i:i + chunk] != w[i:i + chunk]).any(axis=1))[0] + i
+                          for i in range(0, len(g), chunk)] or [np.zeros(0, dtype=np.int64)])
     out = [f"slot {s}: got id {bytes(got[s]['msg_id']).hex()} want {bytes(want[s]['msg_id']).hex()}"
            for s in bad[:limit]]
     if len(bad) > limit:

@@ -6,29 +6,35 @@ import os
 import re
 
 from grapevine_amd import abi
-from grapevine_amd.store import EXPORTED, load_library
+from grapevine_amd.store import EXPORTED, TEST_EXPORTED, load_library
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    src = open(os.path.join(ROOT, "include", "gvstore.h")).read()
+def declared_functions(header="gvstore.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(gvs_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_every_declared_symbol_is_exported():
-    lib = load_library()
     decl = declared_functions()
     assert len(decl) >= 12
-    for name in decl:
-        assert hasattr(lib, name), name
     assert set(decl) == set(EXPORTED)
+    assert set(declared_functions("gvstore_test.h")) == set(TEST_EXPORTED)
+    prod = load_library(os.path.join(ROOT, "grapevine_amd", "libgvstore.so"))
+    test = load_library(os.path.join(ROOT, "grapevine_amd", "libgvstore_test.so"))
+    for name in decl:
+        assert hasattr(prod, name) and hasattr(test, name), name
+    for name in TEST_EXPORTED:  # the production library has no test hooks
+        assert hasattr(test, name), name
+        assert not hasattr(prod, name), name
 
 
 def test_library_contains_gfx950_code():
-    path = os.path.join(ROOT, "grapevine_amd", "libgvstore.so")
-    # the embedded HIP fat binary names its code object target
-    assert b"amdgcn-amd-amdhsa--gfx950" in open(path, "rb").read()
+    for lib in ("libgvstore.so", "libgvstore_test.so"):
+        path = os.path.join(ROOT, "grapevine_amd", lib)
+        # the embedded HIP fat binary names its code object target
+        assert b"amdgcn-amd-amdhsa--gfx950" in open(path, "rb").read()
 
 
 def test_pod_sizes_match_header():

@@ -1,0 +1,64 @@
+"""Timing side of the obliviousness contract (api/proto/grapevine.proto:120-122:
+READ, UPDATE and DELETE must be indistinguishable in access patterns *and
+timings*) at the headline shape, BASELINE config 3: a 2^24-message store and
+64K-request batches.
+
+Each mix runs tools/oblivious_probe.py under `rocprofv3 --kernel-trace`; every
+kernel's duration on the measured batches must match the reference mix within
+the run-to-run noise, taken from the prefill batches that every process runs
+identically.  The mixes include adversarial ones: every request aimed at one
+recipient (hot_next, hot_next_rud), every read missing (all_miss_read), only
+deletes.  A pass whose workgroups did work in proportion to the ops routed to
+them would show the hot mixes here."""
+import os
+import statistics
+
+import pytest
+
+from test_oblivious import gvs_rows, rocprof, short, split_batches, SHAPES
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MIXES = ["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]
+SHAPES["c3"] = dict(args=["--log2n", "24", "--batch", "65536", "--identities", "200000"],
+                    mixes=MIXES)
+N_MEAS = 3
+
+
+def test_kernel_durations_independent_of_mix(tmp_path):
+    per_mix = {}
+    for mix in MIXES:
+        d = rocprof(["--kernel-trace"], mix, str(tmp_path / f"kt_{mix}"), "c3")
+        rows = gvs_rows(os.path.join(d, "**", "*kernel_trace.csv"))
+        vals = [(short(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                for r in rows]
+        per_mix[mix] = split_batches(vals)
+    ref_b = per_mix["rud"]
+    kernels = [k for k, _ in ref_b[-1]]
+    n_pre = min(len(bs) for bs in per_mix.values()) - N_MEAS
+    lines, bad = [], []
+    for idx, k in enumerate(kernels):
+        # noise: spread of the identical prefill batches (batch 0: cold) across
+        # the processes, and of the reference mix's own measured batches
+        spread = 0.0
+        for i in range(1, n_pre):
+            v = [bs[i][idx][1] for bs in per_mix.values()]
+            spread = max(spread, max(v) - min(v))
+        own = [b[idx][1] for b in ref_b[-N_MEAS:]]
+        spread = max(spread, max(own) - min(own))
+        ref = statistics.median(own)
+        tol = 3.0 * spread + 2.0  # us; +2 us: launch-to-launch jitter floor of the trace clock
+        row = [f"{k[:30]:30s} ref={ref:10.1f}us spread={spread:7.1f} tol={tol:7.1f}"]
+        for mix, bs in per_mix.items():
+            assert [x[0] for x in bs[-1]] == kernels, f"{mix}: kernel sequence differs"
+            med = statistics.median(b[idx][1] for b in bs[-N_MEAS:])
+            row.append(f"{mix}:{med - ref:+.1f}")
+            if abs(med - ref) > tol:
+                bad.append((k, mix, round(med - ref, 1), round(tol, 1)))
+        lines.append(" ".join(row))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "timing_c3.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+        f.write(f"violations: {bad}\n")
+    assert not bad, f"kernel durations depend on the request mix: {bad}"
