@@ -24,6 +24,7 @@
 #include "../../include/gvstore_test.h"
 #include "gvs_kernels.h"
 #include "gvs_route.h"
+#include "gvs_txn.h"
 
 using namespace gvs;
 
@@ -97,6 +98,23 @@ struct Engine {
   // expiry sweep: X = cfg.expiry_per_batch ops at [B - X, B)
   uint32_t X = 0, xk = 1, xep = 0;
   uint4* xbuf = nullptr;     // X records of 128 B, written by the message pass
+  // fixed-slot message pass (gvs_txn.h, pipeline 2)
+  uint32_t c = 0;            // transaction slots per message partition
+  uint32_t par = 0;          // flips with every applied batch (ping-pong buffers)
+  uint32_t stamp_run = 0, stamp_prev = kNone, stamp_next = 1;
+  uint4* tbuf[2] = {};       // (W*c + B) x 128-B slot descriptors
+  uint4* xb2[2] = {};        // expiry records, written by one pass, read by the next batch
+  uint4* rpos = nullptr;     // B sorted-position records
+  uint4* rsb = nullptr;      // B x 128 B
+  uint4* snap = nullptr;     // W*c x 1 KiB
+  uint4* pbuf = nullptr;     // W*c x 1 KiB
+  uint4* snapdummy = nullptr, *pdummy = nullptr;  // B x 1 KiB
+  uint4* dryb = nullptr;     // W x 1 KiB
+  RtxV* rtx_agg = nullptr;
+  RtxV* rtx_carry = nullptr;
+  Rr1V* rr1_agg = nullptr;
+  Rr1V* rr1_carry = nullptr;
+  uint4* vagg = nullptr, *vagg2 = nullptr, *vcarry2 = nullptr, *vcarry = nullptr;
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -134,6 +152,7 @@ struct gvs_handle {
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
   int rpass_variant = 6;
+  int pipeline = 1;          // 1: per-op message pass; 2: fixed-slot transactions (gvs_txn.h)
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   std::vector<void*> allocs;
   std::string err;
@@ -217,6 +236,20 @@ static uint32_t auto_capacity(uint32_t B, uint32_t S) {
   uint64_t c = (uint64_t)std::ceil(mu + 8.0 * std::sqrt(mu) + 64.0);
   c = (c + 63) / 64 * 64;
   return (uint32_t)(c < B ? c : B);
+}
+
+// Transaction slots per message partition (gvs_txn.h): the distinct rows a
+// batch's B ops touch in one of W partitions are at most binomial(B, 1/W) for
+// uniformly spread slots; mean + 8 standard deviations + 16, rounded to 8,
+// overflows with probability far below 1e-12 per batch.  At most S (a
+// partition's rows) and B.
+static uint32_t txn_slots(uint32_t B, uint32_t W, uint32_t S) {
+  const double mu = (double)B / W;
+  uint64_t c = (uint64_t)std::ceil(mu + 8.0 * std::sqrt(mu) + 16.0);
+  c = (c + 7) / 8 * 8;
+  if (c > S) c = S;
+  if (c > B) c = B;
+  return (uint32_t)c;
 }
 
 // ------------------------------------------------- authenticated storage (host)
@@ -325,9 +358,10 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   e.B = B;
   e.logQ = log2u(e.Q);
   // rows per message-table partition (one workgroup each): the config value
-  // if set, else N/16384 clamped to [256, 4096] (C3: 1024 rows -> 16384
-  // workgroups, so the grid is many times the resident capacity)
-  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : e.N / 16384;
+  // if set, else N/4096 clamped to [256, 4096] (C3: 4096 rows -> 4096
+  // workgroups, 16 times the chip's resident capacity; few partitions keep
+  // the fixed transaction slots W*c small, gvs_txn.h)
+  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : e.N / 4096;
   if (S < (uint64_t)kTile) S = kTile;
   if (S > (uint64_t)kRowsMax) S = kRowsMax;
   if (S > e.N) S = e.N;
@@ -337,6 +371,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   e.nblk = B / 1024;
   e.ring_size = e.N + B;
   if (e.W + 1 > (uint32_t)kBinsMax) return GVS_ERR_INVALID_ARG;
+  e.c = txn_slots(B, e.W, e.S);
   // expiry sweep: X records per batch; workgroups w = epoch (mod xk) record
   // xep each (X >= W: every workgroup, X / W each; X < W: one each, a rotating
   // 1/xk of the workgroups)
@@ -390,6 +425,29 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(mtag, e.N);
     A(btag, e.R);
   }
+  {  // fixed-slot message pass
+    const uint64_t WC = (uint64_t)e.W * e.c;
+    for (int k = 0; k < 2; ++k) {
+      A(tbuf[k], (WC + B) * 8);
+      if (e.X) A(xb2[k], (uint64_t)e.X * 8);
+    }
+    A(rpos, B);
+    A(rsb, (uint64_t)B * 8);
+    A(snap, WC * 64);
+    A(pbuf, WC * 64);
+    A(snapdummy, (uint64_t)B * 64);
+    A(pdummy, (uint64_t)B * 64);
+    A(dryb, (uint64_t)e.W * 64);
+    A(rtx_agg, B / kScanT);
+    A(rtx_carry, B / kScanT);
+    A(rr1_agg, B / kScanT);
+    A(rr1_carry, B / kScanT);
+    const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
+    A(vagg, nvb * kVLineU4);
+    A(vcarry, nvb * kVLineU4);
+    A(vagg2, nvb2 * kVLineU4);
+    A(vcarry2, nvb2 * kVLineU4);
+  }
 #undef A
   hipStream_t s = h->stream;
   GVS_HIP(h, hipMemsetAsync(e.img + (uint64_t)B * 64, 0, E * 1024, s));
@@ -398,6 +456,10 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
   if (e.X) GVS_HIP(h, hipMemsetAsync(e.xbuf, 0, (uint64_t)e.X * 128, s));
+  for (int k = 0; k < 2; ++k) {
+    GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, ((uint64_t)e.W * e.c + B) * 128, s));
+    if (e.X) GVS_HIP(h, hipMemsetAsync(e.xb2[k], 0, (uint64_t)e.X * 128, s));
+  }
   // free ring = slots 0..N-1 in order; scalars
   std::vector<uint32_t> ring(e.ring_size, kNone);
   for (uint64_t i = 0; i < e.N; ++i) ring[i] = (uint32_t)i;
@@ -709,6 +771,138 @@ static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   return GVS_OK;
 }
 
+// ------------------------------------------- pipeline 2: fixed-slot transactions
+
+// Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
+// sort and the transaction slots (k_rtx), so that every fixed-capacity check
+// (mailbox groups, transaction slots) is decided before any state changes.
+static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride, uint32_t n) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B, nblk = e.nblk;
+  e.stamp_run = e.stamp_next++;
+  if (e.stamp_next == kNone) e.stamp_next = 1;
+  GVS_HIP(h, hipMemsetAsync(e.qcount, 0, (e.Q + 1) * sizeof(uint32_t), s));
+  GVS_HIP(h, hipMemsetAsync(e.pcount, 0, (e.W + 1) * sizeof(uint32_t), s));
+  const uint32_t xbase = B - e.X;
+  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
+                     (const uint4*)(e.X ? e.xb2[e.par ^ 1] : nullptr), xbase);
+  mark(h, "copy");
+  {
+    MetaArgs a{e.img, e.types, e.ops,  e.kinds, e.s1keys, e.qcount, n,
+               B,     e.Q,     e.logQ, e.N,     e.kc,     xbase};
+    hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
+  }
+  mark(h, "meta");
+  if (int r = sort_keys<Key128, 4>(h, e.s1keys, B)) return r;
+  mark(h, "sort_s1");
+  hipLaunchKernelGGL(k_m1<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  mark(h, "m1");
+  {
+    AllocArgs a = aargs(e);
+    hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
+  }
+  mark(h, "alloc");
+  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  mark(h, "sort_r");
+  {
+    RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,
+              B,       e.W,    e.S,           e.c,       B / kScanT,  e.stamp_run};
+    hipLaunchKernelGGL(k_scan_a<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "rtx");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B, nblk = e.nblk;
+  {
+    R2Args a{};
+    a.table = e.table;
+    a.tcur = e.tbuf[e.par];
+    a.tprev = e.tbuf[e.par ^ 1];
+    a.stamp_cur = e.stamp_run;
+    a.stamp_prev = e.stamp_prev;
+    a.pbuf = e.pbuf;
+    a.snap = e.snap;
+    a.dry = e.dryb;
+    a.scal = e.scal;
+    a.W = e.W;
+    a.S = e.S;
+    a.c = e.c;
+    a.xon = e.X ? 1u : 0u;
+    a.xk = e.xk;
+    a.xrot = e.epoch % e.xk;
+    a.xep = e.xep;
+    a.xexcl = e.xk == 1 ? 1u : 0u;
+    a.cutoff = h->cutoff;
+    a.xbuf = e.X ? e.xb2[e.par] : nullptr;
+    a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
+    hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+  }
+  mark(h, "rpass");
+  {
+    Rr1Args a{e.rpos, e.rop, e.img, e.snap, e.snapdummy, e.rsb, e.rr1_agg, e.rr1_carry, e.scal,
+              B,      B / kScanT, B - e.X};
+    hipLaunchKernelGGL(k_scan_a<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<Rr1Op>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "rr1");
+  {
+    Rr2Args a{};
+    a.vagg = e.vagg;
+    a.vagg2 = e.vagg2;
+    a.vcarry2 = e.vcarry2;
+    a.vcarry = e.vcarry;
+    a.scal = e.scal;
+    a.nvb = B / kVBlk;
+    a.nvb2 = (a.nvb + 63) / 64;
+    a.rs = e.rsb;
+    a.img = e.img;
+    a.snap = e.snap;
+    a.snapdummy = e.snapdummy;
+    a.pbuf = e.pbuf;
+    a.pdummy = e.pdummy;
+    a.resp = e.resp;
+    a.rres = e.rres;
+    a.B = B;
+    a.cutoff = h->cutoff;
+    hipLaunchKernelGGL(k_vscan_a<Rr2Op>, dim3((a.nvb + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_vscan_b1<Rr2Op>, dim3(a.nvb2), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_vscan_b2<Rr2Op>, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_vscan_b3<Rr2Op>, dim3(a.nvb2), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rr2_c, dim3(a.nvb), dim3(256), 0, s, a);
+  }
+  mark(h, "rr2");
+  {
+    PostArgs a{e.kinds, e.rres, e.rop, e.dflag, e.dslot, e.bsum2, e.ring, e.scal, B, nblk,
+               e.ring_size};
+    hipLaunchKernelGGL(k_post_sum, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
+  }
+  mark(h, "post");
+  hipLaunchKernelGGL(k_m2<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  if (d_out && n)
+    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
+  mark(h, "m2");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+static int phase_a_any(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride, uint32_t n) {
+  return h->pipeline == 2 ? phase_a2(h, e, d_in, stride, n) : phase_a(h, e, d_in, stride, n);
+}
+static int phase_b_any(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
+  return h->pipeline == 2 ? phase_b2(h, e, n, d_out) : phase_b(h, e, n, d_out);
+}
+
 static RouteArgs rargs(gvs_handle* h, const Router& r, const Engine& e, const uint4* in,
                        uint32_t n) {
   RouteArgs a{};
@@ -795,8 +989,8 @@ static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out)
   if (int r = reset_errors(h)) return r;
   if (h->mode == kSingle) {
     Engine& e = h->eng[0];
-    if (int r = phase_a(h, e, d_in, kAbiU4, n)) return r;
-    return phase_b(h, e, n, d_out);
+    if (int r = phase_a_any(h, e, d_in, kAbiU4, n)) return r;
+    return phase_b_any(h, e, n, d_out);
   }
   const uint32_t n_src = (uint32_t)h->rt.size();
   for (uint32_t k = 0; k < n_src; ++k) {
@@ -809,11 +1003,11 @@ static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out)
   mark(h, "xchg");
   const uint32_t SC = h->S * h->C;
   for (auto& e : h->eng)
-    if (int r = phase_a(h, e, e.recv, kSlotU4, SC)) return r;
+    if (int r = phase_a_any(h, e, e.recv, kSlotU4, SC)) return r;
   if (int r = agree_errors(h)) return r;
   mark(h, "agree");
   for (auto& e : h->eng)
-    if (int r = phase_b(h, e, SC, nullptr)) return r;
+    if (int r = phase_b_any(h, e, SC, nullptr)) return r;
   if (int r = exchange(h, false)) return r;
   mark(h, "xchg_back");
   for (uint32_t k = 0; k < n_src; ++k) {
@@ -853,11 +1047,21 @@ static int finish(gvs_handle* h) {
     h->err = "batch overflow: more than 512 distinct recipients in one mailbox partition";
     return GVS_ERR_BATCH_OVERFLOW;
   }
+  if (e & kRErr) {
+    h->err = "batch overflow: more distinct rows of one message partition than its transaction slots";
+    return GVS_ERR_BATCH_OVERFLOW;
+  }
   if (e) {
     h->err = "internal error flag " + std::to_string(e);
     return GVS_ERR_INTERNAL;
   }
-  for (auto& en : h->eng) en.epoch += 1;  // every row was rewritten at epoch + 1
+  for (auto& en : h->eng) {
+    en.epoch += 1;  // every row was rewritten at epoch + 1
+    if (h->pipeline == 2) {  // this batch's slots now hold the pending final states
+      en.par ^= 1u;
+      en.stamp_prev = en.stamp_run;
+    }
+  }
   return GVS_OK;
 }
 
@@ -998,6 +1202,14 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
     h->rpass_variant = (int)value;
     return GVS_OK;
   }
+  if (std::strcmp(key, "pipeline") == 0 && (value == 1 || value == 2)) {
+    // only between batches of a fresh store: the two keep different pending state
+    if (value == 2 && h->auth) return GVS_ERR_INVALID_ARG;
+    for (auto& e : h->eng)
+      if (e.epoch != 0) return GVS_ERR_INVALID_ARG;
+    h->pipeline = (int)value;
+    return GVS_OK;
+  }
   return GVS_ERR_INVALID_ARG;
 }
 
@@ -1063,6 +1275,19 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
   for (const auto& e : h->eng) {
     GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
     GVS_HIP(h, hipStreamSynchronize(h->stream));
+    if (h->pipeline == 2 && e.stamp_prev != kNone) {
+      // rows the last batch changed are pending in P (applied by the next pass)
+      const uint64_t WC = (uint64_t)e.W * e.c;
+      std::vector<uint4> td(WC * 8), pv(WC * 64);
+      GVS_HIP(h, hipMemcpy(td.data(), e.tbuf[e.par ^ 1], WC * 128, hipMemcpyDeviceToHost));
+      GVS_HIP(h, hipMemcpy(pv.data(), e.pbuf, WC * 1024, hipMemcpyDeviceToHost));
+      for (uint64_t k = 0; k < WC; ++k) {
+        const uint4 d = td[k * 8];
+        if (d.y != e.stamp_prev || d.x >= e.S) continue;
+        const uint64_t row = (k / e.c) * e.S + d.x;
+        std::memcpy(phys.data() + row * 1024, &pv[k * 64], 1024);
+      }
+    }
     for (uint64_t sl = 0; sl < N; ++sl) {
       uint64_t row = (sl % e.W) * e.S + sl / e.W;
       uint8_t* d = dst + sl * 1024;

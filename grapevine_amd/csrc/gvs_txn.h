@@ -1,0 +1,841 @@
+// gvs_txn.h — fixed-slot transactions of the message-table pass.
+//
+// The message pass used to apply every op to its row inside the workgroup
+// that owns the row's partition, so a workgroup's time grew with the ops
+// routed to it (a hot message or recipient made one workgroup long: a timing
+// leak, api/proto/grapevine.proto:120-122).  Here every piece of work has a
+// fixed size:
+//
+//   k_rtx_{a,b,c}  over the R-sorted ops (row, class, seq): each row an op
+//                  touches becomes ONE transaction slot of its partition (the
+//                  segmented rank of the row's first op); a partition has c
+//                  slots, more distinct rows is a batch overflow.  128-B slot
+//                  descriptors T (this batch) are stamped with the run id.
+//   k_rpass2       table pass, one workgroup per partition: streams all S rows,
+//                  applies the PREVIOUS batch's final row states P (c slots)
+//                  and snapshots this batch's rows (c slots of SNAP), reads
+//                  and writes every slot of both whether used or not.
+//   k_rr1_{a,b,c}  op-parallel: copy-forward of the row's identity along its
+//                  segment (the row's pre-batch identity from the snapshot,
+//                  the pop of a next-message DELETE, the record of a CREATE);
+//                  statuses of next ops and creates, match of by-id ops.
+//   k_rr2_{a,b,c}  op-parallel, one wave per op: copy-forward of the 1 KiB
+//                  record along the segment (a DELETE freezes it empty, an
+//                  UPDATE replaces it), every response, and the row's final
+//                  state into P by the segment's last op.
+//
+// P is applied by the next batch's pass (deferred write-back): the table pass
+// is the only kernel that touches table rows, every row exactly once.  Every
+// op reads and writes the same bytes whatever its kind or outcome, and every
+// per-position record is written by whole-line stores (DESIGN.md §3 rules).
+#pragma once
+#include "gvs_kernels.h"
+
+namespace gvs {
+
+constexpr uint32_t kScanT = 256;  // positions per block of the op scans (one thread each)
+constexpr uint32_t kRErr = 16u;   // error bit: a partition's distinct rows exceed c
+
+// -------------------------------------------------------------- utilities
+
+// Store a 128-B record per lane (rec[0..7]) to base[idx] through the wave's
+// LDS stage (64 x 128 B): every store instruction then writes 8 whole records,
+// so no record line is ever left partially written (DESIGN.md §3 rule 2).
+__device__ inline void wave_store128(uint4* stage, uint4* base, uint64_t idx, const uint4 (&rec)[8]) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int c = 0; c < 8; ++c) stage[lane * 8 + c] = rec[c];
+  wave_lds_sync();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t r = (uint32_t)it * 8 + (lane >> 3), ch = lane & 7u;
+    const uint64_t ix = shfl_u64(idx, (int)r);
+    base[ix * 8 + ch] = stage[r * 8 + ch];
+  }
+  wave_lds_sync();
+}
+
+// ---------------------------------------------------- generic op scans
+//
+// Three kernels over B positions, one thread per position: (a) block
+// aggregates, (b) one workgroup scans the aggregates, (c) each position gets
+// its exclusive prefix and emits.  Op supplies V, identity(), combine(a, b)
+// (a precedes b; associative), local(args, p) and emit(args, p, excl, loc).
+// Each phase reads every position's inputs once, whatever they hold.
+
+template <class V>
+__device__ inline void v_copy(V& d, const V& s) { d = s; }
+
+template <class Op>
+__device__ inline typename Op::V block_excl(const typename Op::V& x, typename Op::V* s,
+                                            typename Op::V& total) {
+  using V = typename Op::V;
+  const uint32_t t = threadIdx.x;
+  s[t] = x;
+  __syncthreads();
+  for (uint32_t d = 1; d < kScanT; d <<= 1) {
+    V y = s[t];
+    if (t >= d) y = Op::combine(s[t - d], y);
+    __syncthreads();
+    s[t] = y;
+    __syncthreads();
+  }
+  V ex = Op::identity();
+  if (t) ex = s[t - 1];
+  total = s[kScanT - 1];
+  __syncthreads();
+  return ex;
+}
+
+// Phase-B scans stop when the batch already failed (Op::stop): an abandoned
+// batch must not overwrite the pending final states of the previous one.
+template <class Op>
+__global__ __launch_bounds__(kScanT) void k_scan_a(typename Op::Args a) {
+  __shared__ typename Op::V s[kScanT];
+  if (Op::stop(a)) return;
+  const uint32_t p = blockIdx.x * kScanT + threadIdx.x;
+  typename Op::V tot;
+  block_excl<Op>(Op::local(a, p), s, tot);
+  if (threadIdx.x == 0) a.agg[blockIdx.x] = tot;
+}
+
+template <class Op>
+__global__ __launch_bounds__(kScanT) void k_scan_b(typename Op::Args a) {
+  using V = typename Op::V;
+  __shared__ V s[kScanT];
+  if (Op::stop(a)) return;
+  const uint32_t t = threadIdx.x, nb = a.nblk;
+  const uint32_t per = (nb + kScanT - 1) / kScanT, lo = min(nb, t * per), hi = min(nb, lo + per);
+  V r = Op::identity();
+  for (uint32_t i = lo; i < hi; ++i) r = Op::combine(r, a.agg[i]);
+  V tot;
+  V ex = block_excl<Op>(r, s, tot);
+  for (uint32_t i = lo; i < hi; ++i) {
+    a.carry[i] = ex;
+    ex = Op::combine(ex, a.agg[i]);
+  }
+}
+
+template <class Op>
+__global__ __launch_bounds__(kScanT) void k_scan_c(typename Op::Args a) {
+  __shared__ typename Op::V s[kScanT];
+  __shared__ uint4 stage[4 * 64 * 8];  // per-wave record stage (wave_store128)
+  if (Op::stop(a)) return;
+  const uint32_t p = blockIdx.x * kScanT + threadIdx.x;
+  const typename Op::V loc = Op::local(a, p);
+  typename Op::V tot;
+  typename Op::V ex = block_excl<Op>(loc, s, tot);
+  ex = Op::combine(a.carry[blockIdx.x], ex);
+  Op::emit(a, p, ex, loc, stage + (threadIdx.x >> 6) * 64 * 8);
+}
+
+// ------------------------------------------------------------ k_rtx
+
+// per sorted position: x = seq | head << 20 | last << 21 | null << 22,
+// y = global slot w*c + k of the op's row (kNone for null ops), z = w, w = row
+// offset in the partition
+constexpr uint32_t kPosHead = 1u << 20, kPosLast = 1u << 21, kPosNull = 1u << 22;
+
+struct RtxV {
+  uint32_t reset;  // position starts a partition
+  uint32_t cnt;    // row heads since the last partition start
+};
+
+struct RtxArgs {
+  const uint64_t* rkeys;  // sorted
+  uint4* rpos;            // B
+  uint4* tbuf;            // 128-B records: this batch's slots (W*c), then B dummies
+  RtxV* agg;
+  RtxV* carry;
+  Scal* scal;
+  uint32_t B, W, S, c, nblk, stamp;
+};
+
+struct RtxOp {
+  using V = RtxV;
+  using Args = RtxArgs;
+  __device__ static bool stop(const Args&) { return false; }  // phase A: always runs
+  __device__ static V identity() { return V{0u, 0u}; }
+  __device__ static V combine(const V& a, const V& b) {
+    return b.reset ? b : V{a.reset, a.cnt + b.cnt};
+  }
+  __device__ static void row_of(const Args& a, uint32_t p, uint64_t& row, uint32_t& w) {
+    const uint64_t k = a.rkeys[p];
+    row = k >> 22;
+    w = row == kRNullRow ? a.W : (uint32_t)(row / a.S);
+  }
+  __device__ static V local(const Args& a, uint32_t p) {
+    uint64_t row, prow = ~0ull;
+    uint32_t w, pw = ~0u;
+    row_of(a, p, row, w);
+    if (p) row_of(a, p - 1, prow, pw);
+    const bool head = row != kRNullRow && (p == 0 || row != prow);
+    return V{(uint32_t)(p == 0 || w != pw), head ? 1u : 0u};
+  }
+  __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
+    uint64_t row, nrow = ~0ull;
+    uint32_t w, nw;
+    row_of(a, p, row, w);
+    if (p + 1 < a.B) row_of(a, p + 1, nrow, nw);
+    const bool null = row == kRNullRow;
+    const bool head = loc.cnt != 0u;
+    const bool last = !null && (p + 1 == a.B || nrow != row);
+    // heads before this position in its partition (the row's own head included
+    // for non-heads)
+    const uint32_t before = loc.reset ? 0u : ex.cnt;
+    const uint32_t k = head ? before : before - 1u;
+    if (head && k >= a.c) atomicOr(&a.scal->error, kRErr);
+    const uint32_t kk = min(k, a.c - 1u);
+    const uint32_t o = null ? 0u : (uint32_t)(row - (uint64_t)w * a.S);
+    const uint32_t seq = (uint32_t)a.rkeys[p] & kSeqMask;
+    a.rpos[p] = make_uint4(seq | (head ? kPosHead : 0u) | (last ? kPosLast : 0u) | (null ? kPosNull : 0u),
+                           null ? kNone : w * a.c + kk, w, o);
+    uint4 rec[8];
+    rec[0] = make_uint4(o, a.stamp, 0u, 0u);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
+    const uint64_t idx = head ? (uint64_t)w * a.c + kk : (uint64_t)a.W * a.c + p;
+    wave_store128(stage, a.tbuf, idx, rec);
+  }
+};
+
+// --------------------------------------------------------- k_rpass2
+
+struct R2Args {
+  uint4* table;        // N rows x 64 uint4, partition-major
+  const uint4* tcur;   // this batch's slot descriptors (W*c records of 128 B)
+  const uint4* tprev;  // the previous applied batch's
+  uint32_t stamp_cur, stamp_prev;
+  const uint4* pbuf;   // W*c final row states of the previous batch
+  uint4* snap;         // W*c snapshots for this batch
+  uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
+  Scal* scal;
+  uint32_t W, S, c;
+  // expiry sweep: on the rows as they stand before this batch
+  uint32_t xon, xk, xrot, xep, xexcl;
+  uint64_t cutoff;
+  uint4* xbuf;         // records written by this pass
+  const uint4* xprev;  // records being deleted by this batch (exclusion)
+};
+
+// Expiry detection on a chunk (v1 x_detect plus the exclusion of rows whose
+// delete this batch already carries, lane 0 compares the row's id).
+template <int U>
+__device__ inline uint32_t x_detect2(const R2Args& a, const uint4 (&v)[U], uint4* buf, uint32_t xc,
+                                     const uint4* s_xx, uint32_t nx) {
+  const uint32_t lane = lane_id();
+  const uint32_t part = lane == 0 ? 0u : lane - 2u;
+  const bool writer = lane == 0 || lane == 3 || lane == 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t ts = ((uint64_t)v[u].y << 32) | v[u].x;
+    bool ex = false;
+    for (uint32_t k = 0; k < nx; ++k) ex |= eq4(v[u], s_xx[k]);
+    const uint64_t m_old = __ballot(lane == 5 && ts < a.cutoff);
+    const uint64_t m_msg = __ballot(lane == 0 && nz4(v[u]) && !ex);
+    const uint32_t hit = (uint32_t)((m_old >> 5) & m_msg & 1ull);
+    const uint32_t slot = min(xc, a.xep);
+    if (writer) buf[slot * 3 + part] = v[u];
+    xc += hit;
+  }
+  return xc;
+}
+
+__device__ inline uint32_t x_merge2(uint32_t xep, const uint4* s_xw, const uint32_t* s_xc,
+                                    uint4* s_xp, uint32_t tot) {
+  const uint32_t tid = threadIdx.x, cap = xep;
+  uint32_t add = 0;
+  if (tid < 3 * cap) {
+    const uint32_t k = tid / 3, c = tid % 3;
+    uint32_t off = k - tot, src = kNone;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t cw = min(s_xc[w], cap);
+      const bool take = k >= tot && src == kNone && off < cw;
+      src = selu32(take, ((uint32_t)w * (kXepMax + 1) + off) * 3 + c, src);
+      off -= cw;
+    }
+    if (src != kNone) s_xp[k * 3 + c] = s_xw[src];
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) add += min(s_xc[w], cap);
+  return min(tot + add, cap);
+}
+
+template <bool NTL>
+__device__ inline uint4 ld_line(const uint4* p) { return ld_row<NTL>(p); }
+
+template <int U, bool NTL, bool NTS, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
+  __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
+  __shared__ uint32_t s_np, s_ns;
+  __shared__ uint4 s_xw[4 * (kXepMax + 1) * 3];
+  __shared__ uint4 s_xp[kXepMax * 3];
+  __shared__ uint4 s_xx[kXepMax];
+  __shared__ uint32_t s_xc[4], s_xt;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t w = blockIdx.x;
+  if (a.scal->error) return;
+  for (uint32_t o = tid; o < a.S; o += 256) {
+    s_pk[o] = -1;
+    s_sk[o] = -1;
+  }
+  if (tid == 0) {
+    s_np = 0;
+    s_ns = 0;
+    s_xt = 0;
+  }
+  __syncthreads();
+  // every slot descriptor of this partition, both batches (fixed reads)
+  const uint64_t sbase = (uint64_t)w * a.c;
+  for (uint32_t k = tid; k < a.c; k += 256) {
+    const uint4 dp = a.tprev[(sbase + k) * 8];
+    const uint4 ds = a.tcur[(sbase + k) * 8];
+    if (dp.y == a.stamp_prev && dp.x < a.S) {
+      s_pk[dp.x] = (int16_t)k;
+      atomicAdd(&s_np, 1u);
+    }
+    if (ds.y == a.stamp_cur && ds.x < a.S) {
+      s_sk[ds.x] = (int16_t)k;
+      atomicAdd(&s_ns, 1u);
+    }
+  }
+  // the expiry deletes this batch already carries for this partition
+  uint32_t nx = 0;
+  if (a.xon && a.xexcl) {
+    if (tid < a.xep) {
+      const uint4 r = a.xprev[((uint64_t)w * a.xep + tid) * 8];
+      const uint4 vld = a.xprev[((uint64_t)w * a.xep + tid) * 8 + 3];
+      s_xx[tid] = vld.x ? r : make_uint4(0, 0, 0, 0);
+    }
+    nx = a.xep;
+  }
+  __syncthreads();
+  const uint32_t np = s_np, ns = s_ns;
+  uint4* part = a.table + (uint64_t)w * a.S * 64;
+  const uint4* pslot = a.pbuf + sbase * 64;
+  uint4* sslot = a.snap + sbase * 64;
+  uint4* dry = a.dry + (uint64_t)w * 64;
+  const uint32_t tiles = a.S / kTile;
+  for (uint32_t t = 0; t < tiles; ++t) {
+    uint32_t xc = 0;
+    const uint32_t rb = t * kTile + wave * 64;
+    for (uint32_t j = 0; j < 64; j += U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
+      uint32_t mp = 0, ms = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        mp |= s_pk[rb + j + u] >= 0 ? (1u << u) : 0u;
+        ms |= s_sk[rb + j + u] >= 0 ? (1u << u) : 0u;
+      }
+      mp = __builtin_amdgcn_readfirstlane(mp);
+      ms = __builtin_amdgcn_readfirstlane(ms);
+      // The first chunk of wave 0 runs each loop once "dry" on the workgroup's
+      // own dry line, so every workgroup executes the same code whatever its
+      // slots hold (instruction fetch shows in FETCH_SIZE, DESIGN.md §3 rule 6).
+      bool dry_p = t == 0 && j == 0 && wave == 0, dry_s = dry_p;
+      while (mp || dry_p) {  // rows the previous batch changed: its final state
+        const uint32_t bit = dry_p ? 0u : (mp & (0u - mp));
+        if (!dry_p) mp &= mp - 1u;
+        const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + (uint32_t)__builtin_ctz(bit | (1u << 31))];
+        const uint4* src = dry_p ? dry : pslot + (uint64_t)k * 64;
+        const uint4 x = ld_row<true>(&src[lane]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
+        dry_p = false;
+      }
+      while (ms || dry_s) {  // rows this batch touches: their snapshot
+        const uint32_t bit = dry_s ? 0u : (ms & (0u - ms));
+        if (!dry_s) ms &= ms - 1u;
+        const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31));
+        const int16_t k = dry_s ? (int16_t)0 : s_sk[rb + j + (u0 & 31u)];
+        uint4 cur = v[0];
+#pragma unroll
+        for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
+        uint4* dst = dry_s ? dry : sslot + (uint64_t)k * 64;
+        st_row<true>(&dst[lane], cur);
+        dry_s = false;
+      }
+      if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
+#pragma unroll
+      for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
+    }
+    if (lane == 0) s_xc[wave] = xc;
+    __syncthreads();
+    if (a.xon) {
+      const uint32_t tot = x_merge2(a.xep, s_xw, s_xc, s_xp, s_xt);
+      __syncthreads();
+      if (tid == 0) s_xt = tot;
+    }
+  }
+  // unused slots: every slot of P is read and every slot of SNAP written once
+  for (uint32_t k = np + wave; k < a.c; k += 4) {
+    uint4 x = ld_row<true>(&pslot[(uint64_t)k * 64 + lane]);
+    keep4(x);
+  }
+  for (uint32_t k = ns + wave; k < a.c; k += 4) st_row<true>(&sslot[(uint64_t)k * 64 + lane], make_uint4(0, 0, 0, 0));
+  if (a.xon && w % a.xk == a.xrot) {
+    __syncthreads();
+    if (wave == 0 && lane < 8 * a.xep) {
+      const uint32_t k = lane >> 3, part8 = lane & 7;
+      const bool valid = k < s_xt;
+      uint4 val = make_uint4(part8 == 3 && valid ? 1u : 0u, 0, 0, 0);
+      if (part8 < 3) val = valid ? s_xp[k * 3 + part8] : make_uint4(0, 0, 0, 0);
+      a.xbuf[((uint64_t)(w / a.xk) * a.xep + k) * 8 + part8] = val;
+    }
+  }
+}
+
+// ------------------------------------------------------------- k_rr1
+
+// set kinds of the record copy-forward (k_rr2)
+constexpr uint32_t kSetNone = 0, kSetRec = 1, kSetZero = 2, kFreeze = 3;
+// RS flags (word 1 of the 128-B per-position record)
+constexpr uint32_t kRsHead = 1u, kRsLast = 2u, kRsNull = 4u, kRsClass2 = 8u, kRsCand = 16u,
+                   kRsRcptOk = 32u, kRsExpiry = 64u;
+__device__ inline uint32_t rs_setkind(uint32_t f) { return (f >> 8) & 3u; }
+
+struct Rr1V {
+  uint32_t reset, nd_valid, cr_valid, pad;
+  uint4 r0[5];  // the row's identity before the batch: id, sender, recipient
+  uint4 nd;     // id popped by a next-message DELETE
+  uint4 cr[5];  // identity of the record a CREATE put in the row
+};
+
+struct Rr1Args {
+  const uint4* rpos;
+  const ROp* rop;
+  const uint4* img;
+  const uint4* snap;       // W*c slots
+  const uint4* snapdummy;  // B x 1 KiB (non-heads read their own, fixed bytes)
+  uint4* rs;               // B x 128 B
+  Rr1V* agg;
+  Rr1V* carry;
+  const Scal* scal;
+  uint32_t B, nblk, xbase;
+};
+
+struct Rr1Op {
+  using V = Rr1V;
+  using Args = Rr1Args;
+  __device__ static bool stop(const Args& a) { return a.scal->error != 0u; }
+  __device__ static V identity() {
+    V v;
+    v.reset = v.nd_valid = v.cr_valid = v.pad = 0;
+    for (int i = 0; i < 5; ++i) v.r0[i] = v.cr[i] = make_uint4(0, 0, 0, 0);
+    v.nd = make_uint4(0, 0, 0, 0);
+    return v;
+  }
+  // selects only (a branch over a struct would put it in scratch)
+  __device__ static V combine(const V& a, const V& b) {
+    V r;
+    const bool br = b.reset != 0u, bn = br || b.nd_valid, bc = br || b.cr_valid;
+    r.reset = selu32(br, 1u, a.reset);
+    r.nd_valid = selu32(bn, b.nd_valid, a.nd_valid);
+    r.cr_valid = selu32(bc, b.cr_valid, a.cr_valid);
+    r.pad = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      r.r0[i] = sel4(br, b.r0[i], a.r0[i]);
+      r.cr[i] = sel4(bc, b.cr[i], a.cr[i]);
+    }
+    r.nd = sel4(bn, b.nd, a.nd);
+    return r;
+  }
+  __device__ static V local(const Args& a, uint32_t p) {
+    const uint4 rp = a.rpos[p];
+    const uint32_t seq = rp.x & kSeqMask;
+    const bool head = rp.x & kPosHead, null = rp.x & kPosNull;
+    const ROp& r = a.rop[seq];
+    const uint32_t kind = r.kind, st = r.status;
+    const uint4* im = a.img + (uint64_t)seq * 64;
+    const uint4* sn = head ? a.snap + (uint64_t)rp.y * 64 : a.snapdummy + (uint64_t)p * 64;
+    V v = identity();
+    v.reset = (head || null) ? 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const uint4 s = sn[i];
+      v.r0[i] = sel4(head, s, make_uint4(0, 0, 0, 0));
+    }
+    const uint4 id = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    const uint4 q1 = im[1], q2 = im[2], q3 = im[3], q4 = im[4];
+    v.nd_valid = (!null && kind == KIND_NEXT_DEL && st == kPending) ? 1u : 0u;
+    v.nd = id;
+    v.cr_valid = (!null && kind == KIND_CREATE && st == kPending) ? 1u : 0u;
+    v.cr[0] = id;
+    v.cr[1] = q1;
+    v.cr[2] = q2;
+    v.cr[3] = q3;
+    v.cr[4] = q4;
+    return v;
+  }
+  __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
+    const uint4 rp = a.rpos[p];
+    const uint32_t seq = rp.x & kSeqMask;
+    const bool head = rp.x & kPosHead, last = rp.x & kPosLast, null = rp.x & kPosNull;
+    const ROp& r = a.rop[seq];
+    const uint32_t kind = r.kind;
+    const uint4* im = a.img + (uint64_t)seq * 64;
+    const uint4 qid = im[0], q1 = im[1], q2 = im[2], q3 = im[3], q4 = im[4];
+    const V in = combine(ex, loc);  // this op's own head / pop / create included
+    const bool r0_exists = nz4(in.r0[0]);
+    const uint4 rid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    // the pop of a next-message DELETE succeeds on a row that holds its id
+    const bool nd_ok = in.nd_valid && r0_exists && eq4(in.nd, in.r0[0]);
+    const bool is_next = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
+    const bool is_create = kind == KIND_CREATE;
+    uint32_t status = r.status, setk = kSetNone, flags = 0;
+    uint4 ident[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) ident[i] = in.r0[i];
+    if (!null && is_next) {
+      // M1 resolved it to this row: the row must hold that id
+      status = (r0_exists && eq4(in.r0[0], rid)) ? 1u : 8u;
+      setk = (kind == KIND_NEXT_DEL && status == 1u) ? kSetZero : kSetNone;
+    } else if (!null && is_create) {
+      // the allocator hands out free rows: the row is empty after the pops
+      status = (r0_exists && !nd_ok) ? 8u : 1u;
+      setk = status == 1u ? kSetRec : kSetNone;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) ident[i] = in.cr[i];
+    } else if (!null) {
+      // by-id READ / UPDATE / DELETE: the row as the creates and pops of this
+      // batch left it (class order: pops, creates, then these)
+      const bool cr_ok = in.cr_valid && !(r0_exists && !nd_ok);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        ident[i] = sel4(cr_ok, in.cr[i], sel4(nd_ok, make_uint4(0, 0, 0, 0), in.r0[i]));
+      const bool exists1 = nz4(ident[0]);
+      const bool cand = exists1 && eq4(qid, ident[0]) &&
+                        ((eq4(q1, ident[1]) && eq4(q2, ident[2])) || (eq4(q1, ident[3]) && eq4(q2, ident[4])));
+      const bool rcpt_ok = eq4(q3, ident[3]) && eq4(q4, ident[4]);
+      const bool expiry = seq >= a.xbase;
+      flags |= kRsClass2 | (cand ? kRsCand : 0u) | (rcpt_ok ? kRsRcptOk : 0u) | (expiry ? kRsExpiry : 0u);
+      if (cand && rcpt_ok && !expiry) {
+        if (kind == KIND_UPDATE) setk = kSetRec;
+        if (kind == KIND_DELETE) setk = kFreeze;
+      }
+    }
+    flags |= (head ? kRsHead : 0u) | (last ? kRsLast : 0u) | (null ? kRsNull : 0u) | (setk << 8);
+    uint4 rec[8];
+    rec[0] = make_uint4(seq, flags, status, kind);
+    rec[1] = make_uint4(rp.y, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) rec[2 + i] = ident[i];
+    rec[7] = make_uint4(0, 0, 0, 0);
+    wave_store128(stage, a.rs, p, rec);
+  }
+};
+
+// ------------------------------------------------- 1 KiB copy-forward scans
+//
+// Scans whose carried value is a 1 KiB row (lane l of a wave holds 16 B) and
+// whose element flags F (4 words, wave-uniform) say how the value moves:
+// Op::takes_b(a, b) is true when b's value replaces the running one, and
+// Op::f_combine is associative.  The value itself is never combined, only
+// selected, so a block aggregate carries the value of one op.
+//   vscan_a   one wave per block of 64 ops: flag scan, then the defining
+//             op's value (one 1 KiB read per block) -> agg
+//   vscan_b1  one workgroup per 64 blocks: sequential in registers, 16 blocks
+//             per wave -> per-64-block aggregates
+//   vscan_b2  one wave: exclusive carries of the 64-block aggregates
+//   vscan_b3  as b1, re-walked from its carry: exclusive carry of every block
+// Every aggregate is read the same number of times whatever it holds, and each
+// value is copied, never re-read by many readers (shared reads would hit in L2
+// and make FETCH_SIZE depend on the data).  The op-specific phase C walks 16
+// ops per wave from its carry (vscan_carry_in).
+
+constexpr uint32_t kVBlk = 64;        // ops per block aggregate
+constexpr uint32_t kVLineU4 = 72;     // aggregate record: flag line + 1 KiB value
+
+template <class Op>
+__device__ inline void f_walk(const typename Op::Args& a, uint32_t p0, uint32_t n, uint4& f,
+                              uint32_t& idx) {
+  f = Op::f_identity();
+  idx = 0;
+#pragma unroll 16
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint4 e = Op::f_of(a, p0 + j);
+    idx = Op::takes_b(f, e) ? j : idx;
+    f = Op::f_combine(f, e);
+  }
+}
+
+__device__ inline uint4 uni4(uint4 x) {
+  return make_uint4(__builtin_amdgcn_readfirstlane(x.x), __builtin_amdgcn_readfirstlane(x.y),
+                    __builtin_amdgcn_readfirstlane(x.z), __builtin_amdgcn_readfirstlane(x.w));
+}
+
+__device__ inline void vrec_store(uint4* rec, uint4 f, uint4 v) {
+  const uint32_t lane = lane_id();
+  rec[8 + lane] = v;
+  if (lane < 8) rec[lane] = lane == 0 ? f : make_uint4(0, 0, 0, 0);
+}
+
+template <class Op>
+__global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
+  if (a.scal->error) return;
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.nvb) return;
+  uint4 f;
+  uint32_t d;
+  f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
+  const uint4 v = Op::value_of(a, b * kVBlk + d, f);
+  vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, v);
+}
+
+// sequential combine of records rec[i], i in [lo, hi), into (f, v); with
+// `out`, also the exclusive carries out[i]
+template <class Op>
+__device__ inline void vwalk_records(const uint4* rec, uint32_t lo, uint32_t hi, uint4& f, uint4& v,
+                                     uint4* out) {
+  const uint32_t lane = lane_id();
+  for (uint32_t i0 = lo; i0 < hi; i0 += 8) {
+    uint4 rf[8], rv[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {  // loads of 8 records in flight together
+      const uint32_t i = min(i0 + u, hi - 1);
+      rf[u] = rec[(uint64_t)i * kVLineU4];
+      rv[u] = rec[(uint64_t)i * kVLineU4 + 8 + lane];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      if (i0 + u < hi) {
+        if (out) vrec_store(out + (uint64_t)(i0 + u) * kVLineU4, f, v);
+        const uint4 e = uni4(rf[u]);
+        v = sel4(Op::takes_b(f, e), rv[u], v);
+        f = Op::f_combine(f, e);
+      }
+    }
+  }
+}
+
+template <class Op>
+__global__ __launch_bounds__(256) void k_vscan_b1(typename Op::Args a) {
+  if (a.scal->error) return;
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t lo = min(a.nvb, blockIdx.x * 64 + wave * 16), hi = min(a.nvb, lo + 16);
+  uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
+  vwalk_records<Op>(a.vagg, lo, hi, f, v, nullptr);
+  s_v[wave][lane] = v;
+  if (lane == 0) s_f[wave] = f;
+  __syncthreads();
+  if (wave == 0) {
+    uint4 g = Op::f_identity(), gv = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < 4; ++k) {
+      const uint4 e = s_f[k];
+      gv = sel4(Op::takes_b(g, e), s_v[k][lane], gv);
+      g = Op::f_combine(g, e);
+    }
+    vrec_store(a.vagg2 + (uint64_t)blockIdx.x * kVLineU4, g, gv);
+  }
+}
+
+template <class Op>
+__global__ __launch_bounds__(64) void k_vscan_b2(typename Op::Args a) {
+  if (a.scal->error) return;
+  uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
+  vwalk_records<Op>(a.vagg2, 0, a.nvb2, f, v, a.vcarry2);
+}
+
+template <class Op>
+__global__ __launch_bounds__(256) void k_vscan_b3(typename Op::Args a) {
+  if (a.scal->error) return;
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t lo = min(a.nvb, blockIdx.x * 64 + wave * 16), hi = min(a.nvb, lo + 16);
+  uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
+  vwalk_records<Op>(a.vagg, lo, hi, f, v, nullptr);
+  s_v[wave][lane] = v;
+  if (lane == 0) s_f[wave] = f;
+  __syncthreads();
+  const uint4* c = a.vcarry2 + (uint64_t)blockIdx.x * kVLineU4;
+  uint4 cf = uni4(c[0]), cv = c[8 + lane];
+  for (uint32_t k = 0; k < wave; ++k) {
+    const uint4 e = s_f[k];
+    cv = sel4(Op::takes_b(cf, e), s_v[k][lane], cv);
+    cf = Op::f_combine(cf, e);
+  }
+  vwalk_records<Op>(a.vagg, lo, hi, cf, cv, a.vcarry);
+}
+
+// Phase C prologue: the carry into the first of this wave's 16 ops (block
+// carry, then the aggregates of the block's earlier waves through LDS).  Each
+// wave reads one value of its own ops here, which its walk re-reads.
+template <class Op>
+__device__ inline void vscan_carry_in(const typename Op::Args& a, uint4 (*s_v)[64], uint4* s_f,
+                                      uint4& cf, uint4& cv) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x, p0 = b * kVBlk + wave * 16;
+  uint4 f;
+  uint32_t d;
+  f_walk<Op>(a, p0, 16, f, d);
+  s_v[wave][lane] = Op::value_of(a, p0 + d, f);
+  if (lane == 0) s_f[wave] = f;
+  __syncthreads();
+  const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
+  cf = uni4(c[0]);
+  cv = c[8 + lane];
+  for (uint32_t k = 0; k < wave; ++k) {
+    const uint4 e = s_f[k];
+    cv = sel4(Op::takes_b(cf, e), s_v[k][lane], cv);
+    cf = Op::f_combine(cf, e);
+  }
+}
+
+// common vscan buffers (each Op's Args embeds these names)
+#define GVS_VSCAN_FIELDS                                                    \
+  uint4* vagg;    /* nvb block aggregates */                                \
+  uint4* vagg2;   /* nvb2 = ceil(nvb / 64) aggregates of 64 blocks */      \
+  uint4* vcarry2; /* their exclusive carries */                             \
+  uint4* vcarry;  /* nvb exclusive block carries */                         \
+  const Scal* scal;                                                         \
+  uint32_t nvb, nvb2;
+
+// ------------------------------------------------------------- k_rr2
+//
+// The record copy-forward of the message rows.  The element of an op: reset
+// (row head: the snapshot), then its own effect: a set (CREATE, UPDATE: the
+// request image with the row identity in lanes 0..4), a set to empty (a
+// popping next DELETE), or a freeze (a DELETE: empty, and nothing after it in
+// the row applies).  F = {reset, frozen, has, 0}.
+
+struct Rr2Args {
+  GVS_VSCAN_FIELDS
+  const uint4* rs;        // B x 128 B
+  const uint4* img;
+  const uint4* snap;
+  const uint4* snapdummy;
+  uint4* pbuf;            // W*c final states
+  uint4* pdummy;          // B x 1 KiB
+  uint4* resp;            // B internal response slots (kRespSlot)
+  RRes* rres;
+  uint32_t B;
+  uint64_t cutoff;
+};
+
+// the per-position record words every lane needs (RS lines 0 and 1)
+struct RsHdr {
+  uint32_t seq, flags, status, kind, slot;
+};
+
+__device__ inline RsHdr rs_hdr(const uint4* rs, uint32_t p) {
+  const uint4 w0 = uni4(rs[(uint64_t)p * 8]), w1 = uni4(rs[(uint64_t)p * 8 + 1]);
+  return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x};
+}
+
+struct Rr2Op {
+  using Args = Rr2Args;
+  __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
+  __device__ static uint4 f_combine(uint4 a, uint4 b) {
+    uint4 r = sel4(b.z != 0u, make_uint4(a.x, 0u, 1u, 0u), a);
+    r = sel4(b.y != 0u, make_uint4(a.x, 1u, 1u, 0u), r);
+    r = sel4(a.y != 0u, a, r);
+    return sel4(b.x != 0u, b, r);
+  }
+  __device__ static bool takes_b(uint4 a, uint4 b) { return b.x || (!a.y && (b.y || b.z)); }
+  __device__ static uint4 f_of_hdr(const RsHdr& h) {
+    const uint32_t sk = rs_setkind(h.flags);
+    uint4 e = make_uint4((h.flags & (kRsHead | kRsNull)) ? 1u : 0u, 0u, 0u, 0u);
+    e.z = e.x;
+    if (sk == kSetRec || sk == kSetZero) e.z = 1u;
+    if (sk == kFreeze) e.y = e.z = 1u;
+    return e;
+  }
+  __device__ static uint4 f_of(const Args& a, uint32_t p) { return f_of_hdr(rs_hdr(a.rs, p)); }
+  // value of op p's own element, lane-wise, from its sources: the snapshot for
+  // a head without a set, the request image with the row identity (RS lines
+  // 2..6 -> lanes 0..4) for a set, empty for a pop / freeze / null op
+  __device__ static uint4 own_value(const RsHdr& h, uint4 snapv, uint4 imgv, uint4 identv) {
+    const uint32_t lane = lane_id(), sk = rs_setkind(h.flags);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 v = sel4((h.flags & kRsHead) != 0u, snapv, z);
+    v = sel4(sk == kSetRec, sel4(lane < 5, identv, imgv), v);
+    v = sel4(sk == kSetZero || sk == kFreeze || (h.flags & kRsNull), z, v);
+    return v;
+  }
+  __device__ static uint4 ident_of(const Args& a, uint32_t p) {
+    return a.rs[(uint64_t)p * 8 + 2 + min(lane_id(), 4u)];
+  }
+  // the aggregate value: one 1 KiB read, always a line phase C also reads
+  // (the head's snapshot, or the op's request image)
+  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 f) {
+    const RsHdr h = rs_hdr(a.rs, p);
+    const bool from_snap = (h.flags & kRsHead) && rs_setkind(h.flags) != kSetRec;
+    const uint4* src = from_snap ? a.snap + (uint64_t)h.slot * 64 : a.img + (uint64_t)h.seq * 64;
+    const uint4 x = ld_row<false>(&src[lane_id()]);
+    const uint4 v = own_value(h, x, x, ident_of(a, p));
+    return sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v);
+  }
+};
+
+// failure record: all zero but the request's server time (lane 5 low 8 B)
+__device__ inline uint4 fail_rec(uint4 imgv, uint32_t status) {
+  const uint32_t lane = lane_id();
+  const uint4 ts = shfl4(imgv, 5);
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (lane == 5 && status != 0u) {
+    r.x = ts.x;
+    r.y = ts.y;
+  }
+  return r;
+}
+
+// k_rr2_c: each wave walks its 16 ops in order from its carry: statuses of
+// by-id ops, every response, and the rows' final states (the row's last op
+// writes its P slot, every other op its own dummy line: fixed bytes)
+__global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
+  if (a.scal->error) return;
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint4 cf, cv;
+  vscan_carry_in<Rr2Op>(a, s_v, s_f, cf, cv);
+  const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t p = p0 + j;
+    const RsHdr h = rs_hdr(a.rs, p);
+    const bool head = h.flags & kRsHead;
+    const uint4* sp = head ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)p * 64;
+    const uint4 sv = ld_row<false>(&sp[lane]);
+    const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+    const uint4 idv = Rr2Op::ident_of(a, p);
+    // the row state before this op
+    const uint4 pf = sel4(head, make_uint4(1u, 0u, 1u, 0u), cf);
+    const uint4 pv = sel4(head, sv, cv);
+    uint32_t status = h.status;
+    if (h.flags & kRsClass2) {
+      // by-id op: the row must still hold the record it named (no DELETE
+      // before it in this batch); an expiry delete also needs the record's
+      // current time below the cutoff
+      const uint64_t ts = ((uint64_t)__shfl(pv.y, 5) << 32) | __shfl(pv.x, 5);
+      const bool fresh = (h.flags & kRsExpiry) && !(ts < a.cutoff);
+      const bool found = (h.flags & kRsCand) && !pf.y && !fresh;
+      status = !found ? 2u : ((h.kind != KIND_READ && !(h.flags & kRsRcptOk)) ? 4u : 1u);
+    }
+    const bool ok = status == 1u;
+    const uint4 own = Rr2Op::own_value(h, sv, iv, idv);
+    const uint4 resp = sel4(!ok, fail_rec(iv, status), sel4(rs_setkind(h.flags) == kSetRec, own, pv));
+    const uint4 e = Rr2Op::f_of_hdr(h);
+    cv = sel4(Rr2Op::takes_b(cf, e), own, cv);
+    cf = Rr2Op::f_combine(cf, e);
+    // an expiry delete is the last op of its row: it only decides the final state
+    const uint4 fin = sel4((h.flags & kRsExpiry) && ok, make_uint4(0, 0, 0, 0), cv);
+    uint4* dst = a.resp + (uint64_t)h.seq * (kRespSlot / 16);
+    dst[lane] = resp;
+    if (lane < 8) {
+      const uint4 t = make_uint4(lane == 0 ? status : 0u, 0, 0, 0);
+      dst[64 + lane] = t;
+      reinterpret_cast<uint4*>(a.rres)[(uint64_t)h.seq * 8 + lane] = t;
+    }
+    uint4* pd = (h.flags & kRsLast) ? a.pbuf + (uint64_t)h.slot * 64 : a.pdummy + (uint64_t)p * 64;
+    st_row<true>(&pd[lane], fin);
+  }
+}
+
+}  // namespace gvs

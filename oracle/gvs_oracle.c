@@ -214,7 +214,7 @@ gvo_model *gvo_create(const gvs_config *cfg) {
   m->tail = m->N;
   /* message-table partitions of the engine (gvs_engine.hip engine_init): the
    * expiry sweep's selection rule is defined over them [D] */
-  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : m->N / 16384;
+  uint64_t S = cfg->rows_per_partition ? cfg->rows_per_partition : m->N / 4096;
   if (S < 256) S = 256;
   if (S > 4096) S = 4096;
   if (S > m->N) S = m->N;
