@@ -24,7 +24,7 @@
 #include "../../include/gvstore_test.h"
 #include "gvs_kernels.h"
 #include "gvs_route.h"
-#include "gvs_txn.h"
+#include "gvs_mtx.h"
 
 using namespace gvs;
 
@@ -115,6 +115,16 @@ struct Engine {
   Rr1V* rr1_agg = nullptr;
   Rr1V* rr1_carry = nullptr;
   uint4* vagg = nullptr, *vagg2 = nullptr, *vcarry2 = nullptr, *vcarry = nullptr;
+  // fixed-slot mailbox passes (gvs_mtx.h)
+  uint32_t cm = 0;           // group slots per mailbox partition
+  uint4* mpos = nullptr;     // B
+  uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
+  uint4* msnap = nullptr;    // Q*cm x 1 KiB
+  uint4* mdummy = nullptr;   // B x 1 KiB
+  uint4* mdry = nullptr;     // Q x 1 KiB
+  uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
+  GtxV* gtx_agg = nullptr;
+  GtxV* gtx_carry = nullptr;
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -372,6 +382,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   e.ring_size = e.N + B;
   if (e.W + 1 > (uint32_t)kBinsMax) return GVS_ERR_INVALID_ARG;
   e.c = txn_slots(B, e.W, e.S);
+  e.cm = txn_slots(B, e.Q, kGroupMax);  // recipient groups per mailbox partition
   // expiry sweep: X records per batch; workgroups w = epoch (mod xk) record
   // xep each (X >= W: every workgroup, X / W each; X < W: one each, a rotating
   // 1/xk of the workgroups)
@@ -447,6 +458,15 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(vcarry, nvb * kVLineU4);
     A(vagg2, nvb2 * kVLineU4);
     A(vcarry2, nvb2 * kVLineU4);
+    const uint64_t QC = (uint64_t)e.Q * e.cm;
+    A(mpos, B);
+    A(gtx, (QC + B) * 8);
+    A(msnap, QC * 64);
+    A(mdummy, (uint64_t)B * 64);
+    A(mdry, (uint64_t)e.Q * 64);
+    A(m2tx, (QC + B) * kVLineU4);
+    A(gtx_agg, B / kScanT);
+    A(gtx_carry, B / kScanT);
   }
 #undef A
   hipStream_t s = h->stream;
@@ -456,6 +476,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
   if (e.X) GVS_HIP(h, hipMemsetAsync(e.xbuf, 0, (uint64_t)e.X * 128, s));
+  GVS_HIP(h, hipMemsetAsync(e.gtx, 0, ((uint64_t)e.Q * e.cm + B) * 128, s));
   for (int k = 0; k < 2; ++k) {
     GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, ((uint64_t)e.W * e.c + B) * 128, s));
     if (e.X) GVS_HIP(h, hipMemsetAsync(e.xb2[k], 0, (uint64_t)e.X * 128, s));
@@ -773,6 +794,37 @@ static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
 
 // ------------------------------------------- pipeline 2: fixed-slot transactions
 
+static MArgs margs2(const gvs_handle* h, const Engine& e) {
+  MArgs a = margs(h, e);
+  a.gtx = e.gtx;
+  a.m2tx = e.m2tx;
+  a.msnap = e.msnap;
+  a.mdry = e.mdry;
+  a.stamp = e.stamp_run;
+  a.cm = e.cm;
+  return a;
+}
+
+template <class A>
+static void vscan_fields(A& a, const Engine& e) {
+  a.vagg = e.vagg;
+  a.vagg2 = e.vagg2;
+  a.vcarry2 = e.vcarry2;
+  a.vcarry = e.vcarry;
+  a.scal = e.scal;
+  a.nvb = e.B / kVBlk;
+  a.nvb2 = (a.nvb + 63) / 64;
+}
+
+// the four scan kernels of a 1 KiB copy-forward (phase C is op-specific)
+template <class Op>
+static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
+  hipLaunchKernelGGL(k_vscan_a<Op>, dim3((a.nvb + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_vscan_b1<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_vscan_b2<Op>, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_vscan_b3<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
+}
+
 // Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
 // sort and the transaction slots (k_rtx), so that every fixed-capacity check
 // (mailbox groups, transaction slots) is decided before any state changes.
@@ -791,12 +843,35 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     MetaArgs a{e.img, e.types, e.ops,  e.kinds, e.s1keys, e.qcount, n,
                B,     e.Q,     e.logQ, e.N,     e.kc,     xbase};
     hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
   }
   mark(h, "meta");
   if (int r = sort_keys<Key128, 4>(h, e.s1keys, B)) return r;
   mark(h, "sort_s1");
-  hipLaunchKernelGGL(k_m1<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  {
+    GtxArgs a{e.s1keys, e.ops, e.mpos, e.gtx, e.gtx_agg, e.gtx_carry, e.scal,
+              B,        e.Q,   e.logQ, e.cm,  B / kScanT, e.stamp_run};
+    hipLaunchKernelGGL(k_scan_a<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<GtxOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "gtx");
+  if (h->auth)
+    hipLaunchKernelGGL(k_m1x<true>, dim3(e.Q), dim3(256), 0, s, margs2(h, e));
+  else
+    hipLaunchKernelGGL(k_m1x<false>, dim3(e.Q), dim3(256), 0, s, margs2(h, e));
+  {
+    M1rArgs a{};
+    vscan_fields(a, e);
+    a.mpos = e.mpos;
+    a.ops = e.ops;
+    a.msnap = e.msnap;
+    a.mdummy = e.mdummy;
+    a.m1out = e.m1out;
+    a.N = e.N;
+    a.kc = e.kc;
+    vscan_abc<M1rOp>(s, a);
+    hipLaunchKernelGGL(k_m1r_c, dim3(a.nvb), dim3(256), 0, s, a);
+  }
   mark(h, "m1");
   {
     AllocArgs a = aargs(e);
@@ -857,13 +932,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   mark(h, "rr1");
   {
     Rr2Args a{};
-    a.vagg = e.vagg;
-    a.vagg2 = e.vagg2;
-    a.vcarry2 = e.vcarry2;
-    a.vcarry = e.vcarry;
-    a.scal = e.scal;
-    a.nvb = B / kVBlk;
-    a.nvb2 = (a.nvb + 63) / 64;
+    vscan_fields(a, e);
     a.rs = e.rsb;
     a.img = e.img;
     a.snap = e.snap;
@@ -874,10 +943,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.rres = e.rres;
     a.B = B;
     a.cutoff = h->cutoff;
-    hipLaunchKernelGGL(k_vscan_a<Rr2Op>, dim3((a.nvb + 3) / 4), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_vscan_b1<Rr2Op>, dim3(a.nvb2), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_vscan_b2<Rr2Op>, dim3(1), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_vscan_b3<Rr2Op>, dim3(a.nvb2), dim3(256), 0, s, a);
+    vscan_abc<Rr2Op>(s, a);
     hipLaunchKernelGGL(k_rr2_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
   mark(h, "rr2");
@@ -888,7 +954,26 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
   }
   mark(h, "post");
-  hipLaunchKernelGGL(k_m2<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
+  {
+    M2rArgs a{};
+    vscan_fields(a, e);
+    a.mpos = e.mpos;
+    a.ops = e.ops;
+    a.rop = e.rop;
+    a.rres = e.rres;
+    a.m1out = e.m1out;
+    a.m2tx = e.m2tx;
+    a.Q = e.Q;
+    a.cm = e.cm;
+    a.stamp = e.stamp_run;
+    vscan_abc<M2rOp>(s, a);
+    hipLaunchKernelGGL(k_m2r_c, dim3(a.nvb), dim3(256), 0, s, a);
+  }
+  mark(h, "m2r");
+  if (h->auth)
+    hipLaunchKernelGGL(k_m2x<true>, dim3(e.Q), dim3(256), 0, s, margs2(h, e));
+  else
+    hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), 0, s, margs2(h, e));
   if (d_out && n)
     hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
   mark(h, "m2");
@@ -1044,7 +1129,9 @@ static int finish(gvs_handle* h) {
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & 1u) {
-    h->err = "batch overflow: more than 512 distinct recipients in one mailbox partition";
+    h->err = h->pipeline == 2
+                 ? "batch overflow: more recipients in one mailbox partition than its group slots"
+                 : "batch overflow: more than 512 distinct recipients in one mailbox partition";
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & kRErr) {

@@ -415,6 +415,12 @@ struct MArgs {
   SealCtx sc;          // authenticated storage (AUTH instantiations)
   const uint32_t* te;  // AES table (256 words)
   uint4* btag;         // R mailbox row tags
+  // fixed-slot mailbox passes (gvs_mtx.h)
+  const uint4* gtx;    // Q*cm group descriptors (128 B) of this batch
+  const uint4* m2tx;   // Q*cm group results (1152 B) for the write pass
+  uint4* msnap;        // Q*cm group snapshots (1 KiB) from the read pass
+  uint4* mdry;         // Q x 1 KiB: each workgroup's dry-run line
+  uint32_t stamp, cm;
 };
 
 // packed per-op info kept in LDS: seq | class<<20 | sub<<22 | success<<23

@@ -1,0 +1,671 @@
+// gvs_mtx.h — fixed-slot transactions of the mailbox passes.
+//
+// The mailbox passes used to discover each partition's recipient groups from
+// its sorted ops and to visit every op inside the partition's workgroup, so a
+// hot recipient made one workgroup long (a timing leak).  Here:
+//
+//   k_gtx_{a,b,c}  over the S1-sorted ops (recipient hash, class, seq): each
+//                  recipient group becomes ONE slot of its mailbox partition
+//                  (cm slots; more groups is a batch overflow); the group's
+//                  last op writes the 128-B group descriptor (counts per
+//                  class, first create), every other op a dummy line.
+//   k_m1x          mailbox read pass, one workgroup per partition: matches
+//                  rows to its cm slots, admits new recipients, and writes
+//                  every slot's snapshot (the row's 62 ids, with the group's
+//                  verdict in lanes 0..1): cm slots whatever they hold.
+//   k_m1r_*        op-parallel copy-forward of the snapshot along the group:
+//                  next-message ops take id d, creates their mailbox verdict,
+//                  by-id deletes the position of their id.
+//   k_m2r_*        op-parallel after the message pass: per group the ids of
+//                  its successful creates (lane 2 + rank) and the removal mask
+//                  of its successful by-id deletes -> the group's result slot.
+//   k_m2x          mailbox write pass: every row rewritten, every result slot
+//                  read once.
+#pragma once
+#include "gvs_txn.h"
+
+namespace gvs {
+
+// ---------------------------------------------------------------- k_gtx
+
+// per S1-sorted position: x = seq | head << 20 | last << 21 | null << 22 |
+// class << 23 | sub << 25, y = slot q*cm + k (kNone: no mailbox), z = q,
+// w = rank among the group's creates
+constexpr uint32_t kMPosHead = 1u << 20, kMPosLast = 1u << 21, kMPosNull = 1u << 22;
+__host__ __device__ inline uint32_t mpos_cls(uint32_t x) { return (x >> 23) & 3u; }
+__host__ __device__ inline uint32_t mpos_sub(uint32_t x) { return (x >> 25) & 1u; }
+
+struct GtxV {
+  uint32_t preset, gcnt;                            // partition segments: group heads
+  uint32_t greset, n_next, n_del, n_create, n_x;    // group segments: counts per class
+  uint32_t fcs, g0, c1;                             // first create's seq, group start, first create
+};
+
+struct GtxArgs {
+  const Key128* keys;  // sorted
+  const OpState* ops;
+  uint4* mpos;         // B
+  uint4* gtx;          // 128-B records: Q*cm group slots, then B dummies
+  GtxV* agg;
+  GtxV* carry;
+  Scal* scal;
+  uint32_t B, Q, logQ, cm, nblk, stamp;
+};
+
+struct GtxOp {
+  using V = GtxV;
+  using Args = GtxArgs;
+  __device__ static bool stop(const Args&) { return false; }  // phase A
+  __device__ static V identity() { return V{0, 0, 0, 0, 0, 0, 0, kNone, 0, kNone}; }
+  __device__ static V combine(const V& a, const V& b) {
+    V r;
+    r.preset = selu32(b.preset != 0u, 1u, a.preset);
+    r.gcnt = selu32(b.preset != 0u, b.gcnt, a.gcnt + b.gcnt);
+    const bool g = b.greset != 0u;
+    r.greset = selu32(g, 1u, a.greset);
+    r.n_next = selu32(g, b.n_next, a.n_next + b.n_next);
+    r.n_del = selu32(g, b.n_del, a.n_del + b.n_del);
+    r.n_create = selu32(g, b.n_create, a.n_create + b.n_create);
+    r.n_x = selu32(g, b.n_x, a.n_x + b.n_x);
+    r.fcs = selu32(g, b.fcs, selu32(a.fcs != kNone, a.fcs, b.fcs));
+    r.g0 = selu32(g, b.g0, a.g0);
+    r.c1 = selu32(g, b.c1, selu32(a.c1 != kNone, a.c1, b.c1));
+    return r;
+  }
+  __device__ static uint32_t part(const Args& a, const Key128& k) {
+    const bool null = s1_class(k.lo) == 3u;
+    return null ? a.Q : (a.logQ ? (uint32_t)(k.hi >> (64 - a.logQ)) : 0u);
+  }
+  __device__ static bool same_group(const Key128& x, const Key128& y) {
+    return x.hi == y.hi && s1_group(x.lo) == s1_group(y.lo);
+  }
+  __device__ static V local(const Args& a, uint32_t p) {
+    const Key128 k = a.keys[p];
+    Key128 pk = {~0ull, ~0ull};
+    if (p) pk = a.keys[p - 1];
+    const uint32_t cls = s1_class(k.lo), seq = s1_seq(k.lo);
+    const bool null = cls == 3u;
+    const bool gh = !null && (p == 0 || !same_group(k, pk));
+    const bool ph = p == 0 || part(a, k) != part(a, pk);
+    V v;
+    v.preset = ph ? 1u : 0u;
+    v.gcnt = gh ? 1u : 0u;
+    v.greset = (gh || null) ? 1u : 0u;
+    v.n_next = (!null && cls == 0u) ? 1u : 0u;
+    v.n_del = (!null && cls == 0u && s1_sub(k.lo)) ? 1u : 0u;
+    v.n_create = (!null && cls == 1u) ? 1u : 0u;
+    v.n_x = (!null && cls == 2u) ? 1u : 0u;
+    v.fcs = (!null && cls == 1u) ? seq : kNone;
+    v.g0 = p;
+    v.c1 = (!null && cls == 1u) ? p : kNone;
+    return v;
+  }
+  __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
+    const Key128 k = a.keys[p];
+    Key128 nk = {~0ull, ~0ull};
+    if (p + 1 < a.B) nk = a.keys[p + 1];
+    const V in = combine(ex, loc);
+    const uint32_t cls = s1_class(k.lo), seq = s1_seq(k.lo), sub = (uint32_t)s1_sub(k.lo);
+    const bool null = cls == 3u;
+    const bool head = loc.gcnt != 0u;
+    const bool last = !null && (p + 1 == a.B || !same_group(k, nk));
+    const uint32_t before = loc.preset ? 0u : ex.gcnt;
+    const uint32_t kslot = head ? before : before - 1u;
+    if (head && kslot >= a.cm) atomicOr(&a.scal->error, 1u);
+    const uint32_t kk = min(kslot, a.cm - 1u);
+    const uint32_t q = part(a, k);
+    const uint32_t rank = (!null && cls == 1u && in.c1 != kNone) ? p - in.c1 : 0u;
+    a.mpos[p] = make_uint4(seq | (head ? kMPosHead : 0u) | (last ? kMPosLast : 0u) |
+                               (null ? kMPosNull : 0u) | (cls << 23) | (sub << 25),
+                           null ? kNone : q * a.cm + kk, q, rank);
+    const OpState& os = a.ops[seq];
+    const uint64_t glo = s1_group(k.lo);
+    uint4 rec[8];
+    rec[0] = make_uint4(a.stamp, in.n_next, in.n_del, in.n_create);
+    rec[1] = make_uint4(in.n_x, in.fcs, in.g0, in.c1);
+    rec[2] = make_uint4((uint32_t)k.hi, (uint32_t)(k.hi >> 32), (uint32_t)glo, (uint32_t)(glo >> 32));
+    rec[3] = make_uint4(os.x[0], os.x[1], os.x[2], os.x[3]);
+    rec[4] = make_uint4(os.x[4], os.x[5], os.x[6], os.x[7]);
+    rec[5] = rec[6] = rec[7] = make_uint4(0, 0, 0, 0);
+    const uint64_t idx = last ? (uint64_t)q * a.cm + kk : (uint64_t)a.Q * a.cm + p;
+    wave_store128(stage, a.gtx, idx, rec);
+  }
+};
+
+// ------------------------------------------------------ LDS group table
+
+struct GroupM {  // 64 B
+  uint64_t hi, glo;
+  uint32_t n_del, n_create, fcs, len;
+  int32_t slot;
+  uint32_t flags, fl, n_succ, mlo, mhi;
+  uint32_t pad[2];
+};
+
+// group of (hi, glo) among g[0, ng) (sorted), or -1: a fixed-step search
+__device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint64_t hi, uint64_t glo) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t step = kGroupMax; step > 0; step >>= 1) {
+    const uint32_t c = pos + step;
+    const GroupM& G = g[min(c - 1, (uint32_t)kGroupMax)];
+    const bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
+    pos = (c <= ng && less) ? c : pos;
+  }
+  const GroupM& G = g[min(pos, (uint32_t)kGroupMax)];
+  return (pos < ng && G.hi == hi && G.glo == glo) ? (int)pos : -1;
+}
+
+// occupied rows of the partition -> groups, every side entry read (AUTH:
+// decrypted here, authenticated with its row later)
+template <bool AUTH>
+__device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uint32_t ng,
+                                      int16_t* s_sg, uint8_t* s_occb, uint32_t* s_occ,
+                                      const uint32_t* s_te) {
+  for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
+    const uint64_t row = (uint64_t)q * a.Sr + j;
+    uint4 sd = a.side[row];
+    if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
+    const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
+    const bool occ = (w1 & 1u) != 0;
+    const int k = occ ? find_group_m(g, ng, hi, w1 >> 23) : -1;
+    if (occ) atomicAdd(s_occ, 1u);
+    if (k >= 0) {
+      g[k].slot = (int32_t)j;
+      g[k].len = (uint32_t)(w1 >> 1) & 63u;
+    }
+    s_sg[j] = (int16_t)k;
+    s_occb[j] = occ ? 1 : 0;
+  }
+}
+
+// this partition's group slots: real ones (stamped by this batch) are dense
+// at the front; every descriptor line is read
+__device__ inline uint32_t load_groups(const MArgs& a, uint32_t q, GroupM* g, uint32_t* s_ng,
+                                       bool with_results) {
+  if (threadIdx.x == 0) *s_ng = 0;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < a.cm; k += 256) {
+    const uint4* r = a.gtx + ((uint64_t)q * a.cm + k) * 8;
+    const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
+    uint4 h = make_uint4(0, 0, 0, 0);
+    if (with_results) h = a.m2tx[((uint64_t)q * a.cm + k) * kVLineU4];
+    GroupM G;
+    G.hi = u4lo(r2);
+    G.glo = u4hi(r2);
+    G.n_del = r0.z;
+    G.n_create = r0.w;
+    G.fcs = r1.y;
+    G.len = 0;
+    G.slot = -1;
+    G.flags = 0;
+    G.fl = 0;
+    G.n_succ = h.y;
+    G.mlo = h.z;
+    G.mhi = h.w;
+    G.pad[0] = G.pad[1] = 0;
+    g[k] = G;
+    if (r0.x == a.stamp) atomicAdd(s_ng, 1u);
+  }
+  __syncthreads();
+  return *s_ng;
+}
+
+// --------------------------------------------------------------- k_m1x
+
+// mailbox read pass: snapshot of every group's row, with the verdict header
+// lane 0 = {len, fl (length after the pops), flags (1 exists after the
+// pops, 2 admitted as a new mailbox), row}; lanes 2.. = the 62 ids
+template <bool AUTH>
+__global__ __launch_bounds__(256) void k_m1x(MArgs a) {
+  __shared__ GroupM g[kGroupMax + 1];
+  __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint8_t s_occb[kSrMax];
+  __shared__ uint32_t s_ng, s_occ, s_empt;
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t q = blockIdx.x;
+  if (a.scal->error) return;
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
+  const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4 va[kMU], vb[kMU];
+  load_rows(va, part, wave * kMU, a.Sr);
+  const uint32_t ng = load_groups(a, q, g, &s_ng, false);
+  if (tid == 0) {
+    s_occ = 0;
+    s_empt = 0;
+  }
+  __syncthreads();
+  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  __syncthreads();
+  // admission (grapevine.proto:74): rows that empty after the pops are free
+  // again; new recipients are admitted by the seq of their first create
+  for (uint32_t k = tid; k < a.cm; k += 256) {
+    const GroupM& G = g[k];
+    if (k < ng && G.slot >= 0 && G.len == min(G.n_del, G.len)) atomicAdd(&s_empt, 1u);
+  }
+  __syncthreads();
+  const uint32_t freeq = (a.Sr - s_occ) + s_empt;
+  for (uint32_t k = tid; k < a.cm; k += 256) {
+    GroupM& G = g[k];
+    const bool real = k < ng;
+    const uint32_t len1 = (real && G.slot >= 0) ? G.len - min(G.n_del, G.len) : 0u;
+    const bool exists1 = len1 > 0;
+    const bool isnew = real && !exists1 && G.n_create > 0;
+    uint32_t rank = 0;
+    for (uint32_t k2 = 0; k2 < a.cm; ++k2) {  // every slot: fixed work
+      const GroupM& H = g[k2];
+      const uint32_t hl = (k2 < ng && H.slot >= 0) ? H.len - min(H.n_del, H.len) : 0u;
+      rank += (k2 < ng && hl == 0 && H.n_create > 0 && H.fcs < G.fcs) ? 1u : 0u;
+    }
+    G.fl = len1;
+    G.flags = (exists1 ? 1u : 0u) | ((isnew && rank < freeq) ? 2u : 0u);
+  }
+  __syncthreads();
+  uint4* snap = a.msnap + (uint64_t)q * a.cm * 64;
+  uint4* dry = a.mdry + (uint64_t)q * 64;
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+    if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
+    uint4 v[kMU];
+    uint32_t mm = 0;
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) {
+      v[u] = va[u];
+      keep4(v[u]);  // every row is read, used or not
+      mm |= (j0 + u < a.Sr && s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
+    }
+    if (AUTH) m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    bool dry_run = j0 == 0;  // wave 0's first chunk runs the loop once dry
+    while (mm || dry_run) {
+      const uint32_t bit = dry_run ? 0u : (mm & (0u - mm));
+      if (!dry_run) mm &= mm - 1u;
+      uint4 cur = v[0];
+#pragma unroll
+      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+      const int k = dry_run ? 0 : s_sg[j0 + u0];
+      const GroupM& G = g[k];
+      const uint4 hdr = make_uint4(G.len, G.fl, G.flags, (uint32_t)G.slot);
+      cur = sel4(lane == 0, hdr, sel4(lane == 1, make_uint4(0, 0, 0, 0), cur));
+      uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
+      st_row<true>(&dst[lane], cur);
+      dry_run = false;
+    }
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) va[u] = vb[u];
+  }
+  // slots without a row (new recipients, misses, unused slots): header only;
+  // wave 0 also runs once dry, so every slot of MSNAP is written exactly once
+  for (uint32_t k = wave; k <= a.cm; k += 4) {
+    const bool dry_run = k == a.cm;
+    const GroupM& G = g[min(k, a.cm - 1u)];
+    const bool has_row = !dry_run && k < ng && G.slot >= 0;
+    if (has_row) continue;
+    const bool real = !dry_run && k < ng;
+    const uint4 hdr = sel4(real, make_uint4(0u, G.fl, G.flags, (uint32_t)G.slot), make_uint4(0, 0, 0, 0));
+    uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
+    st_row<true>(&dst[lane], sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
+  }
+}
+
+// -------------------------------------------------------------- k_m1r
+// copy-forward of the group snapshot; F = {reset, next-deletes, creates, 0}
+
+struct M1rArgs {
+  GVS_VSCAN_FIELDS
+  const uint4* mpos;
+  const OpState* ops;
+  const uint4* msnap;
+  const uint4* mdummy;  // B x 1 KiB
+  M1Out* m1out;
+  uint64_t N;
+  KeyCtx kc;
+};
+
+struct M1rOp {
+  using Args = M1rArgs;
+  static constexpr bool kSelect = true;
+  __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
+  __device__ static uint4 f_combine(uint4 a, uint4 b) {
+    return sel4(b.x != 0u, b, make_uint4(a.x, a.y + b.y, a.z + b.z, 0u));
+  }
+  __device__ static bool takes_b(uint4, uint4 b) { return b.x != 0u; }
+  __device__ static uint4 v_combine(uint4, uint4 va, uint4 fb, uint4 vb) { return sel4(fb.x != 0u, vb, va); }
+  __device__ static uint4 f_of_pos(uint32_t x) {
+    const bool null = x & kMPosNull, head = x & kMPosHead;
+    const uint32_t cls = mpos_cls(x);
+    return make_uint4((head || null) ? 1u : 0u, (!null && cls == 0u && mpos_sub(x)) ? 1u : 0u,
+                      (!null && cls == 1u) ? 1u : 0u, 0u);
+  }
+  __device__ static uint4 f_of(const Args& a, uint32_t p) { return f_of_pos(uni4(a.mpos[p]).x); }
+  __device__ static const uint4* src_of(const Args& a, uint32_t p, uint4 mp) {
+    return (mp.x & kMPosHead) ? a.msnap + (uint64_t)mp.y * 64 : a.mdummy + (uint64_t)p * 64;
+  }
+  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4) {
+    const uint4 mp = uni4(a.mpos[p]);
+    return ld_row<false>(&src_of(a, p, mp)[lane_id()]);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  if (a.scal->error) return;
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint4 cf, cv;
+  vscan_carry_in<M1rOp>(a, s_v, s_f, cf, cv);
+  const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t p = p0 + j;
+    const uint4 mp = uni4(a.mpos[p]);
+    const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
+    const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;
+    const uint4 A = ld_row<false>(&M1rOp::src_of(a, p, mp)[lane]);
+    const OpState& os = a.ops[seq];
+    const uint4 myid = make_uint4(os.id[0], os.id[1], os.id[2], os.id[3]);
+    const uint4 pf = sel4(head, make_uint4(1u, 0u, 0u, 0u), cf);
+    const uint4 pv = sel4(head, A, cv);
+    const uint4 hdr = uni4(shfl4(pv, 0));
+    const uint32_t len = hdr.x, fl = hdr.y, gflags = hdr.z;
+    // next-message op: the one with d delete-nexts before it reads id d
+    const uint32_t d = pf.y;
+    const uint4 idv = shfl4(pv, 2 + (int)min(d, 61u));
+    const uint32_t dec = id_decode(a.kc, u4lo(idv), u4hi(idv), a.N);  // every op: fixed work
+    const bool found = !null && d < len;
+    // create: rank r among the group's creates (grapevine.proto:73-75)
+    const uint32_t r = pf.z;
+    const bool exists1 = gflags & 1u, admitted = gflags & 2u;
+    const bool cok = exists1 ? (fl + r < GVS_MAILBOX_SLOTS) : (admitted && r < GVS_MAILBOX_SLOTS);
+    // by-id delete: the position of its id in the mailbox (for the write pass)
+    const uint64_t hit = __ballot(lane >= 2 && lane < 2 + len && eq4(pv, myid));
+    const uint32_t pos = hit ? (uint32_t)__builtin_ctzll(hit) - 2u : 63u;
+    uint32_t status = kPending, slot = kNone, flags = 0, opos = 63u;
+    uint4 oid = make_uint4(0, 0, 0, 0);
+    if (!null && cls == 0u) {
+      status = found ? kPending : 2u;
+      slot = found ? dec : kNone;
+      flags = (found && mpos_sub(mp.x)) ? CF_POP : 0u;
+      oid = sel4(found, idv, oid);
+    } else if (!null && cls == 1u) {
+      status = cok ? kPending : ((exists1 || admitted) ? 5u : 6u);
+      flags = cok ? CF_MBOX_OK : 0u;
+    } else if (!null) {
+      opos = pos;
+    }
+    uint4* o = reinterpret_cast<uint4*>(a.m1out) + (uint64_t)seq * 8;
+    if (lane < 8)
+      o[lane] = sel4(lane == 0, make_uint4(status, slot, flags, opos), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0)));
+    const uint4 e = M1rOp::f_of_pos(mp.x);
+    cv = M1rOp::v_combine(cf, cv, e, A);
+    cf = M1rOp::f_combine(cf, e);
+  }
+}
+
+// -------------------------------------------------------------- k_m2r
+// per group: the new ids of its successful creates at lane 2 + rank and the
+// mailbox positions its successful by-id deletes remove.  F = {reset, mask lo,
+// mask hi, creates}; values merge lane-wise (ids are never zero).
+
+struct M2rArgs {
+  GVS_VSCAN_FIELDS
+  const uint4* mpos;
+  const OpState* ops;
+  const ROp* rop;
+  const RRes* rres;
+  const M1Out* m1out;
+  uint4* m2tx;  // (Q*cm + B) x 1152 B
+  uint32_t Q, cm, stamp;
+};
+
+struct M2rOp {
+  using Args = M2rArgs;
+  static constexpr bool kSelect = false;
+  __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
+  __device__ static uint4 f_combine(uint4 a, uint4 b) {
+    return sel4(b.x != 0u, b, make_uint4(a.x, a.y | b.y, a.z | b.z, a.w + b.w));
+  }
+  __device__ static bool takes_b(uint4, uint4 b) { return b.x != 0u; }
+  __device__ static uint4 v_combine(uint4, uint4 va, uint4 fb, uint4 vb) {
+    return sel4(fb.x != 0u || nz4(vb), vb, va);
+  }
+  __device__ static uint4 f_of(const Args& a, uint32_t p) {
+    const uint4 mp = uni4(a.mpos[p]);
+    const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
+    const bool null = mp.x & kMPosNull, head = mp.x & kMPosHead;
+    const bool succ = __builtin_amdgcn_readfirstlane(a.rres[seq].status) == 1u;
+    const uint32_t pos = __builtin_amdgcn_readfirstlane(a.m1out[seq].pad);
+    const bool del = !null && cls == 2u && succ && pos < GVS_MAILBOX_SLOTS;
+    return make_uint4((head || null) ? 1u : 0u, (del && pos < 32u) ? 1u << pos : 0u,
+                      (del && pos >= 32u) ? 1u << (pos - 32u) : 0u, (!null && cls == 1u && succ) ? 1u : 0u);
+  }
+  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 e) {
+    const uint4 mp = uni4(a.mpos[p]);
+    const uint32_t seq = mp.x & kSeqMask;
+    const ROp& r = a.rop[seq];
+    const uint4 id = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    return sel4(e.w != 0u && lane_id() == 2u + mp.w && mp.w < GVS_MAILBOX_SLOTS, id, make_uint4(0, 0, 0, 0));
+  }
+};
+
+__global__ __launch_bounds__(256) void k_m2r_c(M2rArgs a) {
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  if (a.scal->error) return;
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint4 cf, cv;
+  vscan_carry_in<M2rOp>(a, s_v, s_f, cf, cv);
+  const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t p = p0 + j;
+    const uint4 mp = uni4(a.mpos[p]);
+    const uint32_t seq = mp.x & kSeqMask;
+    const bool last = (mp.x & kMPosLast) && !(mp.x & kMPosNull);
+    const uint4 e = M2rOp::f_of(a, p);
+    cv = M2rOp::v_combine(cf, cv, e, M2rOp::value_of(a, p, e));
+    cf = M2rOp::f_combine(cf, e);
+    // the group's last op writes its result slot, every other op a dummy
+    const OpState& os = a.ops[seq];
+    const uint4 x0 = make_uint4(os.x[0], os.x[1], os.x[2], os.x[3]);
+    const uint4 x1 = make_uint4(os.x[4], os.x[5], os.x[6], os.x[7]);
+    uint4* o = a.m2tx + (last ? (uint64_t)mp.y : (uint64_t)a.Q * a.cm + p) * kVLineU4;
+    // value: lanes 0..1 the recipient key (a new mailbox's first 32 B), lanes
+    // 2.. the appended ids; header: stamp, creates, removal mask
+    o[8 + lane] = sel4(lane == 0, x0, sel4(lane == 1, x1, cv));
+    if (lane < 8) o[lane] = sel4(lane == 0, make_uint4(a.stamp, cf.w, cf.y, cf.z), make_uint4(0, 0, 0, 0));
+  }
+}
+
+// --------------------------------------------------------------- k_m2x
+
+// new state of a mailbox row: matched rows drop their first dp ids and the
+// ids at the positions of `mask`, then take the appended ids; a row placed
+// for a new recipient takes the recipient key and the appended ids
+__device__ inline uint4 m2_row(uint4 v, bool matched, uint32_t len, uint32_t dp, uint64_t mask,
+                               uint32_t n_succ, uint4 app, uint4* wst, uint32_t* fl_out) {
+  const uint32_t lane = lane_id();
+  const uint32_t i = lane - 2u;
+  const bool keep = matched && lane >= 2 && i < len && i >= dp && !((mask >> i) & 1ull);
+  const uint64_t km = __ballot(keep);
+  const uint32_t nk = (uint32_t)__popcll(km);
+  if (keep) wst[mbcnt64(km)] = v;  // compaction through the wave's LDS stage
+  wave_lds_sync();
+  const uint32_t r = lane - 2u;
+  uint4 out = make_uint4(0, 0, 0, 0);
+  if (lane >= 2 && r < nk) out = wst[min(r, 63u)];
+  const uint32_t ra = lane - 2u - nk;  // appended ids follow the survivors
+  const uint4 a = shfl4(app, (int)(2u + min(ra, 61u)));
+  if (lane >= 2 + nk && ra < n_succ && lane < 64) out = a;
+  wave_lds_sync();
+  const uint32_t fl = nk + min(n_succ, GVS_MAILBOX_SLOTS - nk);
+  out = sel4(lane < 2, sel4(matched, v, app), out);  // recipient key
+  *fl_out = fl;
+  return sel4(fl != 0u, out, make_uint4(0, 0, 0, 0));
+}
+
+template <bool AUTH>
+__global__ __launch_bounds__(256) void k_m2x(MArgs a) {
+  __shared__ GroupM g[kGroupMax + 1];
+  __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint8_t s_occb[kSrMax];
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
+  __shared__ uint4 s_wst[AUTH ? 1 : 4][64];  // AUTH: the seal stage doubles as it
+  __shared__ int16_t s_place[kSrMax];
+  __shared__ uint8_t s_flag[kSrMax];
+  __shared__ uint16_t s_pfx[kSrMax + 1];
+  __shared__ uint16_t s_gpfx[kGroupMax + 1];
+  __shared__ uint8_t s_gflag[kGroupMax + 1];
+  __shared__ int16_t s_pend[kGroupMax];
+  __shared__ uint8_t s_ld[kGroupMax];
+  __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t q = blockIdx.x;
+  if (a.scal->error) return;
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
+  uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4* side = a.side + (uint64_t)q * a.Sr;
+  uint4 va[kMU], vb[kMU];
+  load_rows(va, part, wave * kMU, a.Sr);
+  const uint32_t ng = load_groups(a, q, g, &s_ng, true);
+  if (tid == 0) {
+    s_occ = 0;
+    s_delta = 0;
+  }
+  __syncthreads();
+  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  __syncthreads();
+  // final lengths; pending = groups with no row that end non-empty
+  for (uint32_t k = tid; k < a.cm; k += 256) {
+    GroupM& G = g[k];
+    const bool real = k < ng;
+    const uint32_t len = (real && G.slot >= 0) ? G.len : 0u;
+    const uint32_t dp = min(G.n_del, len);
+    const uint64_t lenmask = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
+    const uint64_t mask = (((uint64_t)G.mhi << 32) | G.mlo) & lenmask & ~((1ull << dp) - 1ull);
+    const uint32_t nk = len - dp - (uint32_t)__popcll(mask);
+    G.fl = real ? nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk) : 0u;
+    s_gflag[k] = (real && G.slot < 0 && G.fl > 0) ? 1 : 0;
+    s_ld[k] = 0;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j];
+    const bool occ = s_occb[j] != 0;
+    s_flag[j] = (!occ || (k >= 0 && g[k].fl == 0)) ? 1 : 0;
+  }
+  __syncthreads();
+  block_flag_scan(s_flag, a.Sr, s_pfx, s_w);
+  block_flag_scan(s_gflag, a.cm, s_gpfx, s_w);
+  for (uint32_t k = tid; k < a.cm; k += 256)
+    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t npend = s_gpfx[a.cm];
+  if (tid == 0 && npend > s_pfx[a.Sr]) atomicOr(&a.scal->error, 2u);
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    int16_t pl = -1;
+    if (s_flag[j] && s_pfx[j] < npend) pl = s_pend[s_pfx[j]];
+    s_place[j] = pl;
+    const int k = s_sg[j];
+    if (k >= 0 && g[k].fl == 0) atomicSub(&s_delta, 1u);
+  }
+  if (tid == 0) atomicAdd(&s_delta, npend);
+  __syncthreads();
+  const uint4* res = a.m2tx + (uint64_t)q * a.cm * kVLineU4;
+  const uint4* dry = a.mdry + (uint64_t)q * 64;
+  uint4* wst = AUTH ? st : s_wst[AUTH ? 0 : wave];
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+    if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
+    uint4 v[kMU], sd[kMU];
+    uint32_t mm = 0;
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) {
+      const bool in = j0 + u < a.Sr;  // wave-uniform
+      v[u] = va[u];
+      sd[u] = in ? side[j0 + u] : make_uint4(0, 0, 0, 0);
+      mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
+    }
+    if (AUTH) {
+      m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
+      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
+      uint4 mine = make_uint4(0, 0, 0, 0);
+      if (lane < (uint32_t)kMU)
+        mine = xor4(st[kMU * 4 * kSegU4 + lane], side_keystream(a.sc, s_te, r0 + lane, a.sc.epoch));
+#pragma unroll
+      for (int u = 0; u < kMU; ++u) sd[u] = shfl4(mine, u);
+    }
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    bool dry_run = j0 == 0;
+    while (mm || dry_run) {
+      const uint32_t bit = dry_run ? 0u : (mm & (0u - mm));
+      if (!dry_run) mm &= mm - 1u;
+      uint4 cur = v[0];
+#pragma unroll
+      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+      const uint32_t j = j0 + ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u);
+      const int k = dry_run ? -1 : s_sg[j], pl = dry_run ? -1 : s_place[j];
+      // the slot whose result this row takes: a new recipient placed in it,
+      // else the row's own group
+      const int ge = pl >= 0 ? pl : k;
+      const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
+      const uint4* rs = dry_run ? dry : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
+      const uint4 app = ld_row<true>(&rs[lane]);
+      if (!dry_run && lane == 0) s_ld[ge] = 1;
+      const bool matched = pl < 0;
+      const uint32_t len = matched ? G.len : 0u;
+      const uint32_t dp = min(G.n_del, len);
+      const uint64_t mask = ((uint64_t)G.mhi << 32) | G.mlo;
+      uint32_t fl;
+      const uint4 nv = m2_row(cur, matched, len, dp, mask, G.n_succ, app, wst, &fl);
+      const uint64_t w1 = (G.glo << 23) | ((uint64_t)fl << 1) | 1ull;
+        const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                                                (uint32_t)(w1 >> 32)),
+                             make_uint4(0, 0, 0, 0));
+      if (!dry_run) {
+#pragma unroll
+        for (int uu = 0; uu < kMU; ++uu) {
+          v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
+          sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
+        }
+      }
+      dry_run = false;
+    }
+    if (AUTH) {
+      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
+      const uint32_t ep = a.sc.epoch + 1u;
+      uint4 mine = sd[0];
+#pragma unroll
+      for (int u = 1; u < kMU; ++u) mine = sel4(lane == (uint32_t)u, sd[u], mine);
+      if (lane < (uint32_t)kMU) {
+        const uint4 ct = xor4(mine, side_keystream(a.sc, s_te, r0 + lane, ep));
+        st[kMU * 4 * kSegU4 + lane] = ct;
+        side[j0 + lane] = ct;
+      }
+      wave_seal<kMU>(a.sc, s_te, 1u, r0, ep, v, a.btag, true, st);
+    }
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) {
+      if (j0 + u < a.Sr) {
+        st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
+        if (!AUTH && lane == 0) side[j0 + u] = sd[u];
+      }
+      va[u] = vb[u];
+    }
+  }
+  __syncthreads();
+  // result slots no row took: every slot of M2TX is read once
+  for (uint32_t k = wave; k < a.cm; k += 4) {
+    if (s_ld[k]) continue;
+    uint4 x = ld_row<true>(&res[(uint64_t)k * kVLineU4 + 8 + lane]);
+    keep4(x);
+  }
+  if (tid == 0 && s_delta)
+    atomicAdd((unsigned long long*)&a.scal->n_mailboxes, (unsigned long long)(int64_t)(int32_t)s_delta);
+}
+
+}  // namespace gvs

@@ -574,15 +574,27 @@ __device__ inline void vrec_store(uint4* rec, uint4 f, uint4 v) {
   if (lane < 8) rec[lane] = lane == 0 ? f : make_uint4(0, 0, 0, 0);
 }
 
+// Select scans (Op::kSelect): the block value is the value of one op, read
+// once.  Merge scans (values synthesized from small per-op data, combined
+// lane-wise by Op::v_combine): the block walks all of its ops.
 template <class Op>
 __global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
   if (a.scal->error) return;
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= a.nvb) return;
-  uint4 f;
-  uint32_t d;
-  f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
-  const uint4 v = Op::value_of(a, b * kVBlk + d, f);
+  uint4 f, v = make_uint4(0, 0, 0, 0);
+  if (Op::kSelect) {
+    uint32_t d;
+    f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
+    v = Op::value_of(a, b * kVBlk + d, f);
+  } else {
+    f = Op::f_identity();
+    for (uint32_t j = 0; j < kVBlk; ++j) {
+      const uint4 e = Op::f_of(a, b * kVBlk + j);
+      v = Op::v_combine(f, v, e, Op::value_of(a, b * kVBlk + j, e));
+      f = Op::f_combine(f, e);
+    }
+  }
   vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, v);
 }
 
@@ -605,7 +617,7 @@ __device__ inline void vwalk_records(const uint4* rec, uint32_t lo, uint32_t hi,
       if (i0 + u < hi) {
         if (out) vrec_store(out + (uint64_t)(i0 + u) * kVLineU4, f, v);
         const uint4 e = uni4(rf[u]);
-        v = sel4(Op::takes_b(f, e), rv[u], v);
+        v = Op::v_combine(f, v, e, rv[u]);
         f = Op::f_combine(f, e);
       }
     }
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(256) void k_vscan_b1(typename Op::Args a) {
     uint4 g = Op::f_identity(), gv = make_uint4(0, 0, 0, 0);
     for (int k = 0; k < 4; ++k) {
       const uint4 e = s_f[k];
-      gv = sel4(Op::takes_b(g, e), s_v[k][lane], gv);
+      gv = Op::v_combine(g, gv, e, s_v[k][lane]);
       g = Op::f_combine(g, e);
     }
     vrec_store(a.vagg2 + (uint64_t)blockIdx.x * kVLineU4, g, gv);
@@ -658,7 +670,7 @@ __global__ __launch_bounds__(256) void k_vscan_b3(typename Op::Args a) {
   uint4 cf = uni4(c[0]), cv = c[8 + lane];
   for (uint32_t k = 0; k < wave; ++k) {
     const uint4 e = s_f[k];
-    cv = sel4(Op::takes_b(cf, e), s_v[k][lane], cv);
+    cv = Op::v_combine(cf, cv, e, s_v[k][lane]);
     cf = Op::f_combine(cf, e);
   }
   vwalk_records<Op>(a.vagg, lo, hi, cf, cv, a.vcarry);
@@ -672,10 +684,20 @@ __device__ inline void vscan_carry_in(const typename Op::Args& a, uint4 (*s_v)[6
                                       uint4& cf, uint4& cv) {
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x, p0 = b * kVBlk + wave * 16;
-  uint4 f;
-  uint32_t d;
-  f_walk<Op>(a, p0, 16, f, d);
-  s_v[wave][lane] = Op::value_of(a, p0 + d, f);
+  uint4 f, v = make_uint4(0, 0, 0, 0);
+  if (Op::kSelect) {
+    uint32_t d;
+    f_walk<Op>(a, p0, 16, f, d);
+    v = Op::value_of(a, p0 + d, f);
+  } else {
+    f = Op::f_identity();
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint4 e = Op::f_of(a, p0 + j);
+      v = Op::v_combine(f, v, e, Op::value_of(a, p0 + j, e));
+      f = Op::f_combine(f, e);
+    }
+  }
+  s_v[wave][lane] = v;
   if (lane == 0) s_f[wave] = f;
   __syncthreads();
   const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
@@ -683,7 +705,7 @@ __device__ inline void vscan_carry_in(const typename Op::Args& a, uint4 (*s_v)[6
   cv = c[8 + lane];
   for (uint32_t k = 0; k < wave; ++k) {
     const uint4 e = s_f[k];
-    cv = sel4(Op::takes_b(cf, e), s_v[k][lane], cv);
+    cv = Op::v_combine(cf, cv, e, s_v[k][lane]);
     cf = Op::f_combine(cf, e);
   }
 }
@@ -738,7 +760,11 @@ struct Rr2Op {
     r = sel4(a.y != 0u, a, r);
     return sel4(b.x != 0u, b, r);
   }
+  static constexpr bool kSelect = true;
   __device__ static bool takes_b(uint4 a, uint4 b) { return b.x || (!a.y && (b.y || b.z)); }
+  __device__ static uint4 v_combine(uint4 fa, uint4 va, uint4 fb, uint4 vb) {
+    return sel4(takes_b(fa, fb), vb, va);
+  }
   __device__ static uint4 f_of_hdr(const RsHdr& h) {
     const uint32_t sk = rs_setkind(h.flags);
     uint4 e = make_uint4((h.flags & (kRsHead | kRsNull)) ? 1u : 0u, 0u, 0u, 0u);
