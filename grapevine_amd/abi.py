@@ -97,6 +97,11 @@ ERR_INTEGRITY = -7     # GVS_ERR_INTEGRITY
 
 # gvs_dump_raw / gvs_store_raw regions
 RAW_MESSAGES, RAW_MAILBOXES, RAW_SIDE, RAW_MSG_TAGS, RAW_MBOX_TAGS = range(5)
+# the final row states the last batch left pending (by sorted position), their
+# side entries and tags, and that batch's slot descriptors (include/gvstore_test.h)
+RAW_PENDING, RAW_PENDING_SIDE, RAW_PENDING_TAGS, RAW_SLOTS = range(5, 9)
+# header table field of a message row whose final state is pending in P
+TABLE_PENDING_STATE, TABLE_PENDING_ROW = 2, 0x100
 
 
 def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,

@@ -107,8 +107,11 @@ struct Engine {
   uint4* rpos = nullptr;     // B sorted-position records
   uint4* rsb = nullptr;      // B x 128 B
   uint4* snap = nullptr;     // W*c x 1 KiB
-  uint4* pbuf = nullptr;     // W*c x 1 KiB
-  uint4* snapdummy = nullptr, *pdummy = nullptr;  // B x 1 KiB
+  uint4* pbuf = nullptr;     // B x 1 KiB final row states, by sorted position
+  uint4* psd = nullptr;      // B side entries of P (target row, valid)
+  uint4* ptag = nullptr;     // B tags of P (authenticated storage)
+  uint4* pdum = nullptr;     // W*c x 1 KiB read for unused slots
+  uint4* snapdummy = nullptr;  // B x 1 KiB
   uint4* dryb = nullptr;     // W x 1 KiB
   RtxV* rtx_agg = nullptr;
   RtxV* rtx_carry = nullptr;
@@ -162,7 +165,7 @@ struct gvs_handle {
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
   int rpass_variant = 6;
-  int pipeline = 1;          // 1: per-op message pass; 2: fixed-slot transactions (gvs_txn.h)
+  int pipeline = 2;          // 2: fixed-slot transactions (gvs_txn.h); 1: the per-op message pass
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   std::vector<void*> allocs;
   std::string err;
@@ -259,6 +262,7 @@ static uint32_t txn_slots(uint32_t B, uint32_t W, uint32_t S) {
   c = (c + 7) / 8 * 8;
   if (c > S) c = S;
   if (c > B) c = B;
+  if (c > kSlotMax) c = kSlotMax;
   return (uint32_t)c;
 }
 
@@ -445,9 +449,11 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(rpos, B);
     A(rsb, (uint64_t)B * 8);
     A(snap, WC * 64);
-    A(pbuf, WC * 64);
+    A(pbuf, (uint64_t)B * 64);
+    A(psd, B);
+    if (h->auth) A(ptag, B);
+    A(pdum, WC * 64);
     A(snapdummy, (uint64_t)B * 64);
-    A(pdummy, (uint64_t)B * 64);
     A(dryb, (uint64_t)e.W * 64);
     A(rtx_agg, B / kScanT);
     A(rtx_carry, B / kScanT);
@@ -825,6 +831,10 @@ static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
   hipLaunchKernelGGL(k_vscan_b3<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
 }
 
+static PsealArgs pargs(const gvs_handle* h, const Engine& e, uint32_t ep) {
+  return PsealArgs{e.pbuf, e.psd, e.ptag, seal_of(h, e), h->te, e.scal, ep};
+}
+
 // Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
 // sort and the transaction slots (k_rtx), so that every fixed-capacity check
 // (mailbox groups, transaction slots) is decided before any state changes.
@@ -905,6 +915,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.stamp_cur = e.stamp_run;
     a.stamp_prev = e.stamp_prev;
     a.pbuf = e.pbuf;
+    a.psd = e.psd;
+    a.pdum = e.pdum;
     a.snap = e.snap;
     a.dry = e.dryb;
     a.scal = e.scal;
@@ -919,12 +931,22 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.cutoff = h->cutoff;
     a.xbuf = e.X ? e.xb2[e.par] : nullptr;
     a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
-    hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+    if (h->auth) {
+      a.sc = seal_of(h, e);
+      a.te = h->te;
+      a.mtag = e.mtag;
+      // the previous batch's P (sealed at this epoch) is unsealed in place first
+      if (e.stamp_prev != kNone)
+        hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
+      hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+    }
   }
   mark(h, "rpass");
   {
     Rr1Args a{e.rpos, e.rop, e.img, e.snap, e.snapdummy, e.rsb, e.rr1_agg, e.rr1_carry, e.scal,
-              B,      B / kScanT, B - e.X};
+              B,      B / kScanT, B - e.X, e.S};
     hipLaunchKernelGGL(k_scan_a<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_b<Rr1Op>, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_c<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
@@ -938,7 +960,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.snap = e.snap;
     a.snapdummy = e.snapdummy;
     a.pbuf = e.pbuf;
-    a.pdummy = e.pdummy;
+    a.psd = e.psd;
     a.resp = e.resp;
     a.rres = e.rres;
     a.B = B;
@@ -946,6 +968,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     vscan_abc<Rr2Op>(s, a);
     hipLaunchKernelGGL(k_rr2_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
+  if (h->auth)  // P at the epoch the pass wrote the rows at
+    hipLaunchKernelGGL(k_pseal<true>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch + 1));
   mark(h, "rr2");
   {
     PostArgs a{e.kinds, e.rres, e.rop, e.dflag, e.dslot, e.bsum2, e.ring, e.scal, B, nblk,
@@ -1291,7 +1315,6 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   }
   if (std::strcmp(key, "pipeline") == 0 && (value == 1 || value == 2)) {
     // only between batches of a fresh store: the two keep different pending state
-    if (value == 2 && h->auth) return GVS_ERR_INVALID_ARG;
     for (auto& e : h->eng)
       if (e.epoch != 0) return GVS_ERR_INVALID_ARG;
     h->pipeline = (int)value;
@@ -1320,7 +1343,8 @@ const char* gvs_last_error(gvs_handle* h) { return h ? h->err.c_str() : "null ha
 int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
                          const uint8_t pt[1024], const uint8_t* side_pt, uint8_t ct[1024],
                          uint8_t* side_ct, uint8_t tag[16]) {
-  if (!secret || !pt || !ct || !tag || table > 1 || (side_pt && !side_ct)) return GVS_ERR_INVALID_ARG;
+  const bool known = table <= 2 || table == kPendTable;
+  if (!secret || !pt || !ct || !tag || !known || (side_pt && !side_ct)) return GVS_ERR_INVALID_ARG;
   SealCtx sc{};
   uint32_t te0[256];
   storage_ctx(secret, sc, te0);
@@ -1341,7 +1365,7 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
   for (uint32_t i = 0; i < 4; ++i) {
     uint64_t m[32], l[2];
     for (int k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
-    leaf_prf(sc.leafk[table][i], m, l);
+    leaf_prf(sc.leafk[table & 1][i], m, l);
     t[0] ^= l[0];
     t[1] ^= l[1];
   }
@@ -1362,29 +1386,34 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
   for (const auto& e : h->eng) {
     GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
     GVS_HIP(h, hipStreamSynchronize(h->stream));
+    auto unseal = [&](uint8_t* d, uint32_t table, uint64_t row) {  // decrypt at the current epoch
+      for (uint32_t j = 0; j < 64; ++j) {
+        const uint4 k = ctr_keystream(sc.rk, te0.data(), table, row, e.epoch, j);
+        const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+        for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
+      }
+    };
+    if (h->auth)
+      for (uint64_t row = 0; row < N; ++row) unseal(phys.data() + row * 1024, 0u, row);
     if (h->pipeline == 2 && e.stamp_prev != kNone) {
-      // rows the last batch changed are pending in P (applied by the next pass)
+      // rows the last batch changed are pending in P (applied by the next pass):
+      // slot descriptor {row in partition, stamp, P position}
       const uint64_t WC = (uint64_t)e.W * e.c;
-      std::vector<uint4> td(WC * 8), pv(WC * 64);
+      std::vector<uint4> td(WC * 8);
+      std::vector<uint8_t> pv((uint64_t)e.B * 1024);
       GVS_HIP(h, hipMemcpy(td.data(), e.tbuf[e.par ^ 1], WC * 128, hipMemcpyDeviceToHost));
-      GVS_HIP(h, hipMemcpy(pv.data(), e.pbuf, WC * 1024, hipMemcpyDeviceToHost));
+      GVS_HIP(h, hipMemcpy(pv.data(), e.pbuf, pv.size(), hipMemcpyDeviceToHost));
       for (uint64_t k = 0; k < WC; ++k) {
         const uint4 d = td[k * 8];
-        if (d.y != e.stamp_prev || d.x >= e.S) continue;
-        const uint64_t row = (k / e.c) * e.S + d.x;
-        std::memcpy(phys.data() + row * 1024, &pv[k * 64], 1024);
+        if (d.y != e.stamp_prev || d.x >= e.S || d.z >= e.B) continue;
+        uint8_t* src = pv.data() + (uint64_t)d.z * 1024;
+        if (h->auth) unseal(src, 2u, d.z);
+        std::memcpy(phys.data() + ((k / e.c) * e.S + d.x) * 1024, src, 1024);
       }
     }
     for (uint64_t sl = 0; sl < N; ++sl) {
-      uint64_t row = (sl % e.W) * e.S + sl / e.W;
-      uint8_t* d = dst + sl * 1024;
-      std::memcpy(d, phys.data() + row * 1024, 1024);
-      if (h->auth)  // unseal (decrypt) at the current epoch
-        for (uint32_t j = 0; j < 64; ++j) {
-          const uint4 k = ctr_keystream(sc.rk, te0.data(), 0u, row, e.epoch, j);
-          const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-          for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
-        }
+      const uint64_t row = (sl % e.W) * e.S + sl / e.W;
+      std::memcpy(dst + sl * 1024, phys.data() + row * 1024, 1024);
     }
     dst += N * 1024;
   }
@@ -1401,9 +1430,21 @@ static int raw_region(gvs_handle* h, uint32_t shard, uint32_t region, void** bas
     case 2: *base = e.side; *size = e.R * 16; break;
     case 3: *base = e.mtag; *size = e.mtag ? e.N * 16 : 0; break;
     case 4: *base = e.btag; *size = e.btag ? e.R * 16 : 0; break;
+    // pipeline 2: the final states pending from the last batch, their side
+    // entries and tags, and that batch's slot descriptors
+    case 5: *base = e.pbuf; *size = (uint64_t)e.B * 1024; break;
+    case 6: *base = e.psd; *size = (uint64_t)e.B * 16; break;
+    case 7: *base = e.ptag; *size = e.ptag ? (uint64_t)e.B * 16 : 0; break;
+    case 8: *base = e.tbuf[e.par ^ 1]; *size = (uint64_t)e.W * e.c * 128; break;
     default: return GVS_ERR_INVALID_ARG;
   }
   return *base ? GVS_OK : GVS_ERR_INVALID_ARG;
+}
+
+int gvs_raw_size(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t* size) {
+  if (!h || !size) return GVS_ERR_INVALID_ARG;
+  void* base;
+  return raw_region(h, shard, region, &base, size);
 }
 
 int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset, void* dst,

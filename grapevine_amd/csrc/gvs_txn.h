@@ -190,14 +190,22 @@ struct RtxOp {
     const uint32_t seq = (uint32_t)a.rkeys[p] & kSeqMask;
     a.rpos[p] = make_uint4(seq | (head ? kPosHead : 0u) | (last ? kPosLast : 0u) | (null ? kPosNull : 0u),
                            null ? kNone : w * a.c + kk, w, o);
+    // the row's LAST op writes the slot descriptor: the row, the stamp, and
+    // the position whose final state (k_rr2_c) the next pass applies
     uint4 rec[8];
-    rec[0] = make_uint4(o, a.stamp, 0u, 0u);
+    rec[0] = make_uint4(o, a.stamp, p, 0u);
 #pragma unroll
     for (int i = 1; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
-    const uint64_t idx = head ? (uint64_t)w * a.c + kk : (uint64_t)a.W * a.c + p;
+    const uint64_t idx = last ? (uint64_t)w * a.c + kk : (uint64_t)a.W * a.c + p;
     wave_store128(stage, a.tbuf, idx, rec);
   }
 };
+
+// wave-uniform copy (lane 0's value in scalar registers)
+__device__ inline uint4 uni4(uint4 x) {
+  return make_uint4(__builtin_amdgcn_readfirstlane(x.x), __builtin_amdgcn_readfirstlane(x.y),
+                    __builtin_amdgcn_readfirstlane(x.z), __builtin_amdgcn_readfirstlane(x.w));
+}
 
 // --------------------------------------------------------- k_rpass2
 
@@ -206,11 +214,17 @@ struct R2Args {
   const uint4* tcur;   // this batch's slot descriptors (W*c records of 128 B)
   const uint4* tprev;  // the previous applied batch's
   uint32_t stamp_cur, stamp_prev;
-  const uint4* pbuf;   // W*c final row states of the previous batch
+  const uint4* pbuf;   // B final row states of the previous batch, by its sorted position
+  const uint4* psd;    // B: their target rows (x, y = physical row, z = valid)
+  const uint4* pdum;   // W*c x 1 KiB read for the slots no row uses
   uint4* snap;         // W*c snapshots for this batch
   uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
   Scal* scal;
   uint32_t W, S, c;
+  // authenticated storage (AUTH instantiations)
+  SealCtx sc;
+  const uint32_t* te;
+  uint4* mtag;
   // expiry sweep: on the rows as they stand before this batch
   uint32_t xon, xk, xrot, xep, xexcl;
   uint64_t cutoff;
@@ -265,17 +279,29 @@ __device__ inline uint32_t x_merge2(uint32_t xep, const uint4* s_xw, const uint3
 template <bool NTL>
 __device__ inline uint4 ld_line(const uint4* p) { return ld_row<NTL>(p); }
 
-template <int U, bool NTL, bool NTS, int MINW>
+constexpr uint32_t kSlotMax = 1024;      // transaction slots per partition (c) at most
+constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose final state is pending
+
+// Authenticated storage: a row the batch touches is sealed with the pending
+// flag in its header, so the next pass must find its final state in P (a
+// hidden P slot fails that row's tag); P rows are sealed as table 2, bound to
+// their position and, through their side entry, to the row they replace.
+template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false>
 __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
+  __shared__ uint32_t s_pp[kSlotMax];  // slot -> position of its final state in P
   __shared__ uint32_t s_np, s_ns;
   __shared__ uint4 s_xw[4 * (kXepMax + 1) * 3];
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
   __shared__ uint32_t s_xc[4], s_xt;
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(U) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(U) : 0u);
   for (uint32_t o = tid; o < a.S; o += 256) {
     s_pk[o] = -1;
     s_sk[o] = -1;
@@ -293,6 +319,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
     const uint4 ds = a.tcur[(sbase + k) * 8];
     if (dp.y == a.stamp_prev && dp.x < a.S) {
       s_pk[dp.x] = (int16_t)k;
+      s_pp[k] = dp.z;
       atomicAdd(&s_np, 1u);
     }
     if (ds.y == a.stamp_cur && ds.x < a.S) {
@@ -306,24 +333,41 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
     if (tid < a.xep) {
       const uint4 r = a.xprev[((uint64_t)w * a.xep + tid) * 8];
       const uint4 vld = a.xprev[((uint64_t)w * a.xep + tid) * 8 + 3];
-      s_xx[tid] = vld.x ? r : make_uint4(0, 0, 0, 0);
+      s_xx[tid] = sel4(vld.x != 0u, r, make_uint4(0, 0, 0, 0));
     }
     nx = a.xep;
   }
   __syncthreads();
   const uint32_t np = s_np, ns = s_ns;
-  uint4* part = a.table + (uint64_t)w * a.S * 64;
-  const uint4* pslot = a.pbuf + sbase * 64;
+  const uint64_t rowbase = (uint64_t)w * a.S;
+  uint4* part = a.table + rowbase * 64;
   uint4* sslot = a.snap + sbase * 64;
   uint4* dry = a.dry + (uint64_t)w * 64;
   const uint32_t tiles = a.S / kTile;
   for (uint32_t t = 0; t < tiles; ++t) {
     uint32_t xc = 0;
     const uint32_t rb = t * kTile + wave * 64;
+    // AUTH: the header PRF of the wave's 64 rows at both epochs, one row per
+    // lane; the pending flag comes from the slots of each batch
+    uint64_t hv[2] = {0, 0}, hs[2] = {0, 0};
+    if (AUTH) {
+      const uint64_t z[2] = {0, 0};
+      const uint32_t tv = s_pk[rb + lane] >= 0 ? kPendTable : 0u;
+      const uint32_t ts = s_sk[rb + lane] >= 0 ? kPendTable : 0u;
+      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch, tv, z, hv);
+      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch + 1u, ts, z, hs);
+    }
     for (uint32_t j = 0; j < 64; j += U) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
+      const uint64_t r0 = rowbase + rb + j;  // physical row of v[0]
+      const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
+      if (AUTH) {
+        const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
+        if (!wave_unseal<U>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
+          atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
+      }
       uint32_t mp = 0, ms = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -339,9 +383,13 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       while (mp || dry_p) {  // rows the previous batch changed: its final state
         const uint32_t bit = dry_p ? 0u : (mp & (0u - mp));
         if (!dry_p) mp &= mp - 1u;
-        const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + (uint32_t)__builtin_ctz(bit | (1u << 31))];
-        const uint4* src = dry_p ? dry : pslot + (uint64_t)k * 64;
+        const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+        const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + u0];
+        const uint32_t pos = s_pp[(uint32_t)k & (kSlotMax - 1u)];
+        const uint4* src = dry_p ? dry : a.pbuf + (uint64_t)pos * 64;
         const uint4 x = ld_row<true>(&src[lane]);
+        const uint4 sd = uni4(dry_p ? dry[0] : a.psd[pos]);
+        if (AUTH && !dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
         dry_p = false;
@@ -359,6 +407,10 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
         dry_s = false;
       }
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
+      if (AUTH) {
+        const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
+        wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }
@@ -370,9 +422,9 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       if (tid == 0) s_xt = tot;
     }
   }
-  // unused slots: every slot of P is read and every slot of SNAP written once
+  // unused slots: c reads of final states and c snapshot writes per partition
   for (uint32_t k = np + wave; k < a.c; k += 4) {
-    uint4 x = ld_row<true>(&pslot[(uint64_t)k * 64 + lane]);
+    uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
     keep4(x);
   }
   for (uint32_t k = ns + wave; k < a.c; k += 4) st_row<true>(&sslot[(uint64_t)k * 64 + lane], make_uint4(0, 0, 0, 0));
@@ -382,10 +434,61 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       const uint32_t k = lane >> 3, part8 = lane & 7;
       const bool valid = k < s_xt;
       uint4 val = make_uint4(part8 == 3 && valid ? 1u : 0u, 0, 0, 0);
-      if (part8 < 3) val = valid ? s_xp[k * 3 + part8] : make_uint4(0, 0, 0, 0);
+      if (part8 < 3) val = sel4(valid, s_xp[k * 3 + part8], make_uint4(0, 0, 0, 0));
       a.xbuf[((uint64_t)(w / a.xk) * a.xep + k) * 8 + part8] = val;
     }
   }
+}
+
+// ------------------------------------------------- P sealing (AUTH)
+//
+// P rows (final states by sorted position, B of them) are sealed as table 2
+// at the epoch the pass writes (epoch + 1), their side entry (target row,
+// valid) authenticated with them; the next batch unseals all B in place
+// before its pass.  One wave per 16 positions; every position every batch.
+
+struct PsealArgs {
+  uint4* pbuf;   // B x 1 KiB
+  uint4* psd;    // B side entries
+  uint4* ptag;   // B tags
+  SealCtx sc;
+  const uint32_t* te;
+  Scal* scal;
+  uint32_t ep;   // epoch of the P rows (seal: written; unseal: read)
+};
+
+template <bool SEAL>
+__global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
+  constexpr int U = 16;
+  GVS_TE_LDS s_te[kTeWords];
+  __shared__ uint4 s_st[4 * stage_u4(U)];
+  if (a.scal->error) return;
+  load_te(s_te, a.te);
+  __syncthreads();
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint4* st = s_st + wave * stage_u4(U);
+  const uint64_t p0 = ((uint64_t)blockIdx.x * 4 + wave) * U;
+  uint4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = ld_row<true>(&a.pbuf[(p0 + u) * 64 + lane]);
+  const uint4 ks = ctr_keystream(a.sc.rk, lds_te(s_te), 2u, p0 + (lane & 15u), a.ep, 64u);
+  const uint4 sd = a.psd[p0 + (lane & 15u)];
+  const uint4 sct = SEAL ? xor4(sd, ks) : sd;  // side ciphertext
+  if (lane < (uint32_t)U) st[U * 4 * kSegU4 + lane] = sct;
+  wave_lds_sync();
+  const uint32_t ur = (lane >> 2) % (uint32_t)U;
+  const uint4 x = st[U * 4 * kSegU4 + ur];
+  const uint64_t sdv[2] = {u4lo(x), u4hi(x)};
+  uint64_t hdr[2];
+  header_prf(a.sc.headk, p0 + ur, a.ep, 2u, sdv, hdr);
+  if (SEAL) {
+    wave_seal<U>(a.sc, s_te, 2u, p0, a.ep, v, a.ptag, true, st, hdr);
+  } else if (!wave_unseal<U>(a.sc, s_te, 2u, p0, v, a.ptag, true, st, hdr) && lane == 0) {
+    atomicOr(&a.scal->error, 8u);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) st_row<true>(&a.pbuf[(p0 + u) * 64 + lane], v[u]);
+  if (lane < (uint32_t)U) a.psd[p0 + lane] = SEAL ? sct : xor4(sd, ks);
 }
 
 // ------------------------------------------------------------- k_rr1
@@ -414,7 +517,7 @@ struct Rr1Args {
   Rr1V* agg;
   Rr1V* carry;
   const Scal* scal;
-  uint32_t B, nblk, xbase;
+  uint32_t B, nblk, xbase, S;
 };
 
 struct Rr1Op {
@@ -521,7 +624,9 @@ struct Rr1Op {
     flags |= (head ? kRsHead : 0u) | (last ? kRsLast : 0u) | (null ? kRsNull : 0u) | (setk << 8);
     uint4 rec[8];
     rec[0] = make_uint4(seq, flags, status, kind);
-    rec[1] = make_uint4(rp.y, 0u, 0u, 0u);
+    // the physical row (P side entry: the row a final state replaces)
+    const uint64_t prow = null ? 0ull : (uint64_t)rp.z * a.S + rp.w;
+    rec[1] = make_uint4(rp.y, (uint32_t)prow, (uint32_t)(prow >> 32), 0u);
 #pragma unroll
     for (int i = 0; i < 5; ++i) rec[2 + i] = ident[i];
     rec[7] = make_uint4(0, 0, 0, 0);
@@ -561,11 +666,6 @@ __device__ inline void f_walk(const typename Op::Args& a, uint32_t p0, uint32_t 
     idx = Op::takes_b(f, e) ? j : idx;
     f = Op::f_combine(f, e);
   }
-}
-
-__device__ inline uint4 uni4(uint4 x) {
-  return make_uint4(__builtin_amdgcn_readfirstlane(x.x), __builtin_amdgcn_readfirstlane(x.y),
-                    __builtin_amdgcn_readfirstlane(x.z), __builtin_amdgcn_readfirstlane(x.w));
 }
 
 __device__ inline void vrec_store(uint4* rec, uint4 f, uint4 v) {
@@ -733,8 +833,8 @@ struct Rr2Args {
   const uint4* img;
   const uint4* snap;
   const uint4* snapdummy;
-  uint4* pbuf;            // W*c final states
-  uint4* pdummy;          // B x 1 KiB
+  uint4* pbuf;            // B final states, by sorted position
+  uint4* psd;             // B: {physical row lo, hi, valid (the row's last op), 0}
   uint4* resp;            // B internal response slots (kRespSlot)
   RRes* rres;
   uint32_t B;
@@ -743,12 +843,12 @@ struct Rr2Args {
 
 // the per-position record words every lane needs (RS lines 0 and 1)
 struct RsHdr {
-  uint32_t seq, flags, status, kind, slot;
+  uint32_t seq, flags, status, kind, slot, prow_lo, prow_hi;
 };
 
 __device__ inline RsHdr rs_hdr(const uint4* rs, uint32_t p) {
   const uint4 w0 = uni4(rs[(uint64_t)p * 8]), w1 = uni4(rs[(uint64_t)p * 8 + 1]);
-  return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x};
+  return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z};
 }
 
 struct Rr2Op {
@@ -813,8 +913,9 @@ __device__ inline uint4 fail_rec(uint4 imgv, uint32_t status) {
 }
 
 // k_rr2_c: each wave walks its 16 ops in order from its carry: statuses of
-// by-id ops, every response, and the rows' final states (the row's last op
-// writes its P slot, every other op its own dummy line: fixed bytes)
+// by-id ops, every response, and the state of the row after every op into P
+// at the op's position (the next pass applies the row's last one, named by
+// the slot descriptor; the side entry says which row it replaces)
 __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   if (a.scal->error) return;
   __shared__ uint4 s_v[4][64];
@@ -823,6 +924,7 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   uint4 cf, cv;
   vscan_carry_in<Rr2Op>(a, s_v, s_f, cf, cv);
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  uint4 sd = make_uint4(0, 0, 0, 0);
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
     const RsHdr h = rs_hdr(a.rs, p);
@@ -859,9 +961,10 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
       dst[64 + lane] = t;
       reinterpret_cast<uint4*>(a.rres)[(uint64_t)h.seq * 8 + lane] = t;
     }
-    uint4* pd = (h.flags & kRsLast) ? a.pbuf + (uint64_t)h.slot * 64 : a.pdummy + (uint64_t)p * 64;
-    st_row<true>(&pd[lane], fin);
+    st_row<true>(&a.pbuf[(uint64_t)p * 64 + lane], fin);
+    sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, 0u), sd);
   }
+  if (lane < 16) a.psd[p0 + lane] = sd;
 }
 
 }  // namespace gvs

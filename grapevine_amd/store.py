@@ -28,7 +28,7 @@ EXPORTED = (
     "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
 )
-TEST_EXPORTED = ("gvs_dump_messages", "gvs_dump_raw", "gvs_store_raw")
+TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw")
 
 
 def test_hooks_enabled():
@@ -71,6 +71,7 @@ def load_library(path=None):
     lib.gvs_storage_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
     if hooks:
         lib.gvs_dump_messages.argtypes = [vp, vp, ctypes.c_uint64]
+        lib.gvs_raw_size.argtypes = [vp, u32, u32, ctypes.POINTER(u64)]
         lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
         lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
     lib.gvs_last_error.argtypes = [vp]
@@ -118,7 +119,7 @@ class ObliviousStore:
         self.h = h
         self.B = config.max_batch
         pipe = int(os.environ.get("GVS_PIPELINE", "0"))
-        if pipe and not (config.flags & abi.FLAG_AUTH_STORAGE):
+        if pipe:
             self.set_option("pipeline", pipe)
 
     def close(self):
@@ -160,6 +161,12 @@ class ObliviousStore:
         out = np.zeros(n, dtype=abi.RECORD_DTYPE)
         self._check(self.lib.gvs_dump_messages(self.h, out.ctypes.data, n * 1024))
         return out
+
+    def dump_raw_size(self, region, shard=0):
+        """Size in bytes of one shard's raw region (abi.RAW_*).  Test use."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.gvs_raw_size(self.h, shard, region, ctypes.byref(n)))
+        return n.value
 
     def dump_raw(self, region, offset, nbytes, shard=0):
         """Raw device bytes of one shard's region (abi.RAW_*): ciphertext in

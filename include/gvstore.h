@@ -220,10 +220,12 @@ int gvs_access(gvs_handle *h, const gvs_request *req, gvs_response *out);
 int gvs_get_stats(gvs_handle *h, gvs_stats *out);
 
 /* Authenticated-storage format, host-side and device-free:
- * seal one 1024-B row (and for table 1, the mailbox table, its 16-B side
- * entry; side_pt = NULL for table 0) at `epoch` under the storage keys
- * derived from `secret` (gvs_config.secret_key).  For offline verification
- * of dumps and for tests. */
+ * seal one 1024-B row (and for tables 1 and 2 its 16-B side entry; side_pt =
+ * NULL otherwise) at `epoch` under the storage keys derived from `secret`
+ * (gvs_config.secret_key).  table: 0 message row, 1 mailbox row, 2 a final
+ * row state pending from the last batch (row = its position, side = the
+ * physical row it replaces), 0x100 a message row whose final state is pending.
+ * For offline verification of dumps and for tests. */
 int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
                          const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
                          uint8_t *side_ct, uint8_t tag[16]);

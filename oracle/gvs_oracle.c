@@ -167,7 +167,7 @@ struct gvo_model {
   /* expiry sweep */
   uint32_t X, W, S, xk, xep;
   uint64_t cutoff, batches;
-  struct expiry_rec { uint8_t valid, id[16], rcpt[32]; } *xp; /* X pending deletes */
+  struct expiry_rec { uint8_t valid, id[16], rcpt[32]; } *xp, *xq; /* X pending deletes; next */
 };
 
 static int is_zero(const uint8_t *p, size_t n) {
@@ -229,7 +229,8 @@ gvo_model *gvo_create(const gvs_config *cfg) {
     m->xep = m->X >= m->W ? m->X / m->W : 1;
     m->xk = m->X >= m->W ? 1 : m->W / m->X;
     m->xp = calloc(m->X, sizeof *m->xp);
-    if (!m->xp || m->xep > 8) { /* at most 8 records per partition and batch */
+    m->xq = calloc(m->X, sizeof *m->xq);
+    if (!m->xp || !m->xq || m->xep > 8) { /* at most 8 records per partition and batch */
       gvo_destroy(m);
       return NULL;
     }
@@ -246,6 +247,7 @@ void gvo_destroy(gvo_model *m) {
   free(m->live);
   free(m->live_pos);
   free(m->xp);
+  free(m->xq);
   free(m);
 }
 
@@ -503,18 +505,28 @@ static void do_expire(gvo_model *m, const struct expiry_rec *x) {
   do_delete(m, &rq, &o);
 }
 
-/* The sweep after a batch [D]: partitions w = batches (mod xk) each record
- * their first xep messages with timestamp < cutoff, in slot order within the
+/* The sweep of batch b [D]: on the table as it stands before
+ * the batch (the engine's table pass of batch b applies batch b-1's final row
+ * states and reads every row), partitions w = b (mod xk) each record their
+ * first xep messages with timestamp < cutoff that the batch does not already
+ * delete (the records of batch b-1's sweep), in slot order within the
  * partition (slot s is in partition s mod W at offset s div W), at
- * xp[(w / xk) * xep ..]; unused entries are invalid. */
+ * xq[(w / xk) * xep ..]; unused entries are invalid.  Batch b+1 deletes them. */
+static int pending_expiry(const gvo_model *m, const uint8_t id[16]) {
+  for (uint32_t k = 0; k < m->X; ++k)
+    if (m->xp[k].valid && memcmp(m->xp[k].id, id, 16) == 0) return 1;
+  return 0;
+}
+
 static void expiry_sweep(gvo_model *m) {
-  memset(m->xp, 0, m->X * sizeof *m->xp);
+  memset(m->xq, 0, m->X * sizeof *m->xq);
   for (uint32_t w = m->batches % m->xk; w < m->W; w += m->xk) {
     uint32_t c = 0;
-    struct expiry_rec *dst = m->xp + (uint64_t)(w / m->xk) * m->xep;
+    struct expiry_rec *dst = m->xq + (uint64_t)(w / m->xk) * m->xep;
     for (uint64_t o = 0; o < m->S && c < m->xep; ++o) {
       const gvs_record *r = &m->table[o * m->W + w];
       if (is_zero(r->msg_id, 16) || !(r->timestamp < m->cutoff)) continue;
+      if (m->xk == 1 && pending_expiry(m, r->msg_id)) continue;
       dst[c].valid = 1;
       memcpy(dst[c].id, r->msg_id, 16);
       memcpy(dst[c].rcpt, r->recipient, 32);
@@ -526,6 +538,7 @@ static void expiry_sweep(gvo_model *m) {
 int gvo_process_batch(gvo_model *m, const gvs_request *reqs, uint32_t n,
                       gvs_response *out) {
   if (n > m->B - m->X) return GVS_ERR_INVALID_ARG;
+  if (m->X) expiry_sweep(m);
   for (int cls = 0; cls < 3; ++cls)
     for (uint32_t i = 0; i < n; ++i)
       if (batch_class(&reqs[i]) == cls) gvo_apply_one(m, &reqs[i], &out[i]);
@@ -533,7 +546,9 @@ int gvo_process_batch(gvo_model *m, const gvs_request *reqs, uint32_t n,
     /* the expiry deletes occupy the batch's last X slots: by-id class, after
      * every request */
     for (uint32_t k = 0; k < m->X; ++k) do_expire(m, &m->xp[k]);
-    expiry_sweep(m);
+    struct expiry_rec *t = m->xp;
+    m->xp = m->xq;
+    m->xq = t;
   }
   m->batches++;
   return GVS_OK;

@@ -226,9 +226,13 @@ static void put_le(uint8_t *p, uint64_t v, int n) {
 }
 
 /* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ L_0 ^ .. ^ L_3 with
- *   L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table), leaf i)
+ *   L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table & 1), leaf i)
  *   H   = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
  *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
+ * table: 0 message rows, 1 mailbox rows, 2 pending final states (P, by
+ * position, side = target row), 0x100 a message row whose final state is
+ * pending in P (header only: its keystream and leaves are table 0's; the CTR
+ * block carries the table's low byte). 
  * side_pt may be NULL (message rows); then side_ct is not written and 16 zero
  * bytes stand in for it. */
 void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
@@ -261,7 +265,7 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   for (uint32_t i = 0; i < 4; ++i) {
     uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'}, l[16];
     put_le(person + 8, i, 4);
-    put_le(person + 12, table, 4);
+    put_le(person + 12, table & 1, 4);
     gvo_blake2b(mk, 32, person, ct + 256 * i, 256, l, 16);
     for (int k = 0; k < 16; ++k) tag[k] ^= l[k];
   }

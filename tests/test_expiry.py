@@ -97,26 +97,32 @@ def test_only_older_messages_expire():
 
 
 def test_update_after_sweep_keeps_message():
+    """A message swept for expiry but UPDATEd before its delete runs survives;
+    only messages that were not refreshed are deleted."""
     cfg, m = model()
     fill(m, 768)
     m.set_expiry_cutoff(TS0 + 10**6)
-    empty(m)  # sweep records up to 128 messages
-    # update every live message with a fresh timestamp before the deletes run
+    empty(m)  # batch 0: the sweep records 8 messages per partition (128)
     recs = m.dump_messages()
     live = recs[recs["msg_id"].any(axis=1)]
-    reqs = np.zeros(len(live), dtype=abi.REQUEST_DTYPE)
-    reqs["msg_id"] = live["msg_id"]
-    reqs["auth_identity"] = live["sender"]
-    reqs["recipient"] = live["recipient"]
+    # refresh every other live message; the recorded deletes run after the
+    # updates in the next batch (by-id class, last slots)
+    upd = live[::2]
+    reqs = np.zeros(len(upd), dtype=abi.REQUEST_DTYPE)
+    reqs["msg_id"] = upd["msg_id"]
+    reqs["auth_identity"] = upd["sender"]
+    reqs["recipient"] = upd["recipient"]
     reqs["timestamp"] = TS0 + 2 * 10**6
     reqs["request_type"] = abi.REQUEST_TYPE_UPDATE
-    n0 = m.messages
-    out = m.process_batch(reqs[:768])
+    out = m.process_batch(reqs)
     assert (out["status_code"] == 1).all()
-    # the 128 recorded deletes ran after the updates: only unrefreshed ones died
-    refreshed = min(len(live), 768)
-    assert m.messages >= refreshed
-    assert n0 - m.messages <= 128
+    after = m.dump_messages()
+    alive = {bytes(r["msg_id"]) for r in after if r["msg_id"].any()}
+    updated = {bytes(r["msg_id"]) for r in upd}
+    gone = {bytes(r["msg_id"]) for r in live} - alive
+    assert updated <= alive                 # every refreshed message survived
+    assert gone and not (gone & updated)    # only unrefreshed ones were deleted
+    assert len(gone) <= 128
 
 
 def test_rotating_workgroups_when_X_below_W():

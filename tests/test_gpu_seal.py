@@ -59,6 +59,26 @@ def test_auth_mode_hot_recipient_and_capacity():
     assert seen[5] > 0 and seen[7] > 0, seen
 
 
+def pending_states(store, ep):
+    """The final states the last batch left pending: {physical row: (position,
+    plaintext)}, each checked against the oracle format of table 2 (a P entry,
+    bound to its position and, through its side entry, to its target row)."""
+    B = store.config.max_batch
+    P = store.dump_raw(abi.RAW_PENDING, 0, B * 1024).reshape(B, 1024)
+    side = store.dump_raw(abi.RAW_PENDING_SIDE, 0, B * 16).reshape(B, 16)
+    tags = store.dump_raw(abi.RAW_PENDING_TAGS, 0, B * 16).reshape(B, 16)
+    out = {}
+    for p in range(B):
+        pt, spt = unseal(abi.TABLE_PENDING_STATE, p, ep, P[p].tobytes(), side[p].tobytes())
+        want = ffi.seal_row(SECRET, abi.TABLE_PENDING_STATE, p, ep, pt, spt)
+        assert (P[p].tobytes(), side[p].tobytes(), tags[p].tobytes()) == want, f"P position {p}"
+        row, valid = int.from_bytes(spt[:8], "little"), spt[8] & 1
+        if valid:
+            assert row not in out, f"two final states for row {row}"
+            out[row] = (p, pt)
+    return out
+
+
 def test_stored_bytes_are_the_oracle_format():
     store, model = make_pair()
     model.seed(33)
@@ -69,14 +89,27 @@ def test_stored_bytes_are_the_oracle_format():
     want_tab = model.dump_messages()
     raw = store.dump_raw(abi.RAW_MESSAGES, 0, N * 1024).reshape(N, 1024)
     tags = store.dump_raw(abi.RAW_MSG_TAGS, 0, N * 16).reshape(N, 16)
+    pend = pending_states(store, ep)
+    assert 0 < len(pend) <= 1024
     rng = np.random.default_rng(0)
     live = [s for s in range(N) if want_tab[s]["msg_id"].any()]
-    slots = sorted(set(rng.choice(live, 24, replace=False).tolist()) | {0, N - 1})
+    slots = sorted(set(rng.choice(live, 24, replace=False).tolist()) | {0, N - 1}
+                   | {s for s in range(N) if physical_row(st, s) in pend})
+    n_pend = 0
     for s in slots:
         r = physical_row(st, s)
-        ct, _, tag = ffi.seal_row(SECRET, 0, r, ep, want_tab[s:s + 1].tobytes())
+        if r in pend:
+            # the row holds its state before the last batch, sealed as pending;
+            # its final state is the P entry
+            n_pend += 1
+            assert pend[r][1] == want_tab[s:s + 1].tobytes(), f"slot {s}: pending final state"
+            pt, _ = unseal(0, r, ep, raw[r].tobytes())
+            ct, _, tag = ffi.seal_row(SECRET, abi.TABLE_PENDING_ROW, r, ep, pt)
+        else:
+            ct, _, tag = ffi.seal_row(SECRET, 0, r, ep, want_tab[s:s + 1].tobytes())
         assert raw[r].tobytes() == ct, f"slot {s} row {r}: ciphertext differs"
         assert tags[r].tobytes() == tag, f"slot {s} row {r}: tag differs"
+    assert n_pend == len(pend)
     # mailbox rows: decrypt, re-seal with the oracle, compare bytes and tag
     R = store.config.mailbox_partitions * store.config.mailbox_partition_slots
     mb = store.dump_raw(abi.RAW_MAILBOXES, 0, R * 1024).reshape(R, 1024)
@@ -102,6 +135,9 @@ def run_one(store, model, params, n=1024):
     (abi.RAW_MAILBOXES, 9 * 1024 + 40),   # a mailbox row
     (abi.RAW_SIDE, 3 * 16 + 1),           # a mailbox side entry
     (abi.RAW_MBOX_TAGS, 200 * 16 + 15),   # a mailbox tag
+    (abi.RAW_PENDING, 300 * 1024 + 5),    # a pending final state
+    (abi.RAW_PENDING_SIDE, 17 * 16 + 2),  # its side entry (target row)
+    (abi.RAW_PENDING_TAGS, 900 * 16),     # its tag
 ])
 def test_tamper_is_detected(region, offset):
     store, model = make_pair()
@@ -162,3 +198,52 @@ def test_sharded_local_auth_parity():
         want = cl.process_batch(reqs)
         got = store.process_batch(reqs)
         assert got.tobytes() == want.tobytes(), f"batch {b}"
+
+
+def live_slot_descriptors(store):
+    """Indices of the slot descriptors of the last batch: {row, stamp, position}
+    records carrying the newest stamp."""
+    st = store.stats()
+    n = store.dump_raw_size(abi.RAW_SLOTS) // 128
+    d = store.dump_raw(abi.RAW_SLOTS, 0, n * 128).view(np.uint32).reshape(n, 32)[:, :4]
+    S = st["msg_partition_slots"]
+    stamp = int(d[:, 1].max())
+    live = np.nonzero((d[:, 1] == stamp) & (d[:, 0] < S))[0]
+    return d, live
+
+
+@pytest.mark.parametrize("word,delta", [
+    (1, 1),   # the stamp: the row's pending final state is hidden
+    (0, 1),   # the row: the final state is applied to another row
+    (2, 1),   # the position: another row's final state is applied
+])
+def test_tampered_slot_descriptor_is_detected(word, delta):
+    store, model = make_pair()
+    model.seed(38)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    d, live = live_slot_descriptors(store)
+    assert len(live) > 100
+    k = int(live[len(live) // 2])
+    rec = d[k].copy()
+    rec[word] = (int(rec[word]) + delta) % (1 << 32)
+    store.store_raw(abi.RAW_SLOTS, k * 128, rec.tobytes())
+    with pytest.raises(GvsError) as ei:
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY
+
+
+def test_replayed_pending_state_is_detected():
+    """An older P entry (same position, previous epoch) in place of the current one."""
+    store, model = make_pair()
+    model.seed(39)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    old = [store.dump_raw(r, 0, n).tobytes() for r, n in
+           ((abi.RAW_PENDING, 1024 * 1024), (abi.RAW_PENDING_SIDE, 1024 * 16), (abi.RAW_PENDING_TAGS, 1024 * 16))]
+    run_stream(store, model, params, batches=1, n=1024)
+    for r, b in zip((abi.RAW_PENDING, abi.RAW_PENDING_SIDE, abi.RAW_PENDING_TAGS), old):
+        store.store_raw(r, 0, b)
+    with pytest.raises(GvsError) as ei:
+        run_one(store, model, params)
+    assert ei.value.code == abi.ERR_INTEGRITY

@@ -35,7 +35,7 @@ def py_keys(secret):
 
 
 def counter_block(table, row, epoch, j):
-    return (row.to_bytes(8, "little") + epoch.to_bytes(4, "little") + bytes([table, 0])
+    return (row.to_bytes(8, "little") + epoch.to_bytes(4, "little") + bytes([table & 0xFF, 0])
             + j.to_bytes(2, "big"))
 
 
@@ -54,7 +54,7 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
         tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
                                              person=b"gvs-head" + bytes(8)).digest(), "little")
         for i in range(4):
-            person = b"gvs-leaf" + i.to_bytes(4, "little") + table.to_bytes(4, "little")
+            person = b"gvs-leaf" + i.to_bytes(4, "little") + (table & 1).to_bytes(4, "little")
             tag ^= int.from_bytes(hashlib.blake2b(ct[256 * i:256 * i + 256], key=mk, digest_size=16,
                                                   person=person).digest(), "little")
         out.append((ct, sct, tag.to_bytes(16, "little")))
@@ -94,13 +94,22 @@ def test_blake2b_rfc7693_and_hashlib():
             assert ffi.blake2b(msg, ds, key, person) == want, (n, ds, len(key))
 
 
+# 0 messages, 1 mailboxes, 2 pending final states (side: target row), 0x100 a
+# message row whose final state is pending
+TABLES = [0, 1, 2, 0x100]
+
+
+def has_side(table):
+    return table in (1, 2)
+
+
 @pytest.mark.skipif(not HAVE_OPENSSL, reason="openssl CLI absent")
-@pytest.mark.parametrize("table", [0, 1])
+@pytest.mark.parametrize("table", TABLES)
 def test_seal_row_matches_reference(table):
     rng = np.random.default_rng(3 + table)
     rows = [0, 1, 4095, (1 << 24) - 1, 123456789]
     pts = [rng.bytes(1024) for _ in rows]
-    sides = [rng.bytes(16) for _ in rows] if table == 1 else None
+    sides = [rng.bytes(16) for _ in rows] if has_side(table) else None
     ref = py_seal_rows(SECRET, table, rows, 7, pts, sides)
     for k, r in enumerate(rows):
         got = ffi.seal_row(SECRET, table, r, 7, pts[k], sides[k] if sides else None)
@@ -114,6 +123,9 @@ def test_seal_binds_row_epoch_and_table():
     assert ffi.seal_row(SECRET, 0, 6, 3, pt)[2] != base[2]
     assert ffi.seal_row(SECRET, 0, 5, 4, pt)[2] != base[2]
     assert ffi.seal_row(SECRET, 1, 5, 3, pt, bytes(16))[2] != base[2]
+    assert ffi.seal_row(SECRET, 2, 5, 3, pt, bytes(16))[2] != base[2]
+    pend = ffi.seal_row(SECRET, 0x100, 5, 3, pt)
+    assert pend[0] == base[0] and pend[2] != base[2]  # same ciphertext, another tag
     assert ffi.seal_row(SECRET, 0, 5, 3, pt)[0] != ffi.seal_row(SECRET, 0, 5, 4, pt)[0]
 
 
@@ -127,10 +139,10 @@ def library_seal(table, row, epoch, pt, side=None):
     return ct.raw, (sct.raw if side is not None else None), tag.raw
 
 
-@pytest.mark.parametrize("table", [0, 1])
+@pytest.mark.parametrize("table", TABLES)
 def test_library_host_sealing_matches_oracle(table):
     rng = np.random.default_rng(10 + table)
     for row in (0, 77, (1 << 20) + 3):
         pt = rng.bytes(1024)
-        side = rng.bytes(16) if table == 1 else None
+        side = rng.bytes(16) if has_side(table) else None
         assert library_seal(table, row, 9, pt, side) == ffi.seal_row(SECRET, table, row, 9, pt, side)

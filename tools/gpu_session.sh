@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU session: gpu_session.sh TAG MODE.  Output under gpurun_out/TAG.
+#   tests    the GPU test suite without the long obliviousness/timing tests
+#   timing   the C3 per-kernel duration test
+#   bench    bench.py (default workload)
+#   obl      the obliviousness counter tests (plain shapes)
+#   all      tests, bench, timing
+# Each GPU step runs under its own time limit.  A pytest exit status of 1
+# means failed tests (recorded, the session goes on); anything else (time
+# limit, abort, crash) ends the session.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+O=gpurun_out/$1
+mkdir -p "$O"
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -4 "$O/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name"; exit $rc; fi
+}
+PT="python3 -u -m pytest -v --timeout 600 --timeout-method thread -p no:cacheprovider"
+tests() { step gpu_tests 600 $PT tests -m gpu --ignore=tests/test_oblivious.py --ignore=tests/test_timing.py "$@"; }
+timing() { step timing_c3 300 $PT tests/test_timing.py; cp gpurun_out/timing_c3.txt "$O/" 2>/dev/null; }
+bench() { step bench 300 python3 bench.py; }
+case "$2" in
+  tests) tests ;;
+  timing) timing ;;
+  bench) bench ;;
+  obl) step oblivious 1100 $PT tests/test_oblivious.py -k "plain or launch" ;;
+  all) tests && bench && timing ;;
+esac
+echo ALL_DONE
