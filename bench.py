@@ -329,17 +329,20 @@ def main():
     if rank == 0:
         total = world * nreq * a.steps
         rpass_ms = stage_ms.get("rpass", float("nan"))
-        # algorithmic bytes of one message-table pass: every row
-        # read + written, every op's request image read and response written
-        # (a shard's pipeline processes shard_batch ops: B, or the padded
-        # sub-batches of all sources when sharded)
-        alg_bytes = 2 * N * 1024 + shard_batch * (1024 + 1040)
+        # algorithmic bytes of one fixed-slot message-table pass:
+        # every row read and written, and per transaction slot (W partitions x
+        # c slots, whatever the batch holds) one 1 KiB final state read and one
+        # 1 KiB snapshot written
+        W = st["msg_partitions"]
+        c = store.get_option("txn_slots")
+        alg_bytes = 2 * N * 1024 + 2 * W * c * 1024
         achieved = alg_bytes / (rpass_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("log2n") == a.log2n and tj.get("batch") == B and world == 1 and not a.auth:
+            if (tj.get("kernel") == "k_rpass2" and tj.get("log2n") == a.log2n and tj.get("batch") == B
+                    and world == 1 and not a.auth):
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -367,7 +370,8 @@ def main():
                        "expiry_per_batch": a.expiry},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rpass (message-table pass)",
+                         "kernel": "k_rpass2 (fixed-slot message-table pass)",
+                         "txn_slots": c,
                          "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms},
             "cpu_baseline": cpu,
             "checks": checks,

@@ -1307,6 +1307,17 @@ int gvs_set_timing(gvs_handle* h, int on) {
   return GVS_OK;
 }
 
+int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
+  if (!h || !key || !value) return GVS_ERR_INVALID_ARG;
+  const Engine& e = h->eng[0];
+  if (std::strcmp(key, "txn_slots") == 0) *value = e.c;
+  else if (std::strcmp(key, "group_slots") == 0) *value = e.cm;
+  else if (std::strcmp(key, "pipeline") == 0) *value = h->pipeline;
+  else if (std::strcmp(key, "rpass_variant") == 0) *value = h->rpass_variant;
+  else return GVS_ERR_INVALID_ARG;
+  return GVS_OK;
+}
+
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
   if (std::strcmp(key, "rpass_variant") == 0 && value >= 0 && value <= 10) {

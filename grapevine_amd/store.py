@@ -25,7 +25,7 @@ _TEST_LIB_PATH = os.path.join(_HERE, "libgvstore_test.so")
 EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats",
-    "gvs_synchronize", "gvs_set_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
+    "gvs_synchronize", "gvs_set_option", "gvs_get_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw")
@@ -65,6 +65,7 @@ def load_library(path=None):
     lib.gvs_synchronize.argtypes = [vp]
     lib.gvs_set_timing.argtypes = [vp, i32]
     lib.gvs_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+    lib.gvs_get_option.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
     lib.gvs_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
                                      ctypes.POINTER(ctypes.c_float), i32]
     cp, u64 = ctypes.c_char_p, ctypes.c_uint64
@@ -185,6 +186,11 @@ class ObliviousStore:
 
     def set_option(self, key, value):
         self._check(self.lib.gvs_set_option(self.h, key.encode(), int(value)))
+
+    def get_option(self, key):
+        v = ctypes.c_int64()
+        self._check(self.lib.gvs_get_option(self.h, key.encode(), ctypes.byref(v)))
+        return v.value
 
     def set_expiry_cutoff(self, cutoff):
         """Messages with timestamp < cutoff expire (gvs_set_expiry_cutoff)."""

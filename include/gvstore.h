@@ -238,6 +238,11 @@ int gvs_synchronize(gvs_handle *h);
  * (rows in flight per wave, non-temporal loads/stores). */
 int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 
+/* Read-only engine parameters of shard 0: "txn_slots" (transaction slots per
+ * message partition, c), "group_slots" (recipient-group slots per mailbox
+ * partition), "pipeline", "rpass_variant". */
+int gvs_get_option(gvs_handle *h, const char *key, int64_t *value);
+
 /* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */
 int gvs_set_timing(gvs_handle *h, int on);
 

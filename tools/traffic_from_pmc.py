@@ -33,7 +33,7 @@ def per_launch(d, counter, kernel):
 
 def main():
     fdir, wdir, log2n, batch = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-    kernel = sys.argv[5] if len(sys.argv) > 5 else "k_rpass"
+    kernel = sys.argv[5] if len(sys.argv) > 5 else "k_rpass2"
     f = per_launch(fdir, "FETCH_SIZE", kernel)
     w = per_launch(wdir, "WRITE_SIZE", kernel)
     # the last launches are the timed C3 batches (the prefill batches run on a
@@ -45,7 +45,6 @@ def main():
         "fetch_kib": fm, "write_kib": wm,
         "read_bytes": 2 * fm * 1024, "write_bytes": wm * 1024,
         "rpass_bytes_per_launch": (2 * fm + wm) * 1024,
-        "alg_bytes_per_launch": 2 * (1 << log2n) * 1024 + batch * (1024 + 1040),
         "launches_seen": [len(f), len(w)],
         "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB, MI355X_MICROARCH.md HBM section",
     }
