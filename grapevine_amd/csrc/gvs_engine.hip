@@ -35,8 +35,6 @@ static_assert(sizeof(ncclUniqueId) == GVS_COMM_ID_BYTES, "comm id size");
 
 namespace {
 
-constexpr int kNullBlocks = 32;   // R-pass blocks for ops that touch no row
-constexpr int kDummyBlocks = 32;  // M-pass blocks for ops that touch no mailbox
 constexpr int kMaxMarks = 24;
 constexpr uint64_t kExtra = 64;   // per-op records after the B real ones (record B = dry dummy)
 // Authenticated storage binds every sealed row to a 32-bit epoch (one per
@@ -75,8 +73,6 @@ struct Engine {
   OpState* ops = nullptr;
   uint32_t* kinds = nullptr;
   Key128* s1keys = nullptr;
-  uint32_t* qcount = nullptr;
-  uint32_t* qstart = nullptr;
   M1Out* m1out = nullptr;
   uint32_t* pflag = nullptr;
   uint32_t* pslot = nullptr;
@@ -84,8 +80,6 @@ struct Engine {
   uint32_t* cslot = nullptr;
   ROp* rop = nullptr;
   uint64_t* rkeys = nullptr;
-  uint32_t* pcount = nullptr;
-  uint32_t* pstart = nullptr;
   RRes* rres = nullptr;
   uint4* resp = nullptr;     // (B + extra) internal response slots of kRespSlot bytes
   uint32_t* dflag = nullptr;
@@ -97,8 +91,7 @@ struct Engine {
   uint32_t epoch = 0;        // batches applied: rows are sealed at this epoch
   // expiry sweep: X = cfg.expiry_per_batch ops at [B - X, B)
   uint32_t X = 0, xk = 1, xep = 0;
-  uint4* xbuf = nullptr;     // X records of 128 B, written by the message pass
-  // fixed-slot message pass (gvs_txn.h, pipeline 2)
+  // fixed-slot message pass (gvs_txn.h)
   uint32_t c = 0;            // transaction slots per message partition
   uint32_t par = 0;          // flips with every applied batch (ping-pong buffers)
   uint32_t stamp_run = 0, stamp_prev = kNone, stamp_next = 1;
@@ -164,8 +157,6 @@ struct gvs_handle {
   bool poisoned = false;     // an integrity failure was seen
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
-  int rpass_variant = 6;
-  int pipeline = 2;          // 2: fixed-slot transactions (gvs_txn.h); 1: the per-op message pass
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   std::vector<void*> allocs;
   std::string err;
@@ -418,8 +409,6 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   A(ops, B);
   A(kinds, B);
   A(s1keys, B);
-  A(qcount, e.Q + 1);
-  A(qstart, e.Q + 2);
   A(m1out, B + E);
   A(pflag, B);
   A(pslot, B);
@@ -427,15 +416,12 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   A(cslot, B);
   A(rop, B + E);
   A(rkeys, B);
-  A(pcount, e.W + 1);
-  A(pstart, e.W + 2);
   A(rres, B + E);
   A(resp, (B + E) * kSlotU4);
   A(dflag, B);
   A(dslot, B);
   A(bsum2, e.nblk);
   if (h->mode != kSingle) A(recv, (uint64_t)h->S * h->C * kSlotU4);
-  if (e.X) A(xbuf, (uint64_t)e.X * 8);
   if (h->auth) {
     A(mtag, e.N);
     A(btag, e.R);
@@ -481,7 +467,6 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.table, 0, e.N * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
-  if (e.X) GVS_HIP(h, hipMemsetAsync(e.xbuf, 0, (uint64_t)e.X * 128, s));
   GVS_HIP(h, hipMemsetAsync(e.gtx, 0, ((uint64_t)e.Q * e.cm + B) * 128, s));
   for (int k = 0; k < 2; ++k) {
     GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, ((uint64_t)e.W * e.c + B) * 128, s));
@@ -646,7 +631,6 @@ static MArgs margs(const gvs_handle* h, const Engine& e) {
   a.te = h->te;
   a.btag = e.btag;
   a.keys = e.s1keys;
-  a.qstart = e.qstart;
   a.mbox = e.mbox;
   a.side = e.side;
   a.m1out = e.m1out;
@@ -656,7 +640,6 @@ static MArgs margs(const gvs_handle* h, const Engine& e) {
   a.Q = e.Q;
   a.Sr = e.Sr;
   a.B = e.B;
-  a.dummy_blocks = kDummyBlocks;
   a.N = e.N;
   a.kc = e.kc;
   return a;
@@ -674,7 +657,6 @@ static AllocArgs aargs(const Engine& e) {
   a.ring = e.ring;
   a.rop = e.rop;
   a.rkeys = e.rkeys;
-  a.pcount = e.pcount;
   a.scal = e.scal;
   a.B = e.B;
   a.nblk = e.nblk;
@@ -684,118 +666,6 @@ static AllocArgs aargs(const Engine& e) {
   a.ring_size = e.ring_size;
   a.kc = e.kc;
   return a;
-}
-
-// Phase A: everything up to the mailbox read pass.  Writes only per-batch
-// scratch, so a batch can still be abandoned after it (error words).
-static int phase_a(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride, uint32_t n) {
-  hipStream_t s = h->stream;
-  const uint32_t B = e.B;
-  GVS_HIP(h, hipMemsetAsync(e.qcount, 0, (e.Q + 1) * sizeof(uint32_t), s));
-  GVS_HIP(h, hipMemsetAsync(e.pcount, 0, (e.W + 1) * sizeof(uint32_t), s));
-  const uint32_t xbase = B - e.X;
-  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
-                     (const uint4*)e.xbuf, xbase);
-  mark(h, "copy");
-  {
-    MetaArgs a{e.img, e.types, e.ops,  e.kinds, e.s1keys, e.qcount, n,
-               B,     e.Q,     e.logQ, e.N,     e.kc,     xbase};
-    hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.qcount, e.qstart, e.Q + 1);
-  }
-  mark(h, "meta");
-  if (int r = sort_keys<Key128, 4>(h, e.s1keys, B)) return r;
-  mark(h, "sort_s1");
-  if (h->auth)
-    hipLaunchKernelGGL(k_m1<true>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
-  else
-    hipLaunchKernelGGL(k_m1<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
-  mark(h, "m1");
-  GVS_HIP(h, hipGetLastError());
-  return GVS_OK;
-}
-
-static void launch_rpass(gvs_handle* h, const Engine& e, uint32_t n) {
-  hipStream_t s = h->stream;
-  RArgs a{};
-  a.table = e.table;
-  a.rkeys = e.rkeys;
-  a.pstart = e.pstart;
-  a.rop = e.rop;
-  a.img = e.img;
-  a.resp = e.resp;
-  a.rres = e.rres;
-  a.scal = e.scal;
-  a.n = n;
-  a.B = e.B;
-  a.W = e.W;
-  a.S = e.S;
-  a.null_blocks = kNullBlocks;
-  a.sc = seal_of(h, e);
-  a.te = h->te;
-  a.mtag = e.mtag;
-  a.xbase = e.B - e.X;
-  a.xon = e.X ? 1u : 0u;
-  a.xk = e.xk;
-  a.xrot = e.epoch % e.xk;
-  a.xep = e.xep;
-  a.cutoff = h->cutoff;
-  a.xbuf = e.xbuf;
-  const dim3 g(e.W + kNullBlocks), b(256);
-  if (h->auth) {
-    hipLaunchKernelGGL((k_rpass<16, true, true, 1, true>), g, b, 0, s, a);
-    return;
-  }
-  switch (h->rpass_variant) {
-    case 0: hipLaunchKernelGGL((k_rpass<4, false, false, 1>), g, b, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((k_rpass<4, true, true, 1>), g, b, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((k_rpass<8, true, false, 4>), g, b, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_rpass<8, false, true, 4>), g, b, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((k_rpass<2, true, true, 8>), g, b, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((k_rpass<16, true, true, 2>), g, b, 0, s, a); break;
-    case 7: hipLaunchKernelGGL((k_rpass<32, true, true, 1>), g, b, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_rpass<16, true, true, 1>), g, b, 0, s, a); break;
-    case 9: hipLaunchKernelGGL((k_rpass<8, true, true, 2>), g, b, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((k_rpass<16, false, true, 2>), g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL((k_rpass<8, true, true, 4>), g, b, 0, s, a); break;
-  }
-}
-
-// Phase B: allocation, message pass, commit, mailbox write pass.  Every kernel
-// returns at once if the shard's error word is set.  With d_out, responses for
-// the first n ops are converted to the caller layout; routed shards leave them
-// in e.resp for the return exchange.
-static int phase_b(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
-  hipStream_t s = h->stream;
-  const uint32_t B = e.B, nblk = e.nblk;
-  {
-    AllocArgs a = aargs(e);
-    hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, e.pcount, e.pstart, e.W + 1);
-  }
-  mark(h, "alloc");
-  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
-  mark(h, "sort_r");
-  launch_rpass(h, e, n);
-  mark(h, "rpass");
-  {
-    PostArgs a{e.kinds, e.rres, e.rop, e.dflag, e.dslot, e.bsum2, e.ring, e.scal, B, nblk,
-               e.ring_size};
-    hipLaunchKernelGGL(k_post_sum, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
-  }
-  mark(h, "post");
-  if (h->auth)
-    hipLaunchKernelGGL(k_m2<true>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
-  else
-    hipLaunchKernelGGL(k_m2<false>, dim3(e.Q + kDummyBlocks), dim3(256), 0, s, margs(h, e));
-  if (d_out && n)
-    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
-  mark(h, "m2");
-  GVS_HIP(h, hipGetLastError());
-  return GVS_OK;
 }
 
 // ------------------------------------------- pipeline 2: fixed-slot transactions
@@ -843,15 +713,12 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   const uint32_t B = e.B, nblk = e.nblk;
   e.stamp_run = e.stamp_next++;
   if (e.stamp_next == kNone) e.stamp_next = 1;
-  GVS_HIP(h, hipMemsetAsync(e.qcount, 0, (e.Q + 1) * sizeof(uint32_t), s));
-  GVS_HIP(h, hipMemsetAsync(e.pcount, 0, (e.W + 1) * sizeof(uint32_t), s));
   const uint32_t xbase = B - e.X;
   hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
                      (const uint4*)(e.X ? e.xb2[e.par ^ 1] : nullptr), xbase);
   mark(h, "copy");
   {
-    MetaArgs a{e.img, e.types, e.ops,  e.kinds, e.s1keys, e.qcount, n,
-               B,     e.Q,     e.logQ, e.N,     e.kc,     xbase};
+    MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, n, B, e.Q, e.logQ, e.N, e.kc, xbase};
     hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
   }
   mark(h, "meta");
@@ -1005,12 +872,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   return GVS_OK;
 }
 
-static int phase_a_any(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride, uint32_t n) {
-  return h->pipeline == 2 ? phase_a2(h, e, d_in, stride, n) : phase_a(h, e, d_in, stride, n);
-}
-static int phase_b_any(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
-  return h->pipeline == 2 ? phase_b2(h, e, n, d_out) : phase_b(h, e, n, d_out);
-}
+
 
 static RouteArgs rargs(gvs_handle* h, const Router& r, const Engine& e, const uint4* in,
                        uint32_t n) {
@@ -1098,8 +960,8 @@ static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out)
   if (int r = reset_errors(h)) return r;
   if (h->mode == kSingle) {
     Engine& e = h->eng[0];
-    if (int r = phase_a_any(h, e, d_in, kAbiU4, n)) return r;
-    return phase_b_any(h, e, n, d_out);
+    if (int r = phase_a2(h, e, d_in, kAbiU4, n)) return r;
+    return phase_b2(h, e, n, d_out);
   }
   const uint32_t n_src = (uint32_t)h->rt.size();
   for (uint32_t k = 0; k < n_src; ++k) {
@@ -1112,11 +974,11 @@ static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out)
   mark(h, "xchg");
   const uint32_t SC = h->S * h->C;
   for (auto& e : h->eng)
-    if (int r = phase_a_any(h, e, e.recv, kSlotU4, SC)) return r;
+    if (int r = phase_a2(h, e, e.recv, kSlotU4, SC)) return r;
   if (int r = agree_errors(h)) return r;
   mark(h, "agree");
   for (auto& e : h->eng)
-    if (int r = phase_b_any(h, e, SC, nullptr)) return r;
+    if (int r = phase_b2(h, e, SC, nullptr)) return r;
   if (int r = exchange(h, false)) return r;
   mark(h, "xchg_back");
   for (uint32_t k = 0; k < n_src; ++k) {
@@ -1153,9 +1015,7 @@ static int finish(gvs_handle* h) {
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & 1u) {
-    h->err = h->pipeline == 2
-                 ? "batch overflow: more recipients in one mailbox partition than its group slots"
-                 : "batch overflow: more than 512 distinct recipients in one mailbox partition";
+    h->err = "batch overflow: more recipients in one mailbox partition than its group slots";
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & kRErr) {
@@ -1168,10 +1028,9 @@ static int finish(gvs_handle* h) {
   }
   for (auto& en : h->eng) {
     en.epoch += 1;  // every row was rewritten at epoch + 1
-    if (h->pipeline == 2) {  // this batch's slots now hold the pending final states
-      en.par ^= 1u;
-      en.stamp_prev = en.stamp_run;
-    }
+    // this batch's slots now hold the pending final states
+    en.par ^= 1u;
+    en.stamp_prev = en.stamp_run;
   }
   return GVS_OK;
 }
@@ -1312,25 +1171,12 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
   const Engine& e = h->eng[0];
   if (std::strcmp(key, "txn_slots") == 0) *value = e.c;
   else if (std::strcmp(key, "group_slots") == 0) *value = e.cm;
-  else if (std::strcmp(key, "pipeline") == 0) *value = h->pipeline;
-  else if (std::strcmp(key, "rpass_variant") == 0) *value = h->rpass_variant;
   else return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
-  if (std::strcmp(key, "rpass_variant") == 0 && value >= 0 && value <= 10) {
-    h->rpass_variant = (int)value;
-    return GVS_OK;
-  }
-  if (std::strcmp(key, "pipeline") == 0 && (value == 1 || value == 2)) {
-    // only between batches of a fresh store: the two keep different pending state
-    for (auto& e : h->eng)
-      if (e.epoch != 0) return GVS_ERR_INVALID_ARG;
-    h->pipeline = (int)value;
-    return GVS_OK;
-  }
   return GVS_ERR_INVALID_ARG;
 }
 
@@ -1406,7 +1252,7 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
     };
     if (h->auth)
       for (uint64_t row = 0; row < N; ++row) unseal(phys.data() + row * 1024, 0u, row);
-    if (h->pipeline == 2 && e.stamp_prev != kNone) {
+    if (e.stamp_prev != kNone) {
       // rows the last batch changed are pending in P (applied by the next pass):
       // slot descriptor {row in partition, stamp, P position}
       const uint64_t WC = (uint64_t)e.W * e.c;

@@ -119,9 +119,6 @@ class ObliviousStore:
             raise GvsError(rc, "gvs_create failed (no GPU, bad config or out of memory)")
         self.h = h
         self.B = config.max_batch
-        pipe = int(os.environ.get("GVS_PIPELINE", "0"))
-        if pipe:
-            self.set_option("pipeline", pipe)
 
     def close(self):
         if getattr(self, "h", None):

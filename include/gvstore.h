@@ -233,14 +233,13 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
 /* Wait for all work on the handle's stream. */
 int gvs_synchronize(gvs_handle *h);
 
-/* Tuning knobs (engine-internal choices that never change results):
- * "rpass_variant" 0..10 selects the message-pass kernel instantiation
- * (rows in flight per wave, non-temporal loads/stores). */
+/* Tuning knobs (engine-internal choices that never change results).  This
+ * version has none: every key returns GVS_ERR_INVALID_ARG. */
 int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 
 /* Read-only engine parameters of shard 0: "txn_slots" (transaction slots per
  * message partition, c), "group_slots" (recipient-group slots per mailbox
- * partition), "pipeline", "rpass_variant". */
+ * partition). */
 int gvs_get_option(gvs_handle *h, const char *key, int64_t *value);
 
 /* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */
