@@ -27,6 +27,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md:36
+# vector-ALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per SIMD per
+# 2 cycles (MI355X_MICROARCH.md:54), at the 2.4 GHz max clock (:34)
+VALU_PEAK_GINST = 256 * 4 / 2 * 2.4
 
 
 def parse():
@@ -49,6 +52,7 @@ def parse():
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_auth_latest.json"))
     return p.parse_args()
 
 
@@ -346,7 +350,33 @@ def main():
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
             pass
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "kernel": "k_rpass2 (fixed-slot message-table pass)",
+                    "txn_slots": c, "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms}
+        if a.auth:
+            # sealed rows: the pass is bound by vector-ALU issue (AES + BLAKE2b),
+            # DESIGN.md §8; SQ_INSTS_VALU per launch from a --pmc pass
+            # (tools/valu_from_pmc.py) over the HIP-event kernel time
+            insts = None
+            try:
+                with open(a.valu_json) as f:
+                    vj = json.load(f)
+                if vj.get("log2n") == a.log2n and vj.get("batch") == B:
+                    insts = vj.get("valu_insts_per_launch")
+            except (OSError, ValueError):
+                pass
+            v_ach = insts / (rpass_ms * 1e-3) / 1e9 if insts else None
+            roofline = {"bound": "valu", "achieved": v_ach, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                        "frac": v_ach / VALU_PEAK_GINST if v_ach else None, "traffic": None,
+                        "kernel": "k_rpass2 AUTH (fixed-slot message-table pass, sealed rows)",
+                        "valu_insts_per_launch": insts, "kernel_ms": rpass_ms,
+                        "hbm_achieved": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
+                        "alg_bytes_per_launch": alg_bytes}
         cpu = None if a.no_cpu or world > 1 else cpu_baseline(a.cpu_seconds, a.cpu_threads)
+        R = cfg.mailbox_partitions * cfg.mailbox_partition_slots
+        batch_bytes = 2 * N * 1024 + 4 * R * 1024 + B * (1088 + 1088)
+        batch_gbs = batch_bytes / (elapsed / a.steps) / 1e9
         line = {
             "metric": "oblivious CRUD req/s (node) at 2^24 msgs, 64K batch; % HBM peak",
             "value": total / elapsed,
@@ -368,11 +398,12 @@ def main():
                        "route_capacity": store.stats()["route_capacity"],
                        "shard_batch": shard_batch, "auth_storage": bool(a.auth),
                        "expiry_per_batch": a.expiry},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rpass2 (fixed-slot message-table pass)",
-                         "txn_slots": c,
-                         "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms},
+            "roofline": roofline,
+            # SURVEY.md §8(d) whole-batch figure: message table and mailbox table
+            # (read pass + write pass) read and written, requests in, responses out
+            "batch_roofline": {"bytes": batch_bytes, "achieved": batch_gbs, "unit": "GB/s",
+                               "frac": batch_gbs / HBM_PEAK_GBS,
+                               "formula": "2*N*1024 + 4*R*1024 + B*(1088 + 1088), per ms_per_step"},
             "cpu_baseline": cpu,
             "checks": checks,
             "stage_ms": stage_ms,

@@ -805,6 +805,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
       // the previous batch's P (sealed at this epoch) is unsealed in place first
       if (e.stamp_prev != kNone)
         hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
+      mark(h, "punseal");
       hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
     } else {
       hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
