@@ -104,6 +104,43 @@ RAW_PENDING, RAW_PENDING_SIDE, RAW_PENDING_TAGS, RAW_SLOTS = range(5, 9)
 TABLE_PENDING_STATE, TABLE_PENDING_ROW = 2, 0x100
 
 
+# block store (gvs_oram_*, include/gvstore.h)
+ORAM_READ, ORAM_WRITE = 0, 1
+BLOCK_OP_DTYPE = np.dtype([
+    ("index", "<u8"),
+    ("op", "<u4"),
+    ("reserved", "<u4"),
+    ("data", "u1", 1024),
+])
+assert BLOCK_OP_DTYPE.itemsize == 1040
+
+
+class GvsOramConfig(ctypes.Structure):
+    _fields_ = [
+        ("capacity", ctypes.c_uint64),
+        ("max_batch", ctypes.c_uint32),
+        ("device", ctypes.c_uint32),
+        ("secret_key", ctypes.c_uint8 * 32),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 3),
+    ]
+
+
+assert ctypes.sizeof(GvsOramConfig) == 64
+
+
+def make_oram_config(capacity, max_batch=4096, device=0, secret_key=None, auth_storage=False):
+    cfg = GvsOramConfig()
+    cfg.capacity = capacity
+    cfg.max_batch = max_batch
+    cfg.device = device
+    cfg.flags = FLAG_AUTH_STORAGE if auth_storage else 0
+    key = secret_key if secret_key is not None else bytes((0x67 + 31 * i) & 0xFF for i in range(32))
+    for i in range(32):
+        cfg.secret_key[i] = key[i]
+    return cfg
+
+
 def make_config(msg_capacity, mailbox_partitions=None, mailbox_partition_slots=256,
                 max_batch=None, device=0, secret_key=None, shard_count=0, shard_index=0,
                 route_capacity=0, rows_per_partition=0, auth_storage=False, expiry_per_batch=0):

@@ -25,6 +25,7 @@
 #include "gvs_kernels.h"
 #include "gvs_route.h"
 #include "gvs_mtx.h"
+#include "gvs_kv.h"
 
 using namespace gvs;
 
@@ -32,6 +33,8 @@ static_assert(sizeof(gvs_record) == 1024, "record layout");
 static_assert(sizeof(gvs_request) == 1040, "request layout");
 static_assert(sizeof(gvs_response) == 1040, "response layout");
 static_assert(sizeof(ncclUniqueId) == GVS_COMM_ID_BYTES, "comm id size");
+static_assert(sizeof(gvs_oram_config) == 64, "oram config layout");
+static_assert(sizeof(gvs_block_op) == 1040, "block op layout (kAbiU4 uint4)");
 
 namespace {
 
@@ -110,6 +113,8 @@ struct Engine {
   RtxV* rtx_carry = nullptr;
   Rr1V* rr1_agg = nullptr;
   Rr1V* rr1_carry = nullptr;
+  uint4* rr1g = nullptr;     // B x 256 B (gvs_txn.h Rr1Op::gathered)
+  uint4* m2g = nullptr;      // B x 128 B (gvs_mtx.h k_m2g)
   uint4* vagg = nullptr, *vagg2 = nullptr, *vcarry2 = nullptr, *vcarry = nullptr;
   // fixed-slot mailbox passes (gvs_mtx.h)
   uint32_t cm = 0;           // group slots per mailbox partition
@@ -121,6 +126,9 @@ struct Engine {
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
   GtxV* gtx_carry = nullptr;
+  // block / key-value stores (gvs_kv.h)
+  uint4* kvmeta = nullptr;   // B x 128-B op lines
+  uint4* kvdummy = nullptr;  // B x 1 KiB
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -158,6 +166,7 @@ struct gvs_handle {
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
+  int kind = 0;              // 0 message store, 1 block store (gvs_oram_*)
   std::vector<void*> allocs;
   std::string err;
 };
@@ -445,6 +454,8 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(rtx_carry, B / kScanT);
     A(rr1_agg, B / kScanT);
     A(rr1_carry, B / kScanT);
+    A(rr1g, (uint64_t)B * 16);
+    A(m2g, (uint64_t)B * 8);
     const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
     A(vagg, nvb * kVLineU4);
     A(vcarry, nvb * kVLineU4);
@@ -771,52 +782,59 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   return GVS_OK;
 }
 
+// The message-table pass of the fixed-slot pipeline (also the block and
+// key-value stores' table pass): previous batch's P unsealed first (AUTH).
+static void launch_rpass2(gvs_handle* h, Engine& e) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B;
+  R2Args a{};
+  a.table = e.table;
+  a.tcur = e.tbuf[e.par];
+  a.tprev = e.tbuf[e.par ^ 1];
+  a.stamp_cur = e.stamp_run;
+  a.stamp_prev = e.stamp_prev;
+  a.pbuf = e.pbuf;
+  a.psd = e.psd;
+  a.pdum = e.pdum;
+  a.snap = e.snap;
+  a.dry = e.dryb;
+  a.scal = e.scal;
+  a.W = e.W;
+  a.S = e.S;
+  a.c = e.c;
+  a.xon = e.X ? 1u : 0u;
+  a.xk = e.xk;
+  a.xrot = e.epoch % e.xk;
+  a.xep = e.xep;
+  a.xexcl = e.xk == 1 ? 1u : 0u;
+  a.cutoff = h->cutoff;
+  a.xbuf = e.X ? e.xb2[e.par] : nullptr;
+  a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
+  if (h->auth) {
+    a.sc = seal_of(h, e);
+    a.te = h->te;
+    a.mtag = e.mtag;
+    // the previous batch's P (sealed at this epoch) is unsealed in place first
+    if (e.stamp_prev != kNone)
+      hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
+    mark(h, "punseal");
+    hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+  }
+}
+
 static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   hipStream_t s = h->stream;
   const uint32_t B = e.B, nblk = e.nblk;
-  {
-    R2Args a{};
-    a.table = e.table;
-    a.tcur = e.tbuf[e.par];
-    a.tprev = e.tbuf[e.par ^ 1];
-    a.stamp_cur = e.stamp_run;
-    a.stamp_prev = e.stamp_prev;
-    a.pbuf = e.pbuf;
-    a.psd = e.psd;
-    a.pdum = e.pdum;
-    a.snap = e.snap;
-    a.dry = e.dryb;
-    a.scal = e.scal;
-    a.W = e.W;
-    a.S = e.S;
-    a.c = e.c;
-    a.xon = e.X ? 1u : 0u;
-    a.xk = e.xk;
-    a.xrot = e.epoch % e.xk;
-    a.xep = e.xep;
-    a.xexcl = e.xk == 1 ? 1u : 0u;
-    a.cutoff = h->cutoff;
-    a.xbuf = e.X ? e.xb2[e.par] : nullptr;
-    a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
-    if (h->auth) {
-      a.sc = seal_of(h, e);
-      a.te = h->te;
-      a.mtag = e.mtag;
-      // the previous batch's P (sealed at this epoch) is unsealed in place first
-      if (e.stamp_prev != kNone)
-        hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
-      mark(h, "punseal");
-      hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
-    }
-  }
+  launch_rpass2(h, e);
   mark(h, "rpass");
   {
     Rr1Args a{e.rpos, e.rop, e.img, e.snap, e.snapdummy, e.rsb, e.rr1_agg, e.rr1_carry, e.scal,
-              B,      B / kScanT, B - e.X, e.S};
+              B,      B / kScanT, B - e.X, e.S, e.rr1g, 0u};
     hipLaunchKernelGGL(k_scan_a<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_b<Rr1Op>, dim3(1), dim3(kScanT), 0, s, a);
+    a.pass = 1;
     hipLaunchKernelGGL(k_scan_c<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
   mark(h, "rr1");
@@ -858,6 +876,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.Q = e.Q;
     a.cm = e.cm;
     a.stamp = e.stamp_run;
+    a.m2g = e.m2g;
+    hipLaunchKernelGGL(k_m2g, dim3(B / 256), dim3(256), 0, s, a);
     vscan_abc<M2rOp>(s, a);
     hipLaunchKernelGGL(k_m2r_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
@@ -1023,6 +1043,10 @@ static int finish(gvs_handle* h) {
     h->err = "batch overflow: more distinct rows of one message partition than its transaction slots";
     return GVS_ERR_BATCH_OVERFLOW;
   }
+  if (e & kKvErr) {
+    h->err = "invalid op: block index >= capacity or unknown op code";
+    return GVS_ERR_INVALID_ARG;
+  }
   if (e) {
     h->err = "internal error flag " + std::to_string(e);
     return GVS_ERR_INTERNAL;
@@ -1047,6 +1071,123 @@ static int check_epoch(gvs_handle* h) {
 static uint32_t max_submit(const gvs_handle* h) {
   return h->Bsub * (h->mode == kLocal ? h->S : 1u) - h->eng[0].X;
 }
+
+
+// ------------------------------------------- block store (gvs_oram_*, gvs_kv.h)
+
+// A table of N 1 KiB blocks with the message table's layout and pass; no
+// mailboxes, free ring or expiry.
+static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
+  e.N = N;
+  e.B = B;
+  e.nblk = B / 1024;
+  uint64_t S = N / 4096;
+  if (S < (uint64_t)kTile) S = kTile;
+  if (S > (uint64_t)kRowsMax) S = kRowsMax;
+  if (S > N) S = N;
+  e.S = (uint32_t)S;
+  e.W = (uint32_t)(N / S);
+  e.c = txn_slots(B, e.W, e.S);
+  const uint64_t WC = (uint64_t)e.W * e.c;
+#define A(ptr, n)                                     \
+  do {                                                \
+    if (int r_ = dalloc_t(h, &e.ptr, (n))) return r_; \
+  } while (0)
+  A(table, N * 64);
+  A(scal, 1);
+  A(img, (uint64_t)B * 64);
+  A(kvmeta, (uint64_t)B * 8);
+  A(kvdummy, (uint64_t)B * 64);
+  A(rkeys, B);
+  A(rpos, B);
+  for (int k = 0; k < 2; ++k) A(tbuf[k], (WC + B) * 8);
+  A(snap, WC * 64);
+  A(snapdummy, (uint64_t)B * 64);
+  A(pbuf, (uint64_t)B * 64);
+  A(psd, B);
+  A(pdum, WC * 64);
+  A(dryb, (uint64_t)e.W * 64);
+  A(rtx_agg, B / kScanT);
+  A(rtx_carry, B / kScanT);
+  const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
+  A(vagg, nvb * kVLineU4);
+  A(vcarry, nvb * kVLineU4);
+  A(vagg2, nvb2 * kVLineU4);
+  A(vcarry2, nvb2 * kVLineU4);
+  if (h->auth) {
+    A(mtag, N);
+    A(ptag, B);
+  }
+#undef A
+  hipStream_t s = h->stream;
+  GVS_HIP(h, hipMemsetAsync(e.table, 0, N * 1024, s));
+  for (int k = 0; k < 2; ++k) GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, (WC + B) * 128, s));
+  GVS_HIP(h, hipMemsetAsync(e.scal, 0, sizeof(Scal), s));
+  if (h->auth) {  // every block starts as a sealed all-zero row at epoch 0
+    e.epoch = 0;
+    hipLaunchKernelGGL(k_seal_init, dim3(1024), dim3(256), 0, s, seal_of(h, e), (const uint32_t*)h->te,
+                       e.table, e.mtag, (uint4*)nullptr, 0u, N);
+    GVS_HIP(h, hipGetLastError());
+  }
+  GVS_HIP(h, hipStreamSynchronize(s));
+  return GVS_OK;
+}
+
+// One block-store batch: n ops (gvs_block_op) at d_in, the blocks they saw
+// (n x 1 KiB) to d_out.
+static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, uint4* d_out) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B;
+  h->n_marks = 0;
+  mark(h, "start");
+  if (int r = reset_errors(h)) return r;
+  e.stamp_run = e.stamp_next++;
+  if (e.stamp_next == kNone) e.stamp_next = 1;
+  {
+    BcopyArgs a{d_in, e.img, e.kvmeta, e.rkeys, e.scal, e.N, n, B, e.W, e.S};
+    hipLaunchKernelGGL(k_bcopy, dim3(B / 256), dim3(256), 0, s, a);
+  }
+  mark(h, "copy");
+  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  mark(h, "sort_r");
+  {
+    RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,
+              B,       e.W,    e.S,           e.c,       B / kScanT,  e.stamp_run};
+    hipLaunchKernelGGL(k_scan_a<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "rtx");
+  launch_rpass2(h, e);
+  mark(h, "rpass");
+  {
+    KvArgs a{};
+    vscan_fields(a, e);
+    a.rpos = e.rpos;
+    a.meta = e.kvmeta;
+    a.img = e.img;
+    a.snap = e.snap;
+    a.snapdummy = e.snapdummy;
+    a.pbuf = e.pbuf;
+    a.psd = e.psd;
+    a.out = d_out;
+    a.outdummy = e.kvdummy;
+    a.n = n;
+    a.S = e.S;
+    a.omap = 0;
+    vscan_abc<KvOp>(s, a);
+    hipLaunchKernelGGL(k_kv_c, dim3(a.nvb), dim3(256), 0, s, a);
+  }
+  if (h->auth)  // P at the epoch the pass wrote the rows at
+    hipLaunchKernelGGL(k_pseal<true>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch + 1));
+  mark(h, "kv");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+struct gvs_oram {
+  gvs_handle* h = nullptr;
+};
 
 // ------------------------------------------------------------------ C ABI
 
@@ -1330,5 +1471,104 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
 }
 
 #endif  // GVS_TEST_HOOKS
+
+
+// ---- block store: mc-oblivious-traits ORAM::access, batched
+
+int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
+  if (!cfg || !out) return GVS_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!is_pow2(cfg->capacity) || cfg->capacity < 4096 || cfg->capacity > (1ull << 32))
+    return GVS_ERR_INVALID_ARG;
+  if (!is_pow2(cfg->max_batch) || cfg->max_batch < 1024 || cfg->max_batch > (1u << (kSeqBits - 1)))
+    return GVS_ERR_INVALID_ARG;
+  if (cfg->flags & ~GVS_FLAG_AUTH_STORAGE) return GVS_ERR_INVALID_ARG;
+  for (int i = 0; i < 3; ++i)
+    if (cfg->reserved[i]) return GVS_ERR_INVALID_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GVS_ERR_NO_DEVICE;
+  if ((int)cfg->device >= ndev) return GVS_ERR_INVALID_ARG;
+  gvs_oram* o = new (std::nothrow) gvs_oram();
+  gvs_handle* h = new (std::nothrow) gvs_handle();
+  if (!o || !h) {
+    delete o;
+    delete h;
+    return GVS_ERR_OUT_OF_MEMORY;
+  }
+  o->h = h;
+  h->kind = 1;
+  h->mode = kSingle;
+  h->device = (int)cfg->device;
+  h->auth = (cfg->flags & GVS_FLAG_AUTH_STORAGE) != 0;
+  h->cfg.msg_capacity = cfg->capacity;
+  h->cfg.max_batch = cfg->max_batch;
+  h->cfg.device = cfg->device;
+  h->cfg.flags = cfg->flags;
+  std::memcpy(h->cfg.secret_key, cfg->secret_key, 32);
+  h->Bsub = h->Be = cfg->max_batch;
+  auto fail = [&](int code) {
+    gvs_oram_destroy(o);
+    return code;
+  };
+  if (hipSetDevice(h->device) != hipSuccess) return fail(GVS_ERR_DEVICE);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(GVS_ERR_DEVICE);
+  for (auto& ev : h->ev)
+    if (hipEventCreate(&ev) != hipSuccess) return fail(GVS_ERR_DEVICE);
+  if (h->auth) {
+    uint32_t te0[256];
+    storage_ctx(cfg->secret_key, h->sc, te0);
+    if (int rc = dalloc_t(h, &h->te, 256)) return fail(rc);
+    if (hipMemcpy(h->te, te0, sizeof te0, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GVS_ERR_DEVICE);
+  }
+  h->eng.resize(1);
+  if (int rc = kv_engine_init(h, h->eng[0], cfg->capacity, cfg->max_batch)) return fail(rc);
+  if (int rc = dalloc_t(h, &h->in_stage, (uint64_t)cfg->max_batch * kAbiU4)) return fail(rc);
+  if (int rc = dalloc_t(h, &h->out_stage, (uint64_t)cfg->max_batch * 64)) return fail(rc);
+  *out = o;
+  return GVS_OK;
+}
+
+int gvs_oram_destroy(gvs_oram* o) {
+  if (!o) return GVS_ERR_INVALID_ARG;
+  if (o->h) gvs_destroy(o->h);
+  delete o;
+  return GVS_OK;
+}
+
+int gvs_oram_access_batch(gvs_oram* o, const gvs_block_op* ops, uint32_t n, uint8_t* out) {
+  if (!o || (!ops && n) || (!out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
+  gvs_handle* h = o->h;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
+  GVS_HIP(h, hipSetDevice(h->device));
+  if (n)
+    GVS_HIP(h, hipMemcpyAsync(h->in_stage, ops, (size_t)n * sizeof(gvs_block_op),
+                              hipMemcpyHostToDevice, h->stream));
+  if (int r = oram_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
+  if (n)
+    GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * 1024, hipMemcpyDeviceToHost, h->stream));
+  return finish(h);
+}
+
+int gvs_oram_access_batch_device(gvs_oram* o, const void* d_ops, uint32_t n, void* d_out) {
+  if (!o || (!d_ops && n) || (!d_out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
+  gvs_handle* h = o->h;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
+  GVS_HIP(h, hipSetDevice(h->device));
+  const uint4* in = n ? (const uint4*)d_ops : h->in_stage;
+  if (int r = oram_batch(h, h->eng[0], in, n, n ? (uint4*)d_out : h->out_stage)) return r;
+  return finish(h);
+}
+
+int gvs_oram_set_timing(gvs_oram* o, int on) { return o ? gvs_set_timing(o->h, on) : GVS_ERR_INVALID_ARG; }
+
+int gvs_oram_last_timings(gvs_oram* o, const char** names, float* ms, int cap) {
+  return o ? gvs_last_timings(o->h, names, ms, cap) : GVS_ERR_INVALID_ARG;
+}
+
+const char* gvs_oram_last_error(gvs_oram* o) { return o ? o->h->err.c_str() : "null handle"; }
 
 }  // extern "C"

@@ -312,7 +312,7 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   o.kind = kind;
   o.pre_status = pre;
   o.q = q;
-  a.ops[i] = o;
+  st_drop_rec(a.ops, i, o);  // read by the scans in sorted order
   a.kinds[i] = kind;
   a.s1keys[i] = key;
 }
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(1024) void k_alloc_b(AllocArgs a) {
     r.slot = os.slot;
     if (os.slot != kNone) cls = 2;
   }
-  a.rop[i] = r;
+  st_drop_rec(a.rop, i, r);  // read by the scans in sorted order
   uint64_t rowp = kRNullRow;
   uint32_t part = a.W;
   if (cls < 3) {

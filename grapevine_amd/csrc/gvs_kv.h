@@ -1,0 +1,242 @@
+// gvs_kv.h — block and key-value access on the fixed-slot table pass: the
+// mc-oblivious-traits surfaces of SURVEY.md §8 a10 (ObliviousHashMap) and a11
+// (ORAM::access), batched.
+//
+// A batch of B ops over a table of N 1 KiB rows (partition-major, as the
+// message table) runs:
+//   k_bcopy          ops -> 1 KiB images, 128-B per-op meta lines, row keys
+//   sort64           row keys (row, seq)
+//   k_scan_*<RtxOp>  rows -> transaction slots (gvs_txn.h)
+//   k_rpass2         table pass: apply the previous batch's final states,
+//                    snapshot this batch's rows (gvs_txn.h)
+//   k_vscan_*<KvOp>  (exists, value) copy-forward along each row's ops
+//   k_kv_c           per op: status, the value it saw; the final states (P)
+// Each op's state transform is one of id (READ), const(e, v) (WRITE: (1, v),
+// REMOVE: (0, 0)) and ifabsent(v) (INSERT).  The class is closed under
+// composition, so a row's ops fold associatively and the scan is op-parallel.
+#pragma once
+#include "gvs_txn.h"
+
+namespace gvs {
+
+enum KvKind : uint32_t { KV_READ = 0, KV_WRITE = 1, KV_INSERT = 2, KV_REMOVE = 3 };
+// per-op status (mc-oblivious-traits OMAP_* codes)
+constexpr uint32_t kOmapFound = 0, kOmapNotFound = 1, kOmapOverflow = 2, kOmapInvalidKey = 3;
+// transform kinds in the scan flags F = {kind, e, 0, 0}
+constexpr uint32_t kTId = 0, kTConst = 1, kTIfAbsent = 2;
+
+// ------------------------------------------------------------- k_bcopy
+//
+// ORAM ops (gvs_block_op, 1040 B: index, op, data) -> image (data), meta line
+// {kind, e0 = 1, 0, 0} and row key.  Ops >= n are padding (null row).  An
+// index >= N or an op code > 1 fails the batch (error bit kKvErr) before any
+// state changes.
+constexpr uint32_t kKvErr = 64;
+
+struct BcopyArgs {
+  const uint4* in;   // n x 65 uint4
+  uint4* img;        // B x 64
+  uint4* meta;       // B x 8
+  uint64_t* rkeys;   // B
+  Scal* scal;
+  uint64_t N;
+  uint32_t n, B, W, S;
+};
+
+__global__ __launch_bounds__(256) void k_bcopy(BcopyArgs a) {
+  __shared__ uint4 stage[4 * 64 * 8];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t i0 = (blockIdx.x * 4 + wave) * 64;  // 64 ops per wave: meta lines by wave_store128
+  uint4 rec[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) rec[c] = make_uint4(0, 0, 0, 0);
+  uint32_t my_kind = 0;
+  for (uint32_t j = 0; j < 64; ++j) {
+    const uint32_t i = i0 + j;
+    const bool real = i < a.n;
+    const uint4* src = a.in + (uint64_t)min(i, a.n ? a.n - 1 : 0u) * 65;
+    uint4 v = real ? src[1 + lane] : make_uint4(0, 0, 0, 0);
+    a.img[(uint64_t)i * 64 + lane] = v;
+    const uint4 h = real ? uni4(src[0]) : make_uint4(0, 0, 0, 0);
+    const uint64_t index = (uint64_t)h.x | ((uint64_t)h.y << 32);
+    const bool bad = real && (index >= a.N || h.z > 1u);
+    if (bad && lane == 0) atomicOr(&a.scal->error, kKvErr);
+    const uint64_t row = (real && !bad) ? (index % a.W) * a.S + index / a.W : kRNullRow;
+    if (lane == 0) a.rkeys[i] = r_key(row, 0u, i);
+    my_kind = lane == j ? h.z : my_kind;
+  }
+  rec[0] = make_uint4(my_kind, 1u, 0u, 0u);
+  wave_store128(stage + wave * 64 * 8, a.meta, i0 + lane, rec);
+}
+
+// ------------------------------------------------------------- KvOp scan
+
+struct KvArgs {
+  GVS_VSCAN_FIELDS
+  const uint4* rpos;       // B sorted positions (RtxOp)
+  const uint4* meta;       // B x 128 B, by seq: {kind, e0, overflow, 0}
+  const uint4* img;        // B x 1 KiB, by seq
+  const uint4* snap;       // W*c slot snapshots
+  const uint4* snapdummy;  // B x 1 KiB (non-heads read their own line)
+  uint4* pbuf;             // B final states, by position
+  uint4* psd;              // B side entries {row lo, row hi, valid, 0}
+  uint4* out;              // ORAM: n x 1 KiB (caller); OMAP: B x kRespSlot
+  uint4* outdummy;         // ORAM: B x 1 KiB for padding ops
+  uint32_t n, S, omap;
+};
+
+struct KvHdr {
+  uint32_t seq, flags, slot, kind, e0, ovf;
+  uint64_t prow;
+};
+
+__device__ inline KvHdr kv_hdr(const KvArgs& a, uint32_t p) {
+  const uint4 rp = uni4(a.rpos[p]);
+  KvHdr h;
+  h.seq = rp.x & kSeqMask;
+  h.flags = rp.x;
+  h.slot = rp.y;
+  h.prow = (rp.x & kPosNull) ? 0ull : (uint64_t)rp.z * a.S + rp.w;
+  const uint4 m = uni4(shfl4(line_load(a.meta + (uint64_t)h.seq * 8), 0));
+  h.kind = m.x;
+  h.e0 = m.y;
+  h.ovf = m.z;
+  return h;
+}
+
+struct KvOp {
+  using Args = KvArgs;
+  static constexpr bool kSelect = true;
+  __device__ static uint4 f_identity() { return make_uint4(kTId, 0, 0, 0); }
+  // a then b: function composition of the transforms
+  __device__ static uint4 f_combine(uint4 a, uint4 b) {
+    const uint4 one = make_uint4(kTConst, 1u, 0, 0);
+    uint4 r = sel4(b.x == kTConst, b, a);
+    const uint4 ifa = sel4(a.x == kTId, b, sel4(a.x == kTConst && a.y == 0u, one, a));
+    return sel4(b.x == kTIfAbsent, ifa, r);
+  }
+  __device__ static bool takes_b(uint4 a, uint4 b) {
+    return b.x == kTConst || (b.x == kTIfAbsent && (a.x == kTId || (a.x == kTConst && a.y == 0u)));
+  }
+  __device__ static uint4 v_combine(uint4 fa, uint4 va, uint4 fb, uint4 vb) {
+    return sel4(takes_b(fa, fb), vb, va);
+  }
+  // the op's own transform (an overflowed INSERT / WRITE changes nothing)
+  __device__ static uint4 own_f(const KvHdr& h) {
+    const bool creates = h.kind == KV_WRITE || h.kind == KV_INSERT;
+    uint32_t k = kTId, e = 0;
+    k = selu32(h.kind == KV_WRITE || h.kind == KV_REMOVE, kTConst, k);
+    e = selu32(h.kind == KV_WRITE, 1u, e);
+    k = selu32(h.kind == KV_INSERT, kTIfAbsent, k);
+    k = selu32(creates && h.ovf, kTId, k);
+    return make_uint4(k, e, 0, 0);
+  }
+  // element of position p: a row head starts from const(e0, snapshot)
+  __device__ static uint4 f_of_hdr(const KvHdr& h) {
+    const uint4 o = own_f(h);
+    const uint4 hd = f_combine(make_uint4(kTConst, h.e0, 0, 0), o);
+    const bool head = h.flags & kPosHead, null = h.flags & kPosNull;
+    return sel4(null, make_uint4(kTConst, 0, 0, 0), sel4(head, hd, o));
+  }
+  __device__ static uint4 f_of(const Args& a, uint32_t p) { return f_of_hdr(kv_hdr(a, p)); }
+  // value of position p's element: the op's image when its own transform
+  // supplies the value (WRITE; INSERT into an absent row), else the snapshot
+  // (a head whose own transform keeps the row), zero for REMOVE / null
+  __device__ static bool from_img(const KvHdr& h) {
+    const uint4 o = own_f(h);
+    const bool head = h.flags & kPosHead;
+    return (o.x == kTConst && o.y == 1u) || (o.x == kTIfAbsent && !(head && h.e0));
+  }
+  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 f) {
+    const KvHdr h = kv_hdr(a, p);
+    const bool img = from_img(h);
+    const bool head = h.flags & kPosHead;
+    const uint4* src = (head && !img) ? a.snap + (uint64_t)h.slot * 64 : a.img + (uint64_t)h.seq * 64;
+    const uint4 x = ld_row<false>(&src[lane_id()]);
+    const uint4 o = own_f(h);
+    const bool zero = (h.flags & kPosNull) || (o.x == kTConst && o.y == 0u) || (!head && o.x == kTId);
+    (void)f;
+    return sel4(zero, make_uint4(0, 0, 0, 0), x);
+  }
+};
+
+// k_kv_c: each wave walks its 16 ops from its carry: the state before the op
+// (row head: (e0, snapshot)), the op's status and returned value, the state
+// after it into P at the op's position, and its side entry.
+__global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
+  if (a.scal->error) return;
+  __shared__ uint4 s_v[4][64];
+  __shared__ uint4 s_f[4];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  // each op's snapshot (heads) or own dummy line, and its image, read once
+  uint4 svs[16], ivs[16];
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const KvHdr h = kv_hdr(a, p0 + j);
+    const uint4* sp = (h.flags & kPosHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
+    svs[j] = ld_row<false>(&sp[lane]);
+    ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+  }
+  uint4 cf, cv;
+  {  // the wave's aggregate from registers, then the carry
+    uint4 f = KvOp::f_identity(), v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const KvHdr h = kv_hdr(a, p0 + j);
+      const uint4 e = KvOp::f_of_hdr(h);
+      const bool head = h.flags & kPosHead;
+      const uint4 o = KvOp::own_f(h);
+      const bool zero = (h.flags & kPosNull) || (o.x == kTConst && o.y == 0u) || (!head && o.x == kTId);
+      const uint4 x = sel4(head && !KvOp::from_img(h), svs[j], ivs[j]);
+      v = sel4(KvOp::takes_b(f, e), sel4(zero, make_uint4(0, 0, 0, 0), x), v);
+      f = KvOp::f_combine(f, e);
+    }
+    vscan_carry_tail<KvOp>(a, s_v, s_f, f, v, cf, cv);
+  }
+  uint4 sd = make_uint4(0, 0, 0, 0);
+  const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t p = p0 + j;
+    const KvHdr h = kv_hdr(a, p);
+    const bool head = h.flags & kPosHead, null = h.flags & kPosNull, last = h.flags & kPosLast;
+    const uint4 sv = svs[j], iv = ivs[j];
+    // the state before the op
+    const bool e = head ? h.e0 != 0u : (cf.x == kTConst && cf.y != 0u);
+    const uint4 v = sel4(head, sv, cv);
+    const bool creates = h.kind == KV_WRITE || h.kind == KV_INSERT;
+    uint32_t status = e ? kOmapFound : kOmapNotFound;
+    status = selu32((creates && h.ovf) || (null && creates && a.omap), kOmapOverflow, status);
+    status = selu32(null && !creates, kOmapNotFound, status);
+    const bool ovf = status == kOmapOverflow;
+    // the value handed back: the row's value (READ, WRITE, REMOVE, INSERT of
+    // a present key); the default an INSERT put in; zero when absent
+    uint4 resp = sel4(e && !null, v, z);
+    resp = sel4(h.kind == KV_INSERT && !e && !ovf && !null, iv, resp);
+    // the state after it
+    bool e2 = e;
+    uint4 v2 = v;
+    const bool wr = h.kind == KV_WRITE && !ovf, ins = h.kind == KV_INSERT && !ovf && !e;
+    v2 = sel4(wr || ins, iv, v2);
+    e2 = (wr || ins) ? true : e2;
+    v2 = sel4(h.kind == KV_REMOVE, z, v2);
+    e2 = h.kind == KV_REMOVE ? false : e2;
+    v2 = sel4(null, z, v2);
+    e2 = null ? false : e2;
+    cv = v2;
+    cf = make_uint4(kTConst, e2 ? 1u : 0u, 0, 0);
+    if (a.omap) {
+      const uint64_t r0 = (uint64_t)h.seq * (kRespSlot / 16);
+      st_drop(a.out, r0 + lane, resp);
+      if (lane < 8) st_drop(a.out, r0 + 64 + lane, make_uint4(lane == 0 ? status : 0u, 0, 0, 0));
+    } else {
+      st_drop(null ? a.outdummy : a.out, (uint64_t)h.seq * 64 + lane, v);
+    }
+    st_drop(a.pbuf, (uint64_t)p * 64 + lane, v2);
+    sd = sel4(lane == j, make_uint4((uint32_t)h.prow, (uint32_t)(h.prow >> 32), last ? 1u : 0u, 0u), sd);
+  }
+  if (lane < 16) st_drop(a.psd, p0 + lane, sd);
+}
+
+}  // namespace gvs

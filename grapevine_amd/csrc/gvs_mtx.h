@@ -79,7 +79,7 @@ struct GtxOp {
   __device__ static bool same_group(const Key128& x, const Key128& y) {
     return x.hi == y.hi && s1_group(x.lo) == s1_group(y.lo);
   }
-  __device__ static V local(const Args& a, uint32_t p) {
+  __device__ static V local(const Args& a, uint32_t p, uint4*) {
     const Key128 k = a.keys[p];
     Key128 pk = {~0ull, ~0ull};
     if (p) pk = a.keys[p - 1];
@@ -118,14 +118,16 @@ struct GtxOp {
     a.mpos[p] = make_uint4(seq | (head ? kMPosHead : 0u) | (last ? kMPosLast : 0u) |
                                (null ? kMPosNull : 0u) | (cls << 23) | (sub << 25),
                            null ? kNone : q * a.cm + kk, q, rank);
-    const OpState& os = a.ops[seq];
+    uint4 ol[8];  // OpState: x (the mailbox key) is 32-bit words 14..21
+    wave_load128(stage, reinterpret_cast<const uint4*>(a.ops + seq), ol);
+    const uint32_t* ow = reinterpret_cast<const uint32_t*>(ol);
     const uint64_t glo = s1_group(k.lo);
     uint4 rec[8];
     rec[0] = make_uint4(a.stamp, in.n_next, in.n_del, in.n_create);
     rec[1] = make_uint4(in.n_x, in.fcs, in.g0, in.c1);
     rec[2] = make_uint4((uint32_t)k.hi, (uint32_t)(k.hi >> 32), (uint32_t)glo, (uint32_t)(glo >> 32));
-    rec[3] = make_uint4(os.x[0], os.x[1], os.x[2], os.x[3]);
-    rec[4] = make_uint4(os.x[4], os.x[5], os.x[6], os.x[7]);
+    rec[3] = make_uint4(ow[14], ow[15], ow[16], ow[17]);
+    rec[4] = make_uint4(ow[18], ow[19], ow[20], ow[21]);
     rec[5] = rec[6] = rec[7] = make_uint4(0, 0, 0, 0);
     const uint64_t idx = last ? (uint64_t)q * a.cm + kk : (uint64_t)a.Q * a.cm + p;
     wave_store128(stage, a.gtx, idx, rec);
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
       const uint4 hdr = make_uint4(G.len, G.fl, G.flags, (uint32_t)G.slot);
       cur = sel4(lane == 0, hdr, sel4(lane == 1, make_uint4(0, 0, 0, 0), cur));
       uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
-      st_row<true>(&dst[lane], cur);
+      st_drop(dst, lane, cur);
       dry_run = false;
     }
 #pragma unroll
@@ -308,7 +310,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     const bool real = !dry_run && k < ng;
     const uint4 hdr = sel4(real, make_uint4(0u, G.fl, G.flags, (uint32_t)G.slot), make_uint4(0, 0, 0, 0));
     uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
-    st_row<true>(&dst[lane], sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
+    st_drop(dst, lane, sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
   }
 }
 
@@ -356,17 +358,34 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
   __shared__ uint4 s_f[4];
   if (a.scal->error) return;
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  uint4 cf, cv;
-  vscan_carry_in<M1rOp>(a, s_v, s_f, cf, cv);
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  // each op's snapshot (heads) or own dummy line, read once
+  uint4 As[16];
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint4 mp = uni4(a.mpos[p0 + j]);
+    As[j] = ld_row<false>(&M1rOp::src_of(a, p0 + j, mp)[lane]);
+  }
+  uint4 cf, cv;
+  {  // the wave's aggregate from registers, then the carry
+    uint4 f = M1rOp::f_identity(), v = As[0];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint4 e = M1rOp::f_of(a, p0 + j);
+      v = sel4(M1rOp::takes_b(f, e), As[j], v);
+      f = M1rOp::f_combine(f, e);
+    }
+    vscan_carry_tail<M1rOp>(a, s_v, s_f, f, v, cf, cv);
+  }
+#pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
     const uint4 mp = uni4(a.mpos[p]);
     const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
     const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;
-    const uint4 A = ld_row<false>(&M1rOp::src_of(a, p, mp)[lane]);
-    const OpState& os = a.ops[seq];
-    const uint4 myid = make_uint4(os.id[0], os.id[1], os.id[2], os.id[3]);
+    const uint4 A = As[j];
+    const uint4 ol = line_load(a.ops + seq);  // OpState: id is 32-bit words 10..13
+    const uint4 myid = make_uint4(line_u32(ol, 10), line_u32(ol, 11), line_u32(ol, 12), line_u32(ol, 13));
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 0u, 0u), cf);
     const uint4 pv = sel4(head, A, cv);
     const uint4 hdr = uni4(shfl4(pv, 0));
@@ -396,9 +415,9 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     } else if (!null) {
       opos = pos;
     }
-    uint4* o = reinterpret_cast<uint4*>(a.m1out) + (uint64_t)seq * 8;
     if (lane < 8)
-      o[lane] = sel4(lane == 0, make_uint4(status, slot, flags, opos), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0)));
+      st_drop(a.m1out, (uint64_t)seq * 8 + lane,
+              sel4(lane == 0, make_uint4(status, slot, flags, opos), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0))));
     const uint4 e = M1rOp::f_of_pos(mp.x);
     cv = M1rOp::v_combine(cf, cv, e, A);
     cf = M1rOp::f_combine(cf, e);
@@ -419,6 +438,7 @@ struct M2rArgs {
   const M1Out* m1out;
   uint4* m2tx;  // (Q*cm + B) x 1152 B
   uint32_t Q, cm, stamp;
+  uint4* m2g;   // B x 128 B by position (k_m2g): F, appended id, recipient key
 };
 
 struct M2rOp {
@@ -432,24 +452,49 @@ struct M2rOp {
   __device__ static uint4 v_combine(uint4, uint4 va, uint4 fb, uint4 vb) {
     return sel4(fb.x != 0u || nz4(vb), vb, va);
   }
-  __device__ static uint4 f_of(const Args& a, uint32_t p) {
-    const uint4 mp = uni4(a.mpos[p]);
-    const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
-    const bool null = mp.x & kMPosNull, head = mp.x & kMPosHead;
-    const bool succ = __builtin_amdgcn_readfirstlane(a.rres[seq].status) == 1u;
-    const uint32_t pos = __builtin_amdgcn_readfirstlane(a.m1out[seq].pad);
+  // the element flags from the op's gathered lines (k_m2g)
+  __device__ static uint4 f_from(uint32_t mpx, uint32_t status, uint32_t pos) {
+    const uint32_t cls = mpos_cls(mpx);
+    const bool null = mpx & kMPosNull, head = mpx & kMPosHead;
+    const bool succ = status == 1u;
     const bool del = !null && cls == 2u && succ && pos < GVS_MAILBOX_SLOTS;
     return make_uint4((head || null) ? 1u : 0u, (del && pos < 32u) ? 1u << pos : 0u,
                       (del && pos >= 32u) ? 1u << (pos - 32u) : 0u, (!null && cls == 1u && succ) ? 1u : 0u);
   }
+  __device__ static uint4 f_of(const Args& a, uint32_t p) { return uni4(a.m2g[(uint64_t)p * 8]); }
   __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 e) {
     const uint4 mp = uni4(a.mpos[p]);
-    const uint32_t seq = mp.x & kSeqMask;
-    const ROp& r = a.rop[seq];
-    const uint4 id = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    const uint4 id = a.m2g[(uint64_t)p * 8 + 1];
     return sel4(e.w != 0u && lane_id() == 2u + mp.w && mp.w < GVS_MAILBOX_SLOTS, id, make_uint4(0, 0, 0, 0));
   }
 };
+
+// Gather, once per batch, each sorted position's lines (RRes, M1Out, ROp,
+// OpState) into a position-indexed 128-B record: {F, appended id, recipient
+// key x[0..3], x[4..7]}.  The scans and k_m2r_c read only these records
+// (addresses that do not depend on the data).
+__global__ __launch_bounds__(256) void k_m2g(M2rArgs a) {
+  __shared__ uint4 stage[4 * 64 * 8];
+  if (a.scal->error) return;
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  uint4* st = stage + (threadIdx.x >> 6) * 64 * 8;
+  const uint32_t mpx = a.mpos[p].x, seq = mpx & kSeqMask;
+  uint4 l[8], rec[8];
+  wave_load128(st, reinterpret_cast<const uint4*>(a.rres + seq), l);
+  const uint32_t status = l[0].x;
+  wave_load128(st, reinterpret_cast<const uint4*>(a.m1out + seq), l);
+  const uint32_t pos = l[0].w;
+  wave_load128(st, reinterpret_cast<const uint4*>(a.rop + seq), l);
+  rec[0] = M2rOp::f_from(mpx, status, pos);
+  rec[1] = l[1];  // ROp id
+  wave_load128(st, reinterpret_cast<const uint4*>(a.ops + seq), l);
+  const uint32_t* ow = reinterpret_cast<const uint32_t*>(l);  // OpState: x is words 14..21
+  rec[2] = make_uint4(ow[14], ow[15], ow[16], ow[17]);
+  rec[3] = make_uint4(ow[18], ow[19], ow[20], ow[21]);
+#pragma unroll
+  for (int i = 4; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
+  wave_store128(st, a.m2g, p, rec);
+}
 
 __global__ __launch_bounds__(256) void k_m2r_c(M2rArgs a) {
   __shared__ uint4 s_v[4][64];
@@ -462,20 +507,17 @@ __global__ __launch_bounds__(256) void k_m2r_c(M2rArgs a) {
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
     const uint4 mp = uni4(a.mpos[p]);
-    const uint32_t seq = mp.x & kSeqMask;
     const bool last = (mp.x & kMPosLast) && !(mp.x & kMPosNull);
     const uint4 e = M2rOp::f_of(a, p);
     cv = M2rOp::v_combine(cf, cv, e, M2rOp::value_of(a, p, e));
     cf = M2rOp::f_combine(cf, e);
     // the group's last op writes its result slot, every other op a dummy
-    const OpState& os = a.ops[seq];
-    const uint4 x0 = make_uint4(os.x[0], os.x[1], os.x[2], os.x[3]);
-    const uint4 x1 = make_uint4(os.x[4], os.x[5], os.x[6], os.x[7]);
-    uint4* o = a.m2tx + (last ? (uint64_t)mp.y : (uint64_t)a.Q * a.cm + p) * kVLineU4;
+    const uint4 x0 = a.m2g[(uint64_t)p * 8 + 2], x1 = a.m2g[(uint64_t)p * 8 + 3];
+    const uint64_t o = (last ? (uint64_t)mp.y : (uint64_t)a.Q * a.cm + p) * kVLineU4;
     // value: lanes 0..1 the recipient key (a new mailbox's first 32 B), lanes
     // 2.. the appended ids; header: stamp, creates, removal mask
-    o[8 + lane] = sel4(lane == 0, x0, sel4(lane == 1, x1, cv));
-    if (lane < 8) o[lane] = sel4(lane == 0, make_uint4(a.stamp, cf.w, cf.y, cf.z), make_uint4(0, 0, 0, 0));
+    st_drop(a.m2tx, o + 8 + lane, sel4(lane == 0, x0, sel4(lane == 1, x1, cv)));
+    if (lane < 8) st_drop(a.m2tx, o + lane, sel4(lane == 0, make_uint4(a.stamp, cf.w, cf.y, cf.z), make_uint4(0, 0, 0, 0)));
   }
 }
 

@@ -50,9 +50,40 @@ __device__ inline void wave_store128(uint4* stage, uint4* base, uint64_t idx, co
   for (int it = 0; it < 8; ++it) {
     const uint32_t r = (uint32_t)it * 8 + (lane >> 3), ch = lane & 7u;
     const uint64_t ix = shfl_u64(idx, (int)r);
-    base[ix * 8 + ch] = stage[r * 8 + ch];
+    st_drop(base, ix * 8 + ch, stage[r * 8 + ch]);
   }
   wave_lds_sync();
+}
+
+// Gathers of per-op records (addresses that depend on the data) read whole
+// 128-B lines, 8 lanes per line in one instruction.  A partial read of a line
+// is fetched as 32- or 64-B sectors, how many depending on the other requests
+// to that line in flight, which made FETCH_SIZE depend on the data.
+
+// thread level: lane l gets the 128-B line at its own `src` in rec
+__device__ inline void wave_load128(uint4* stage, const uint4* src, uint4 (&rec)[8]) {
+  const uint32_t lane = lane_id();
+  const uint64_t a = (uint64_t)src;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t r = (uint32_t)it * 8 + (lane >> 3), ch = lane & 7u;
+    const uint4* s = reinterpret_cast<const uint4*>(shfl_u64(a, (int)r));
+    stage[r * 8 + ch] = s[ch];
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int c = 0; c < 8; ++c) rec[c] = stage[lane * 8 + c];
+  wave_lds_sync();
+}
+
+// wave level: the line at a wave-uniform address, lane l holding its 16-B
+// word l mod 8; line_u32 hands 32-bit word k (a constant) to every lane
+__device__ inline uint4 line_load(const void* line) {
+  return reinterpret_cast<const uint4*>(line)[lane_id() & 7u];
+}
+__device__ inline uint32_t line_u32(uint4 x, uint32_t k) {
+  const uint32_t c = (k & 3u) == 0u ? x.x : (k & 3u) == 1u ? x.y : (k & 3u) == 2u ? x.z : x.w;
+  return (uint32_t)__shfl((int)c, (int)(k >> 2));
 }
 
 // ---------------------------------------------------- generic op scans
@@ -66,50 +97,49 @@ __device__ inline void wave_store128(uint4* stage, uint4* base, uint64_t idx, co
 template <class V>
 __device__ inline void v_copy(V& d, const V& s) { d = s; }
 
+// s holds kScanT + 1 entries: s[kScanT] is the identity, so that every step
+// combines unconditionally (a branch around a struct assignment puts the
+// struct in scratch)
 template <class Op>
-__device__ inline typename Op::V block_excl(const typename Op::V& x, typename Op::V* s,
-                                            typename Op::V& total) {
+__device__ inline typename Op::V block_excl(const typename Op::V& x, typename Op::V* s) {
   using V = typename Op::V;
   const uint32_t t = threadIdx.x;
   s[t] = x;
+  if (t == 0) s[kScanT] = Op::identity();
   __syncthreads();
   for (uint32_t d = 1; d < kScanT; d <<= 1) {
-    V y = s[t];
-    if (t >= d) y = Op::combine(s[t - d], y);
+    const V y = Op::combine(s[t >= d ? t - d : kScanT], s[t]);
     __syncthreads();
     s[t] = y;
     __syncthreads();
   }
-  V ex = Op::identity();
-  if (t) ex = s[t - 1];
-  total = s[kScanT - 1];
+  const V ex = s[t ? t - 1 : kScanT];
   __syncthreads();
-  return ex;
+  return ex;  // s[kScanT - 1] still holds the block total
 }
 
 // Phase-B scans stop when the batch already failed (Op::stop): an abandoned
 // batch must not overwrite the pending final states of the previous one.
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_a(typename Op::Args a) {
-  __shared__ typename Op::V s[kScanT];
+  __shared__ typename Op::V s[kScanT + 1];
   if (Op::stop(a)) return;
+  __shared__ uint4 stage[4 * 64 * 8];  // per-wave record stage (wave_load128)
   const uint32_t p = blockIdx.x * kScanT + threadIdx.x;
-  typename Op::V tot;
-  block_excl<Op>(Op::local(a, p), s, tot);
-  if (threadIdx.x == 0) a.agg[blockIdx.x] = tot;
+  block_excl<Op>(Op::local(a, p, stage + (threadIdx.x >> 6) * 64 * 8), s);
+  if (threadIdx.x == 0) a.agg[blockIdx.x] = s[kScanT - 1];
 }
 
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_b(typename Op::Args a) {
   using V = typename Op::V;
-  __shared__ V s[kScanT];
+  __shared__ V s[kScanT + 1];
   if (Op::stop(a)) return;
   const uint32_t t = threadIdx.x, nb = a.nblk;
   const uint32_t per = (nb + kScanT - 1) / kScanT, lo = min(nb, t * per), hi = min(nb, lo + per);
   V r = Op::identity();
   for (uint32_t i = lo; i < hi; ++i) r = Op::combine(r, a.agg[i]);
-  V tot;
-  V ex = block_excl<Op>(r, s, tot);
+  V ex = block_excl<Op>(r, s);
   for (uint32_t i = lo; i < hi; ++i) {
     a.carry[i] = ex;
     ex = Op::combine(ex, a.agg[i]);
@@ -118,13 +148,12 @@ __global__ __launch_bounds__(kScanT) void k_scan_b(typename Op::Args a) {
 
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_c(typename Op::Args a) {
-  __shared__ typename Op::V s[kScanT];
+  __shared__ typename Op::V s[kScanT + 1];
   __shared__ uint4 stage[4 * 64 * 8];  // per-wave record stage (wave_store128)
   if (Op::stop(a)) return;
   const uint32_t p = blockIdx.x * kScanT + threadIdx.x;
-  const typename Op::V loc = Op::local(a, p);
-  typename Op::V tot;
-  typename Op::V ex = block_excl<Op>(loc, s, tot);
+  const typename Op::V loc = Op::local(a, p, stage + (threadIdx.x >> 6) * 64 * 8);
+  typename Op::V ex = block_excl<Op>(loc, s);
   ex = Op::combine(a.carry[blockIdx.x], ex);
   Op::emit(a, p, ex, loc, stage + (threadIdx.x >> 6) * 64 * 8);
 }
@@ -164,7 +193,7 @@ struct RtxOp {
     row = k >> 22;
     w = row == kRNullRow ? a.W : (uint32_t)(row / a.S);
   }
-  __device__ static V local(const Args& a, uint32_t p) {
+  __device__ static V local(const Args& a, uint32_t p, uint4*) {
     uint64_t row, prow = ~0ull;
     uint32_t w, pw = ~0u;
     row_of(a, p, row, w);
@@ -403,7 +432,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
 #pragma unroll
         for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
         uint4* dst = dry_s ? dry : sslot + (uint64_t)k * 64;
-        st_row<true>(&dst[lane], cur);
+        st_drop(dst, lane, cur);
         dry_s = false;
       }
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
@@ -427,7 +456,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
     uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
     keep4(x);
   }
-  for (uint32_t k = ns + wave; k < a.c; k += 4) st_row<true>(&sslot[(uint64_t)k * 64 + lane], make_uint4(0, 0, 0, 0));
+  for (uint32_t k = ns + wave; k < a.c; k += 4) st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
   if (a.xon && w % a.xk == a.xrot) {
     __syncthreads();
     if (wave == 0 && lane < 8 * a.xep) {
@@ -487,8 +516,8 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
     atomicOr(&a.scal->error, 8u);
   }
 #pragma unroll
-  for (int u = 0; u < U; ++u) st_row<true>(&a.pbuf[(p0 + u) * 64 + lane], v[u]);
-  if (lane < (uint32_t)U) a.psd[p0 + lane] = SEAL ? sct : xor4(sd, ks);
+  for (int u = 0; u < U; ++u) st_drop(a.pbuf, (p0 + u) * 64 + lane, v[u]);
+  if (lane < (uint32_t)U) st_drop(a.psd, p0 + lane, SEAL ? sct : xor4(sd, ks));
 }
 
 // ------------------------------------------------------------- k_rr1
@@ -518,6 +547,8 @@ struct Rr1Args {
   Rr1V* carry;
   const Scal* scal;
   uint32_t B, nblk, xbase, S;
+  uint4* g;                // B x 256 B: what pass 0 gathered, by position
+  uint32_t pass;           // 0: k_scan_a gathers; 1: k_scan_c reads g
 };
 
 struct Rr1Op {
@@ -547,23 +578,54 @@ struct Rr1Op {
     r.nd = sel4(bn, b.nd, a.nd);
     return r;
   }
-  __device__ static V local(const Args& a, uint32_t p) {
+  // Pass 0 gathers the op's lines (ROp, request image line 0, snapshot line
+  // 0) once and stores what both passes need by position: g[p] = {kind,
+  // status}, id, image words 0..4, snapshot words 0..4.  Pass 1 and emit read
+  // g (addresses that do not depend on the data), so no data-dependent line
+  // is read twice in the batch.
+  __device__ static void gathered(const Args& a, uint32_t p, uint4* stage, uint4 (&g)[16]) {
+    if (a.pass == 0) {
+      const uint4 rp = a.rpos[p];
+      const uint32_t seq = rp.x & kSeqMask;
+      const bool head = rp.x & kPosHead;
+      uint4 rr[8], im[8], sn[8];  // ROp: {status, slot, kind, flags}, id, ...
+      wave_load128(stage, reinterpret_cast<const uint4*>(a.rop + seq), rr);
+      wave_load128(stage, a.img + (uint64_t)seq * 64, im);
+      wave_load128(stage, head ? a.snap + (uint64_t)rp.y * 64 : a.snapdummy + (uint64_t)p * 64, sn);
+      g[0] = make_uint4(rr[0].z, rr[0].x, 0u, 0u);
+      g[1] = rr[1];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        g[2 + i] = im[i];
+        g[7 + i] = sn[i];
+      }
+#pragma unroll
+      for (int i = 12; i < 16; ++i) g[i] = make_uint4(0, 0, 0, 0);
+      uint4 h0[8], h1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        h0[i] = g[i];
+        h1[i] = g[8 + i];
+      }
+      wave_store128(stage, a.g, 2ull * p, h0);
+      wave_store128(stage, a.g, 2ull * p + 1, h1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[i] = a.g[(uint64_t)p * 16 + i];
+    }
+  }
+  __device__ static V local(const Args& a, uint32_t p, uint4* stage) {
     const uint4 rp = a.rpos[p];
-    const uint32_t seq = rp.x & kSeqMask;
     const bool head = rp.x & kPosHead, null = rp.x & kPosNull;
-    const ROp& r = a.rop[seq];
-    const uint32_t kind = r.kind, st = r.status;
-    const uint4* im = a.img + (uint64_t)seq * 64;
-    const uint4* sn = head ? a.snap + (uint64_t)rp.y * 64 : a.snapdummy + (uint64_t)p * 64;
+    uint4 g[16];
+    gathered(a, p, stage, g);
+    const uint32_t kind = g[0].x, st = g[0].y;
     V v = identity();
     v.reset = (head || null) ? 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const uint4 s = sn[i];
-      v.r0[i] = sel4(head, s, make_uint4(0, 0, 0, 0));
-    }
-    const uint4 id = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
-    const uint4 q1 = im[1], q2 = im[2], q3 = im[3], q4 = im[4];
+    for (int i = 0; i < 5; ++i) v.r0[i] = sel4(head, g[7 + i], make_uint4(0, 0, 0, 0));
+    const uint4 id = g[1];
+    const uint4 q1 = g[3], q2 = g[4], q3 = g[5], q4 = g[6];
     v.nd_valid = (!null && kind == KIND_NEXT_DEL && st == kPending) ? 1u : 0u;
     v.nd = id;
     v.cr_valid = (!null && kind == KIND_CREATE && st == kPending) ? 1u : 0u;
@@ -578,18 +640,18 @@ struct Rr1Op {
     const uint4 rp = a.rpos[p];
     const uint32_t seq = rp.x & kSeqMask;
     const bool head = rp.x & kPosHead, last = rp.x & kPosLast, null = rp.x & kPosNull;
-    const ROp& r = a.rop[seq];
-    const uint32_t kind = r.kind;
-    const uint4* im = a.img + (uint64_t)seq * 64;
-    const uint4 qid = im[0], q1 = im[1], q2 = im[2], q3 = im[3], q4 = im[4];
+    uint4 g[16];
+    gathered(a, p, stage, g);  // pass 1: the position-indexed copy
+    const uint32_t kind = g[0].x, rstatus = g[0].y;
+    const uint4 qid = g[2], q1 = g[3], q2 = g[4], q3 = g[5], q4 = g[6];
     const V in = combine(ex, loc);  // this op's own head / pop / create included
     const bool r0_exists = nz4(in.r0[0]);
-    const uint4 rid = make_uint4(r.id[0], r.id[1], r.id[2], r.id[3]);
+    const uint4 rid = g[1];
     // the pop of a next-message DELETE succeeds on a row that holds its id
     const bool nd_ok = in.nd_valid && r0_exists && eq4(in.nd, in.r0[0]);
     const bool is_next = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
     const bool is_create = kind == KIND_CREATE;
-    uint32_t status = r.status, setk = kSetNone, flags = 0;
+    uint32_t status = rstatus, setk = kSetNone, flags = 0;
     uint4 ident[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) ident[i] = in.r0[i];
@@ -776,26 +838,43 @@ __global__ __launch_bounds__(256) void k_vscan_b3(typename Op::Args a) {
   vwalk_records<Op>(a.vagg, lo, hi, cf, cv, a.vcarry);
 }
 
-// Phase C prologue: the carry into the first of this wave's 16 ops (block
-// carry, then the aggregates of the block's earlier waves through LDS).  Each
-// wave reads one value of its own ops here, which its walk re-reads.
+// Phase C prologue, second half: given the aggregate (f, v) of this wave's
+// 16 ops, the carry into its first op (block carry, then the aggregates of
+// the block's earlier waves through LDS).
+template <class Op>
+__device__ inline void vscan_carry_tail(const typename Op::Args& a, uint4 (*s_v)[64], uint4* s_f,
+                                        uint4 f, uint4 v, uint4& cf, uint4& cv) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x;
+  s_v[wave][lane] = v;
+  if (lane == 0) s_f[wave] = f;
+  __syncthreads();
+  const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
+  cf = uni4(c[0]);
+  cv = c[8 + lane];
+  for (uint32_t k = 0; k < wave; ++k) {
+    const uint4 e = s_f[k];
+    cv = Op::v_combine(cf, cv, e, s_v[k][lane]);
+    cf = Op::f_combine(cf, e);
+  }
+}
+
+// Phase C prologue: the carry into the first of this wave's 16 ops.  Merge
+// scans (values from position-indexed records) only; select scans read their
+// ops' lines once into registers and use vscan_carry_tail (a data-dependent
+// line read twice in one kernel hits or misses L2 depending on what else the
+// XCD read, which made FETCH_SIZE depend on the data).
 template <class Op>
 __device__ inline void vscan_carry_in(const typename Op::Args& a, uint4 (*s_v)[64], uint4* s_f,
                                       uint4& cf, uint4& cv) {
+  static_assert(!Op::kSelect, "select scans: read the lines once, then vscan_carry_tail");
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x, p0 = b * kVBlk + wave * 16;
-  uint4 f, v = make_uint4(0, 0, 0, 0);
-  if (Op::kSelect) {
-    uint32_t d;
-    f_walk<Op>(a, p0, 16, f, d);
-    v = Op::value_of(a, p0 + d, f);
-  } else {
-    f = Op::f_identity();
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint4 e = Op::f_of(a, p0 + j);
-      v = Op::v_combine(f, v, e, Op::value_of(a, p0 + j, e));
-      f = Op::f_combine(f, e);
-    }
+  uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint4 e = Op::f_of(a, p0 + j);
+    v = Op::v_combine(f, v, e, Op::value_of(a, p0 + j, e));
+    f = Op::f_combine(f, e);
   }
   s_v[wave][lane] = v;
   if (lane == 0) s_f[wave] = f;
@@ -921,17 +1000,43 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   __shared__ uint4 s_v[4][64];
   __shared__ uint4 s_f[4];
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  uint4 cf, cv;
-  vscan_carry_in<Rr2Op>(a, s_v, s_f, cf, cv);
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  // every line of this wave's ops, read once: snapshot (heads) or own dummy
+  // line, and request image
+  uint4 svs[16], ivs[16];
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const RsHdr h = rs_hdr(a.rs, p0 + j);
+    const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
+    svs[j] = ld_row<false>(&sp[lane]);
+    ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+  }
+  uint4 cf, cv;
+  {  // the wave's aggregate from registers, then the carry
+    uint4 f = Rr2Op::f_identity(), xs = svs[0], xi = ivs[0];
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint4 e = Rr2Op::f_of(a, p0 + j);
+      const bool t = Rr2Op::takes_b(f, e);
+      d = t ? j : d;
+      xs = sel4(t, svs[j], xs);
+      xi = sel4(t, ivs[j], xi);
+      f = Rr2Op::f_combine(f, e);
+    }
+    const RsHdr hd = rs_hdr(a.rs, p0 + d);
+    const bool from_snap = (hd.flags & kRsHead) && rs_setkind(hd.flags) != kSetRec;
+    const uint4 x = sel4(from_snap, xs, xi);
+    const uint4 v = Rr2Op::own_value(hd, x, x, Rr2Op::ident_of(a, p0 + d));
+    vscan_carry_tail<Rr2Op>(a, s_v, s_f, f, sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v), cf, cv);
+  }
   uint4 sd = make_uint4(0, 0, 0, 0);
+#pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
     const RsHdr h = rs_hdr(a.rs, p);
     const bool head = h.flags & kRsHead;
-    const uint4* sp = head ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)p * 64;
-    const uint4 sv = ld_row<false>(&sp[lane]);
-    const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+    const uint4 sv = svs[j], iv = ivs[j];
     const uint4 idv = Rr2Op::ident_of(a, p);
     // the row state before this op
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 1u, 0u), cf);
@@ -954,17 +1059,17 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
     cf = Rr2Op::f_combine(cf, e);
     // an expiry delete is the last op of its row: it only decides the final state
     const uint4 fin = sel4((h.flags & kRsExpiry) && ok, make_uint4(0, 0, 0, 0), cv);
-    uint4* dst = a.resp + (uint64_t)h.seq * (kRespSlot / 16);
-    dst[lane] = resp;
+    const uint64_t r0 = (uint64_t)h.seq * (kRespSlot / 16);
+    st_drop(a.resp, r0 + lane, resp);
     if (lane < 8) {
       const uint4 t = make_uint4(lane == 0 ? status : 0u, 0, 0, 0);
-      dst[64 + lane] = t;
-      reinterpret_cast<uint4*>(a.rres)[(uint64_t)h.seq * 8 + lane] = t;
+      st_drop(a.resp, r0 + 64 + lane, t);
+      st_drop(a.rres, (uint64_t)h.seq * 8 + lane, t);
     }
-    st_row<true>(&a.pbuf[(uint64_t)p * 64 + lane], fin);
+    st_drop(a.pbuf, (uint64_t)p * 64 + lane, fin);
     sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, 0u), sd);
   }
-  if (lane < 16) a.psd[p0 + lane] = sd;
+  if (lane < 16) st_drop(a.psd, p0 + lane, sd);
 }
 
 }  // namespace gvs

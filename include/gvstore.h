@@ -252,6 +252,50 @@ int gvs_last_timings(gvs_handle *h, const char **names, float *ms, int cap);
 const char *gvs_last_error(gvs_handle *h);
 const char *gvs_version(void);
 
+/* ---------------------------------------------------------------------------
+ * Block store: the mc-oblivious-traits ORAM<1024> surface, batched
+ * (ORAM::access(index, f) with f: FnOnce(&mut A64Bytes<1024>)).
+ *
+ * `capacity` 1 KiB blocks, all zero initially, kept in the message table's
+ * layout and updated by the same fixed-slot table pass.  One
+ * call applies n <= max_batch ops in submission order: GVS_ORAM_READ returns
+ * the block, GVS_ORAM_WRITE returns the block and then replaces it with
+ * `data` (the callback's view before it writes).  The launch sequence, grids,
+ * HBM bytes and kernel durations depend only on (capacity, max_batch, n).  An
+ * index >= capacity or an unknown op fails the whole call with
+ * GVS_ERR_INVALID_ARG and applies nothing.
+ * ------------------------------------------------------------------------- */
+typedef struct gvs_oram gvs_oram;
+
+#define GVS_ORAM_READ 0u
+#define GVS_ORAM_WRITE 1u
+
+typedef struct gvs_oram_config {
+  uint64_t capacity;       /* blocks: power of two in [4096, 2^32] */
+  uint32_t max_batch;      /* power of two in [1024, 2^19] */
+  uint32_t device;
+  uint8_t secret_key[32];  /* storage keys when flags has GVS_FLAG_AUTH_STORAGE */
+  uint32_t flags;
+  uint32_t reserved[3];    /* zero */
+} gvs_oram_config;         /* 64 B */
+
+typedef struct gvs_block_op {
+  uint64_t index;
+  uint32_t op;             /* GVS_ORAM_READ / GVS_ORAM_WRITE */
+  uint32_t reserved;
+  uint8_t data[1024];      /* GVS_ORAM_WRITE: the new block */
+} gvs_block_op;            /* 1040 B */
+
+int gvs_oram_create(const gvs_oram_config *cfg, gvs_oram **out);
+int gvs_oram_destroy(gvs_oram *o);
+/* ops: n host gvs_block_op; out: n x 1024 bytes, the block each op saw. */
+int gvs_oram_access_batch(gvs_oram *o, const gvs_block_op *ops, uint32_t n, uint8_t *out);
+/* The same with device buffers. */
+int gvs_oram_access_batch_device(gvs_oram *o, const void *d_ops, uint32_t n, void *d_out);
+int gvs_oram_set_timing(gvs_oram *o, int on);
+int gvs_oram_last_timings(gvs_oram *o, const char **names, float *ms, int cap);
+const char *gvs_oram_last_error(gvs_oram *o);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,6 +74,12 @@ def lib():
         L.gvo_aes128_encrypt.argtypes = [cp, cp, cp]
         L.gvo_blake2b.argtypes = [cp, ctypes.c_size_t, cp, cp, ctypes.c_size_t, cp, ctypes.c_size_t]
         L.gvo_storage_keys.argtypes = [cp, cp, cp]
+        L.gvo_oram_create.argtypes = [u64]
+        L.gvo_oram_create.restype = vp
+        L.gvo_oram_destroy.argtypes = [vp]
+        L.gvo_oram_access_batch.argtypes = [vp, vp, u32, vp]
+        L.gvo_oram_access_batch.restype = ctypes.c_int
+        L.gvo_oram_read_all.argtypes = [vp, vp]
         L.gvo_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
         L.gvo_id_encode_shard.argtypes = [ctypes.c_char_p, u32, u32, u64, ctypes.c_char_p]
         L.gvo_id_decode_shard.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, u32,
@@ -381,3 +387,35 @@ class PathOramModel:
     @property
     def oram_accesses(self):
         return self.L.gvp_oram_accesses(self.m)
+
+
+class OramModel:
+    """Sequential block store (oracle/gvs_kv.c): the ORAM::access semantics."""
+
+    def __init__(self, capacity):
+        self.L = lib()
+        self.n = capacity
+        self.o = self.L.gvo_oram_create(capacity)
+        if not self.o:
+            raise MemoryError("oracle block store")
+
+    def access(self, ops):
+        """ops: abi.BLOCK_OP_DTYPE array -> (n, 1024) uint8 blocks seen, or None
+        when the batch is invalid (nothing applied)."""
+        ops = np.ascontiguousarray(ops)
+        out = np.zeros((len(ops), 1024), np.uint8)
+        rc = self.L.gvo_oram_access_batch(self.o, ops.ctypes.data, len(ops), out.ctypes.data)
+        return None if rc else out
+
+    def blocks(self):
+        out = np.zeros((self.n, 1024), np.uint8)
+        self.L.gvo_oram_read_all(self.o, out.ctypes.data)
+        return out
+
+    def close(self):
+        if self.o:
+            self.L.gvo_oram_destroy(self.o)
+            self.o = None
+
+    def __del__(self):
+        self.close()
