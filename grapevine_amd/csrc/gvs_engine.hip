@@ -104,7 +104,7 @@ struct Engine {
   uint4* rsb = nullptr;      // B x 128 B
   uint4* snap = nullptr;     // W*c x 1 KiB
   uint4* pbuf = nullptr;     // B x 1 KiB final row states, by sorted position
-  uint4* psd = nullptr;      // B side entries of P (target row, valid)
+  uint4* psd = nullptr;      // B side entries of P (target row, valid), 128 B each
   uint4* ptag = nullptr;     // B tags of P (authenticated storage)
   uint4* pdum = nullptr;     // W*c x 1 KiB read for unused slots
   uint4* snapdummy = nullptr;  // B x 1 KiB
@@ -115,6 +115,11 @@ struct Engine {
   Rr1V* rr1_carry = nullptr;
   uint4* rr1g = nullptr;     // B x 256 B (gvs_txn.h Rr1Op::gathered)
   uint4* m2g = nullptr;      // B x 128 B (gvs_mtx.h k_m2g)
+  uint4* idn = nullptr;      // B x 128 B request identity lines (k_meta -> k_rr1)
+  uint4* snapid = nullptr;   // W*c x 128 B snapshot identity lines (k_rpass2 -> k_rr1)
+  uint4* siddummy = nullptr; // B x 128 B
+  uint4* vraw = nullptr;     // B/64 x 2 KiB: raw rows of each block's defining op (k_rr2)
+  uint4* vdef = nullptr;     // B/64 x 128 B: its position in the block
   uint4* vagg = nullptr, *vagg2 = nullptr, *vcarry2 = nullptr, *vcarry = nullptr;
   // fixed-slot mailbox passes (gvs_mtx.h)
   uint32_t cm = 0;           // group slots per mailbox partition
@@ -445,7 +450,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(rsb, (uint64_t)B * 8);
     A(snap, WC * 64);
     A(pbuf, (uint64_t)B * 64);
-    A(psd, B);
+    A(psd, (uint64_t)B * 8);
     if (h->auth) A(ptag, B);
     A(pdum, WC * 64);
     A(snapdummy, (uint64_t)B * 64);
@@ -456,6 +461,11 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(rr1_carry, B / kScanT);
     A(rr1g, (uint64_t)B * 16);
     A(m2g, (uint64_t)B * 8);
+    A(idn, (uint64_t)B * 8);
+    A(snapid, WC * 8);
+    A(siddummy, (uint64_t)B * 8);
+    A(vraw, (uint64_t)(B / kVBlk) * 128);
+    A(vdef, (uint64_t)(B / kVBlk) * 8);
     const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
     A(vagg, nvb * kVLineU4);
     A(vcarry, nvb * kVLineU4);
@@ -729,7 +739,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
                      (const uint4*)(e.X ? e.xb2[e.par ^ 1] : nullptr), xbase);
   mark(h, "copy");
   {
-    MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, n, B, e.Q, e.logQ, e.N, e.kc, xbase};
+    MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, n, B, e.Q, e.logQ, e.N, e.kc, xbase, e.idn};
     hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
   }
   mark(h, "meta");
@@ -797,6 +807,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.psd = e.psd;
   a.pdum = e.pdum;
   a.snap = e.snap;
+  a.snapid = e.snapid;
   a.dry = e.dryb;
   a.scal = e.scal;
   a.W = e.W;
@@ -831,7 +842,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   mark(h, "rpass");
   {
     Rr1Args a{e.rpos, e.rop, e.img, e.snap, e.snapdummy, e.rsb, e.rr1_agg, e.rr1_carry, e.scal,
-              B,      B / kScanT, B - e.X, e.S, e.rr1g, 0u};
+              B,      B / kScanT, B - e.X, e.S, e.rr1g, 0u, e.idn, e.snapid, e.siddummy};
     hipLaunchKernelGGL(k_scan_a<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_b<Rr1Op>, dim3(1), dim3(kScanT), 0, s, a);
     a.pass = 1;
@@ -842,6 +853,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     Rr2Args a{};
     vscan_fields(a, e);
     a.rs = e.rsb;
+    a.vraw = e.vraw;
+    a.vdef = e.vdef;
     a.img = e.img;
     a.snap = e.snap;
     a.snapdummy = e.snapdummy;
@@ -1104,8 +1117,9 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   A(snap, WC * 64);
   A(snapdummy, (uint64_t)B * 64);
   A(pbuf, (uint64_t)B * 64);
-  A(psd, B);
+  A(psd, (uint64_t)B * 8);
   A(pdum, WC * 64);
+  A(snapid, WC * 8);
   A(dryb, (uint64_t)e.W * 64);
   A(rtx_agg, B / kScanT);
   A(rtx_carry, B / kScanT);
@@ -1432,7 +1446,7 @@ static int raw_region(gvs_handle* h, uint32_t shard, uint32_t region, void** bas
     // pipeline 2: the final states pending from the last batch, their side
     // entries and tags, and that batch's slot descriptors
     case 5: *base = e.pbuf; *size = (uint64_t)e.B * 1024; break;
-    case 6: *base = e.psd; *size = (uint64_t)e.B * 16; break;
+    case 6: *base = e.psd; *size = (uint64_t)e.B * 128; break;
     case 7: *base = e.ptag; *size = e.ptag ? (uint64_t)e.B * 16 : 0; break;
     case 8: *base = e.tbuf[e.par ^ 1]; *size = (uint64_t)e.W * e.c * 128; break;
     default: return GVS_ERR_INVALID_ARG;

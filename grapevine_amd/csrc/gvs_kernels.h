@@ -242,12 +242,19 @@ struct MetaArgs {
   uint64_t N;
   KeyCtx kc;
   uint32_t xbase;  // ops >= xbase: expiry deletes (type kTypeExpire) or padding
+  uint4* idn;      // B x 128 B: the image's first 80 B (id, sender, recipient), for k_rr1
 };
 
 __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4* row = a.img + (uint64_t)i * 64;
   uint4 c0 = row[0], c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4], c5 = row[5];
+  {  // the identity words k_rr1 gathers (so that it never re-reads image lines)
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 w[8] = {c0, c1, c2, c3, c4, z, z, z};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) st_drop(a.idn, (uint64_t)i * 8 + c, w[c]);
+  }
   const uint32_t raw = a.types[i];
   const bool is_x = i >= a.xbase;
   const uint32_t type = selu32(is_x & (raw == kTypeExpire), 4u, raw);  // DELETE

@@ -79,7 +79,7 @@ struct KvArgs {
   const uint4* snap;       // W*c slot snapshots
   const uint4* snapdummy;  // B x 1 KiB (non-heads read their own line)
   uint4* pbuf;             // B final states, by position
-  uint4* psd;              // B side entries {row lo, row hi, valid, 0}
+  uint4* psd;              // B x 128 B side entries {row lo, row hi, valid, 0}
   uint4* out;              // ORAM: n x 1 KiB (caller); OMAP: B x kRespSlot
   uint4* outdummy;         // ORAM: B x 1 KiB for padding ops
   uint32_t n, S, omap;
@@ -107,6 +107,7 @@ __device__ inline KvHdr kv_hdr(const KvArgs& a, uint32_t p) {
 struct KvOp {
   using Args = KvArgs;
   static constexpr bool kSelect = true;
+  static constexpr bool kStash = false;
   __device__ static uint4 f_identity() { return make_uint4(kTId, 0, 0, 0); }
   // a then b: function composition of the transforms
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
     st_drop(a.pbuf, (uint64_t)p * 64 + lane, v2);
     sd = sel4(lane == j, make_uint4((uint32_t)h.prow, (uint32_t)(h.prow >> 32), last ? 1u : 0u, 0u), sd);
   }
-  if (lane < 16) st_drop(a.psd, p0 + lane, sd);
+  if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);
 }
 
 }  // namespace gvs

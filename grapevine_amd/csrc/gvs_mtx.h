@@ -171,11 +171,12 @@ __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uin
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
     const int k = occ ? find_group_m(g, ng, hi, w1 >> 23) : -1;
-    if (occ) atomicAdd(s_occ, 1u);
-    if (k >= 0) {
-      g[k].slot = (int32_t)j;
-      g[k].len = (uint32_t)(w1 >> 1) & 63u;
-    }
+    atomicAdd(s_occ, occ ? 1u : 0u);
+    // rows without a group write the sink entry g[kGroupMax]: the same code
+    // runs whatever the batch holds (instruction fetch shows in FETCH_SIZE)
+    const uint32_t kk = k >= 0 ? (uint32_t)k : (uint32_t)kGroupMax;
+    g[kk].slot = (int32_t)j;
+    g[kk].len = (uint32_t)(w1 >> 1) & 63u;
     s_sg[j] = (int16_t)k;
     s_occb[j] = occ ? 1 : 0;
   }
@@ -207,7 +208,7 @@ __device__ inline uint32_t load_groups(const MArgs& a, uint32_t q, GroupM* g, ui
     G.mhi = h.w;
     G.pad[0] = G.pad[1] = 0;
     g[k] = G;
-    if (r0.x == a.stamp) atomicAdd(s_ng, 1u);
+    atomicAdd(s_ng, r0.x == a.stamp ? 1u : 0u);  // unconditional: no code path skipped
   }
   __syncthreads();
   return *s_ng;
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   // again; new recipients are admitted by the seq of their first create
   for (uint32_t k = tid; k < a.cm; k += 256) {
     const GroupM& G = g[k];
-    if (k < ng && G.slot >= 0 && G.len == min(G.n_del, G.len)) atomicAdd(&s_empt, 1u);
+    atomicAdd(&s_empt, (k < ng && G.slot >= 0 && G.len == min(G.n_del, G.len)) ? 1u : 0u);
   }
   __syncthreads();
   const uint32_t freeq = (a.Sr - s_occ) + s_empt;
@@ -331,6 +332,7 @@ struct M1rArgs {
 struct M1rOp {
   using Args = M1rArgs;
   static constexpr bool kSelect = true;
+  static constexpr bool kStash = false;
   __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
     return sel4(b.x != 0u, b, make_uint4(a.x, a.y + b.y, a.z + b.z, 0u));
@@ -444,6 +446,7 @@ struct M2rArgs {
 struct M2rOp {
   using Args = M2rArgs;
   static constexpr bool kSelect = false;
+  static constexpr bool kStash = false;
   __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
     return sel4(b.x != 0u, b, make_uint4(a.x, a.y | b.y, a.z | b.z, a.w + b.w));
@@ -533,14 +536,17 @@ __device__ inline uint4 m2_row(uint4 v, bool matched, uint32_t len, uint32_t dp,
   const bool keep = matched && lane >= 2 && i < len && i >= dp && !((mask >> i) & 1ull);
   const uint64_t km = __ballot(keep);
   const uint32_t nk = (uint32_t)__popcll(km);
-  if (keep) wst[mbcnt64(km)] = v;  // compaction through the wave's LDS stage
+  // compaction through the wave's LDS stage: survivors at [0, nk), every
+  // other lane after them (all lanes store: the same code runs whatever the
+  // row holds, and instruction fetch shows in FETCH_SIZE)
+  wst[keep ? mbcnt64(km) : nk + mbcnt64(~km)] = v;
   wave_lds_sync();
   const uint32_t r = lane - 2u;
-  uint4 out = make_uint4(0, 0, 0, 0);
-  if (lane >= 2 && r < nk) out = wst[min(r, 63u)];
+  const uint4 w = wst[min(r, 63u)];
+  uint4 out = sel4(lane >= 2 && r < nk, w, make_uint4(0, 0, 0, 0));
   const uint32_t ra = lane - 2u - nk;  // appended ids follow the survivors
   const uint4 a = shfl4(app, (int)(2u + min(ra, 61u)));
-  if (lane >= 2 + nk && ra < n_succ && lane < 64) out = a;
+  out = sel4(lane >= 2 + nk && ra < n_succ && lane < 64, a, out);
   wave_lds_sync();
   const uint32_t fl = nk + min(n_succ, GVS_MAILBOX_SLOTS - nk);
   out = sel4(lane < 2, sel4(matched, v, app), out);  // recipient key
@@ -561,8 +567,8 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   __shared__ uint16_t s_pfx[kSrMax + 1];
   __shared__ uint16_t s_gpfx[kGroupMax + 1];
   __shared__ uint8_t s_gflag[kGroupMax + 1];
-  __shared__ int16_t s_pend[kGroupMax];
-  __shared__ uint8_t s_ld[kGroupMax];
+  __shared__ int16_t s_pend[kGroupMax + 1];
+  __shared__ uint8_t s_ld[kGroupMax + 1];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -604,17 +610,16 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   __syncthreads();
   block_flag_scan(s_flag, a.Sr, s_pfx, s_w);
   block_flag_scan(s_gflag, a.cm, s_gpfx, s_w);
-  for (uint32_t k = tid; k < a.cm; k += 256)
-    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  for (uint32_t k = tid; k < a.cm; k += 256)  // groups not pending write the sink entry
+    s_pend[s_gflag[k] ? s_gpfx[k] : (uint32_t)kGroupMax] = (int16_t)k;
   __syncthreads();
   const uint32_t npend = s_gpfx[a.cm];
   if (tid == 0 && npend > s_pfx[a.Sr]) atomicOr(&a.scal->error, 2u);
   for (uint32_t j = tid; j < a.Sr; j += 256) {
-    int16_t pl = -1;
-    if (s_flag[j] && s_pfx[j] < npend) pl = s_pend[s_pfx[j]];
-    s_place[j] = pl;
+    const int16_t cand = s_pend[min((uint32_t)s_pfx[j], (uint32_t)kGroupMax)];
+    s_place[j] = (s_flag[j] && s_pfx[j] < npend) ? cand : (int16_t)-1;
     const int k = s_sg[j];
-    if (k >= 0 && g[k].fl == 0) atomicSub(&s_delta, 1u);
+    atomicSub(&s_delta, (k >= 0 && g[k >= 0 ? k : 0].fl == 0) ? 1u : 0u);
   }
   if (tid == 0) atomicAdd(&s_delta, npend);
   __syncthreads();
@@ -657,7 +662,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
       const uint4* rs = dry_run ? dry : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
       const uint4 app = ld_row<true>(&rs[lane]);
-      if (!dry_run && lane == 0) s_ld[ge] = 1;
+      if (lane == 0) s_ld[dry_run ? (uint32_t)kGroupMax : (uint32_t)ge] = 1;
       const bool matched = pl < 0;
       const uint32_t len = matched ? G.len : 0u;
       const uint32_t dp = min(G.n_del, len);
@@ -668,12 +673,10 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
         const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
                                                 (uint32_t)(w1 >> 32)),
                              make_uint4(0, 0, 0, 0));
-      if (!dry_run) {
 #pragma unroll
-        for (int uu = 0; uu < kMU; ++uu) {
-          v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
-          sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
-        }
+      for (int uu = 0; uu < kMU; ++uu) {  // the dry run has bit 0: no change
+        v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
+        sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
       }
       dry_run = false;
     }
@@ -706,7 +709,8 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     uint4 x = ld_row<true>(&res[(uint64_t)k * kVLineU4 + 8 + lane]);
     keep4(x);
   }
-  if (tid == 0 && s_delta)
+  // every workgroup adds, zero included: a fixed set of atomics
+  if (tid == 0)
     atomicAdd((unsigned long long*)&a.scal->n_mailboxes, (unsigned long long)(int64_t)(int32_t)s_delta);
 }
 

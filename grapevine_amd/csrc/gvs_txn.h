@@ -244,9 +244,10 @@ struct R2Args {
   const uint4* tprev;  // the previous applied batch's
   uint32_t stamp_cur, stamp_prev;
   const uint4* pbuf;   // B final row states of the previous batch, by its sorted position
-  const uint4* psd;    // B: their target rows (x, y = physical row, z = valid)
+  const uint4* psd;    // B x 128 B: their target rows (x, y = physical row, z = valid), one line each
   const uint4* pdum;   // W*c x 1 KiB read for the slots no row uses
   uint4* snap;         // W*c snapshots for this batch
+  uint4* snapid;       // W*c x 128 B: each snapshot's first line (identity), for k_rr1
   uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
   Scal* scal;
   uint32_t W, S, c;
@@ -417,8 +418,10 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
         const uint32_t pos = s_pp[(uint32_t)k & (kSlotMax - 1u)];
         const uint4* src = dry_p ? dry : a.pbuf + (uint64_t)pos * 64;
         const uint4 x = ld_row<true>(&src[lane]);
-        const uint4 sd = uni4(dry_p ? dry[0] : a.psd[pos]);
-        if (AUTH && !dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
+        if (AUTH) {  // the final state must be the one sealed for this row
+          const uint4 sd = uni4(dry_p ? dry[0] : a.psd[(uint64_t)pos * 8]);
+          if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
         dry_p = false;
@@ -433,6 +436,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
         for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
         uint4* dst = dry_s ? dry : sslot + (uint64_t)k * 64;
         st_drop(dst, lane, cur);
+        if (lane < 8) st_drop(dry_s ? dry : a.snapid + (sbase + (uint64_t)k) * 8, lane, cur);
         dry_s = false;
       }
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
@@ -456,7 +460,10 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
     uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
     keep4(x);
   }
-  for (uint32_t k = ns + wave; k < a.c; k += 4) st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
+  for (uint32_t k = ns + wave; k < a.c; k += 4) {
+    st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
+    if (lane < 8) st_drop(a.snapid, (sbase + k) * 8 + lane, make_uint4(0, 0, 0, 0));
+  }
   if (a.xon && w % a.xk == a.xrot) {
     __syncthreads();
     if (wave == 0 && lane < 8 * a.xep) {
@@ -501,7 +508,7 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
 #pragma unroll
   for (int u = 0; u < U; ++u) v[u] = ld_row<true>(&a.pbuf[(p0 + u) * 64 + lane]);
   const uint4 ks = ctr_keystream(a.sc.rk, lds_te(s_te), 2u, p0 + (lane & 15u), a.ep, 64u);
-  const uint4 sd = a.psd[p0 + (lane & 15u)];
+  const uint4 sd = a.psd[(p0 + (lane & 15u)) * 8];
   const uint4 sct = SEAL ? xor4(sd, ks) : sd;  // side ciphertext
   if (lane < (uint32_t)U) st[U * 4 * kSegU4 + lane] = sct;
   wave_lds_sync();
@@ -517,7 +524,7 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) st_drop(a.pbuf, (p0 + u) * 64 + lane, v[u]);
-  if (lane < (uint32_t)U) st_drop(a.psd, p0 + lane, SEAL ? sct : xor4(sd, ks));
+  if (lane < (uint32_t)U) st_drop(a.psd, (p0 + lane) * 8, SEAL ? sct : xor4(sd, ks));
 }
 
 // ------------------------------------------------------------- k_rr1
@@ -549,6 +556,9 @@ struct Rr1Args {
   uint32_t B, nblk, xbase, S;
   uint4* g;                // B x 256 B: what pass 0 gathered, by position
   uint32_t pass;           // 0: k_scan_a gathers; 1: k_scan_c reads g
+  const uint4* idn;        // B x 128 B: request identity lines (k_meta)
+  const uint4* snapid;     // W*c x 128 B: snapshot identity lines (k_rpass2)
+  const uint4* siddummy;   // B x 128 B (non-heads read their own)
 };
 
 struct Rr1Op {
@@ -578,8 +588,9 @@ struct Rr1Op {
     r.nd = sel4(bn, b.nd, a.nd);
     return r;
   }
-  // Pass 0 gathers the op's lines (ROp, request image line 0, snapshot line
-  // 0) once and stores what both passes need by position: g[p] = {kind,
+  // Pass 0 gathers the op's lines (ROp, request identity, snapshot identity:
+  // copies kept for this pass, so k_rr2 reads the image and snapshot rows for
+  // the first time) once and stores what both passes need by position: g[p] = {kind,
   // status}, id, image words 0..4, snapshot words 0..4.  Pass 1 and emit read
   // g (addresses that do not depend on the data), so no data-dependent line
   // is read twice in the batch.
@@ -590,8 +601,8 @@ struct Rr1Op {
       const bool head = rp.x & kPosHead;
       uint4 rr[8], im[8], sn[8];  // ROp: {status, slot, kind, flags}, id, ...
       wave_load128(stage, reinterpret_cast<const uint4*>(a.rop + seq), rr);
-      wave_load128(stage, a.img + (uint64_t)seq * 64, im);
-      wave_load128(stage, head ? a.snap + (uint64_t)rp.y * 64 : a.snapdummy + (uint64_t)p * 64, sn);
+      wave_load128(stage, a.idn + (uint64_t)seq * 8, im);
+      wave_load128(stage, head ? a.snapid + (uint64_t)rp.y * 8 : a.siddummy + (uint64_t)p * 8, sn);
       g[0] = make_uint4(rr[0].z, rr[0].x, 0u, 0u);
       g[1] = rr[1];
 #pragma unroll
@@ -745,7 +756,23 @@ __global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= a.nvb) return;
   uint4 f, v = make_uint4(0, 0, 0, 0);
-  if (Op::kSelect) {
+  if constexpr (Op::kStash) {
+    // the block's 64 position records read once into LDS; the defining op's
+    // raw rows are kept for phase C (Op::value_stash)
+    __shared__ uint4 s_rec[4][kVBlk * 8];
+    uint4* rec = s_rec[threadIdx.x >> 6];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) rec[i * 64 + lane_id()] = Op::rec_line(a, b * kVBlk * 8 + i * 64 + lane_id());
+    wave_lds_sync();
+    uint32_t d = 0;
+    f = Op::f_identity();
+    for (uint32_t j = 0; j < kVBlk; ++j) {
+      const uint4 e = Op::f_of_rec(rec + j * 8);
+      d = Op::takes_b(f, e) ? j : d;
+      f = Op::f_combine(f, e);
+    }
+    v = Op::value_stash(a, b, d, f, rec + d * 8);
+  } else if constexpr (Op::kSelect) {
     uint32_t d;
     f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
     v = Op::value_of(a, b * kVBlk + d, f);
@@ -913,11 +940,13 @@ struct Rr2Args {
   const uint4* snap;
   const uint4* snapdummy;
   uint4* pbuf;            // B final states, by sorted position
-  uint4* psd;             // B: {physical row lo, hi, valid (the row's last op), 0}
+  uint4* psd;             // B x 128 B: {physical row lo, hi, valid (the row's last op), 0}
   uint4* resp;            // B internal response slots (kRespSlot)
   RRes* rres;
   uint32_t B;
   uint64_t cutoff;
+  uint4* vraw;            // B/64 x 2 KiB: the snapshot and image rows of each block's defining op
+  uint4* vdef;            // B/64 x 128 B: {its position in the block}
 };
 
 // the per-position record words every lane needs (RS lines 0 and 1)
@@ -969,12 +998,29 @@ struct Rr2Op {
   }
   // the aggregate value: one 1 KiB read, always a line phase C also reads
   // (the head's snapshot, or the op's request image)
-  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 f) {
-    const RsHdr h = rs_hdr(a.rs, p);
+  // k_vscan_a: the value of block b's defining op d.  Both of its rows are
+  // read here and kept in vraw, and k_rr2_c takes them from there instead
+  // of reading them again (a row read twice in a batch hits or misses L2
+  // depending on when, which made FETCH_SIZE depend on the data).
+  static constexpr bool kStash = true;
+  __device__ static uint4 rec_line(const Args& a, uint64_t i) { return a.rs[i]; }
+  __device__ static RsHdr hdr_of_rec(const uint4* r) {
+    const uint4 w0 = uni4(r[0]), w1 = uni4(r[1]);
+    return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z};
+  }
+  __device__ static uint4 f_of_rec(const uint4* r) { return f_of_hdr(hdr_of_rec(r)); }
+  __device__ static uint4 value_stash(const Args& a, uint32_t b, uint32_t d, uint4 f, const uint4* r) {
+    const uint32_t lane = lane_id(), p = b * kVBlk + d;
+    const RsHdr h = hdr_of_rec(r);
+    const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)p * 64;
+    const uint4 sv = ld_row<false>(&sp[lane]);
+    const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+    st_drop(a.vraw, (uint64_t)b * 128 + lane, sv);
+    st_drop(a.vraw, (uint64_t)b * 128 + 64 + lane, iv);
+    if (lane < 8) st_drop(a.vdef, (uint64_t)b * 8 + lane, make_uint4(lane == 0 ? d : 0u, 0, 0, 0));
     const bool from_snap = (h.flags & kRsHead) && rs_setkind(h.flags) != kSetRec;
-    const uint4* src = from_snap ? a.snap + (uint64_t)h.slot * 64 : a.img + (uint64_t)h.seq * 64;
-    const uint4 x = ld_row<false>(&src[lane_id()]);
-    const uint4 v = own_value(h, x, x, ident_of(a, p));
+    const uint4 x = sel4(from_snap, sv, iv);
+    const uint4 v = own_value(h, x, x, r[2 + min(lane, 4u)]);
     return sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v);
   }
 };
@@ -999,45 +1045,81 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   if (a.scal->error) return;
   __shared__ uint4 s_v[4][64];
   __shared__ uint4 s_f[4];
+  __shared__ uint4 s_rs[4][16 * 8];  // each wave's 16 RS records
+  __shared__ uint4 s_blk[8 + kVLineU4];  // the block's vdef line and carry record
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
-  // every line of this wave's ops, read once: snapshot (heads) or own dummy
-  // line, and request image
+  const uint32_t b = blockIdx.x, p0 = b * kVBlk + wave * 16;
+  // Every global line this kernel needs is read once: a line read twice in a
+  // kernel hits or misses L2 depending on the traffic in between, whose
+  // addresses depend on the data (FETCH_SIZE would).  RS records and the
+  // block's records go through LDS.
+  s_rs[wave][lane] = a.rs[(uint64_t)p0 * 8 + lane];
+  s_rs[wave][64 + lane] = a.rs[(uint64_t)p0 * 8 + 64 + lane];
+  if (wave == 0) {
+    if (lane < 8) s_blk[lane] = a.vdef[(uint64_t)b * 8 + lane];
+    const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
+    s_blk[8 + 8 + lane] = c[8 + lane];
+    if (lane < 8) s_blk[8 + lane] = c[lane];
+  }
+  __syncthreads();
+  auto hdr = [&](uint32_t j) {
+    const uint4 w0 = uni4(s_rs[wave][j * 8]), w1 = uni4(s_rs[wave][j * 8 + 1]);
+    return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z};
+  };
+  auto ident = [&](uint32_t j) { return s_rs[wave][j * 8 + 2 + min(lane, 4u)]; };
+  // the rows: snapshot (heads) or own dummy row, and request image; the
+  // block's defining op's rows come from vraw (k_vscan_a read them)
+  const uint32_t pdef = b * kVBlk + uni4(s_blk[0]).x;
   uint4 svs[16], ivs[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    const RsHdr h = rs_hdr(a.rs, p0 + j);
-    const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
-    svs[j] = ld_row<false>(&sp[lane]);
-    ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+    const RsHdr h = hdr(j);
+    if (p0 + j == pdef) {
+      svs[j] = a.vraw[(uint64_t)b * 128 + lane];
+      ivs[j] = a.vraw[(uint64_t)b * 128 + 64 + lane];
+    } else {
+      const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
+      svs[j] = ld_row<false>(&sp[lane]);
+      ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
+    }
   }
   uint4 cf, cv;
   {  // the wave's aggregate from registers, then the carry
-    uint4 f = Rr2Op::f_identity(), xs = svs[0], xi = ivs[0];
+    uint4 f = Rr2Op::f_identity(), xs = svs[0], xi = ivs[0], id = ident(0);
     uint32_t d = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
-      const uint4 e = Rr2Op::f_of(a, p0 + j);
+      const uint4 e = Rr2Op::f_of_hdr(hdr(j));
       const bool t = Rr2Op::takes_b(f, e);
       d = t ? j : d;
       xs = sel4(t, svs[j], xs);
       xi = sel4(t, ivs[j], xi);
+      id = sel4(t, ident(j), id);
       f = Rr2Op::f_combine(f, e);
     }
-    const RsHdr hd = rs_hdr(a.rs, p0 + d);
+    const RsHdr hd = hdr(d);
     const bool from_snap = (hd.flags & kRsHead) && rs_setkind(hd.flags) != kSetRec;
     const uint4 x = sel4(from_snap, xs, xi);
-    const uint4 v = Rr2Op::own_value(hd, x, x, Rr2Op::ident_of(a, p0 + d));
-    vscan_carry_tail<Rr2Op>(a, s_v, s_f, f, sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v), cf, cv);
+    const uint4 v = sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), Rr2Op::own_value(hd, x, x, id));
+    s_v[wave][lane] = v;
+    if (lane == 0) s_f[wave] = f;
+    __syncthreads();
+    cf = uni4(s_blk[8]);
+    cv = s_blk[16 + lane];
+    for (uint32_t k = 0; k < wave; ++k) {
+      const uint4 e = s_f[k];
+      cv = Rr2Op::v_combine(cf, cv, e, s_v[k][lane]);
+      cf = Rr2Op::f_combine(cf, e);
+    }
   }
   uint4 sd = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
-    const RsHdr h = rs_hdr(a.rs, p);
+    const RsHdr h = hdr(j);
     const bool head = h.flags & kRsHead;
     const uint4 sv = svs[j], iv = ivs[j];
-    const uint4 idv = Rr2Op::ident_of(a, p);
+    const uint4 idv = ident(j);
     // the row state before this op
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 1u, 0u), cf);
     const uint4 pv = sel4(head, sv, cv);
@@ -1069,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
     st_drop(a.pbuf, (uint64_t)p * 64 + lane, fin);
     sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, 0u), sd);
   }
-  if (lane < 16) st_drop(a.psd, p0 + lane, sd);
+  if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);
 }
 
 }  // namespace gvs

@@ -21,7 +21,7 @@ int gvs_dump_messages(gvs_handle *h, void *host_dst, uint64_t bytes);
  * 0 message table (physical rows), 1 mailbox table, 2 mailbox side entries,
  * 3 message row tags, 4 mailbox row tags (3, 4: authenticated mode only),
  * 5 the final row states the last batch left pending (B x 1024, by sorted
- * position), 6 their side entries (B x 16: target row, valid), 7 their tags
+ * position), 6 their side entries (B x 128: 16 used, target row, valid), 7 their tags
  * (authenticated mode), 8 the last batch's slot descriptors (W*c x 128). */
 int gvs_raw_size(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t *size);
 int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset, void *dst,

@@ -65,7 +65,7 @@ def pending_states(store, ep):
     bound to its position and, through its side entry, to its target row)."""
     B = store.config.max_batch
     P = store.dump_raw(abi.RAW_PENDING, 0, B * 1024).reshape(B, 1024)
-    side = store.dump_raw(abi.RAW_PENDING_SIDE, 0, B * 16).reshape(B, 16)
+    side = store.dump_raw(abi.RAW_PENDING_SIDE, 0, B * 128).reshape(B, 128)[:, :16]
     tags = store.dump_raw(abi.RAW_PENDING_TAGS, 0, B * 16).reshape(B, 16)
     out = {}
     for p in range(B):
@@ -136,7 +136,7 @@ def run_one(store, model, params, n=1024):
     (abi.RAW_SIDE, 3 * 16 + 1),           # a mailbox side entry
     (abi.RAW_MBOX_TAGS, 200 * 16 + 15),   # a mailbox tag
     (abi.RAW_PENDING, 300 * 1024 + 5),    # a pending final state
-    (abi.RAW_PENDING_SIDE, 17 * 16 + 2),  # its side entry (target row)
+    (abi.RAW_PENDING_SIDE, 17 * 128 + 2),  # its side entry (target row)
     (abi.RAW_PENDING_TAGS, 900 * 16),     # its tag
 ])
 def test_tamper_is_detected(region, offset):
@@ -240,7 +240,7 @@ def test_replayed_pending_state_is_detected():
     params = ffi.gen_params(n_identities=200)
     run_stream(store, model, params, batches=2, n=1024)
     old = [store.dump_raw(r, 0, n).tobytes() for r, n in
-           ((abi.RAW_PENDING, 1024 * 1024), (abi.RAW_PENDING_SIDE, 1024 * 16), (abi.RAW_PENDING_TAGS, 1024 * 16))]
+           ((abi.RAW_PENDING, 1024 * 1024), (abi.RAW_PENDING_SIDE, 1024 * 128), (abi.RAW_PENDING_TAGS, 1024 * 16))]
     run_stream(store, model, params, batches=1, n=1024)
     for r, b in zip((abi.RAW_PENDING, abi.RAW_PENDING_SIDE, abi.RAW_PENDING_TAGS), old):
         store.store_raw(r, 0, b)

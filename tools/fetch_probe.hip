@@ -25,6 +25,21 @@ __global__ __launch_bounds__(256) void k_rows(const uint4* __restrict__ src, con
   if (lane == 0) out[w] = x;
 }
 
+// 16 rows per wave, all loads in flight together (as the phase-C walks)
+__global__ __launch_bounds__(256) void k_rows16(const uint4* __restrict__ src, const uint32_t* __restrict__ idx,
+                                                uint32_t* __restrict__ out, uint32_t n) {
+  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (w * 16 >= n) return;
+  uint4 v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = src[(uint64_t)idx[w * 16 + j] * 64 + lane];
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+  if (lane == 0) out[w] = x;
+}
+
 #define CK(x)                                                   \
   do {                                                          \
     hipError_t e_ = (x);                                        \
@@ -57,6 +72,9 @@ int main() {
     for (int k = 0; k < 4; ++k) {
       CK(hipMemset(flush, r + k, (size_t)rows * 1024));
       hipLaunchKernelGGL(k_rows, dim3(n / 4), dim3(256), 0, 0, src, idx + (size_t)k * n, out, n);
+      CK(hipGetLastError());
+      CK(hipMemset(flush, r + k + 1, (size_t)rows * 1024));
+      hipLaunchKernelGGL(k_rows16, dim3(n / 64), dim3(256), 0, 0, src, idx + (size_t)k * n, out, n);
       CK(hipGetLastError());
     }
   CK(hipDeviceSynchronize());

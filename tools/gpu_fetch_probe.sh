@@ -16,7 +16,7 @@ for d in ["f", "r"]:
     for r in rows:
         if "k_rows" not in r["Kernel_Name"]:
             continue
-        per[int(r.get("Dispatch_Id", 0))][r["Counter_Name"]] = float(r["Counter_Value"])
+        per[(int(r.get("Dispatch_Id", 0)), r["Kernel_Name"][:9])][r["Counter_Name"]] = float(r["Counter_Value"])
     for i, k in enumerate(sorted(per)):
-        print(d, ["seq", "perm", "scatter", "mixed"][i % 4], per[k])
+        print(d, k[1], ["seq", "perm", "scatter", "mixed"][(i // 2) % 4], per[k])
 PY
