@@ -129,6 +129,23 @@ class GvsOramConfig(ctypes.Structure):
 assert ctypes.sizeof(GvsOramConfig) == 64
 
 
+# key-value map (gvs_omap_*, include/gvstore.h)
+OMAP_READ, OMAP_WRITE, OMAP_INSERT, OMAP_REMOVE = 0, 1, 2, 3
+OMAP_FOUND, OMAP_NOT_FOUND, OMAP_OVERFLOW, OMAP_INVALID_KEY = 0, 1, 2, 3
+OMAP_OP_DTYPE = np.dtype([
+    ("key", "u1", 16),
+    ("op", "<u4"),
+    ("reserved", "<u4", 3),
+    ("value", "u1", 1024),
+])
+OMAP_RESULT_DTYPE = np.dtype([
+    ("value", "u1", 1024),
+    ("status", "<u4"),
+    ("reserved", "<u4", 3),
+])
+assert OMAP_OP_DTYPE.itemsize == 1056 and OMAP_RESULT_DTYPE.itemsize == 1040
+
+
 def make_oram_config(capacity, max_batch=4096, device=0, secret_key=None, auth_storage=False):
     cfg = GvsOramConfig()
     cfg.capacity = capacity

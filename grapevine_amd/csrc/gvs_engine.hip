@@ -26,6 +26,7 @@
 #include "gvs_route.h"
 #include "gvs_mtx.h"
 #include "gvs_kv.h"
+#include "gvs_omap.h"
 
 using namespace gvs;
 
@@ -35,6 +36,8 @@ static_assert(sizeof(gvs_response) == 1040, "response layout");
 static_assert(sizeof(ncclUniqueId) == GVS_COMM_ID_BYTES, "comm id size");
 static_assert(sizeof(gvs_oram_config) == 64, "oram config layout");
 static_assert(sizeof(gvs_block_op) == 1040, "block op layout (kAbiU4 uint4)");
+static_assert(sizeof(gvs_omap_op) == 1056, "map op layout (66 uint4)");
+static_assert(sizeof(gvs_omap_result) == 1040, "map result layout (k_out)");
 
 namespace {
 
@@ -131,9 +134,19 @@ struct Engine {
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
   GtxV* gtx_carry = nullptr;
-  // block / key-value stores (gvs_kv.h)
+  // block / key-value stores (gvs_kv.h, gvs_omap.h)
   uint4* kvmeta = nullptr;   // B x 128-B op lines
   uint4* kvdummy = nullptr;  // B x 1 KiB
+  uint4* kdir = nullptr;     // N x 32 B key directory (key, hash)
+  Key128* okeys = nullptr;   // B (hash, seq) sort keys
+  uint4* opr = nullptr;      // B x 128 B position records
+  uint4* opos = nullptr;     // B
+  uint4* ogt = nullptr;      // (W*c + B) x 128 B group records
+  uint4* ogp = nullptr;      // (B + W*c) x 128 B group results by head position
+  OgtV* ogt_agg = nullptr;
+  OgtV* ogt_carry = nullptr;
+  OrowV* orow_agg = nullptr;
+  OrowV* orow_carry = nullptr;
 };
 
 // Router state of one source rank (kLocal: one per virtual rank).
@@ -171,7 +184,7 @@ struct gvs_handle {
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
-  int kind = 0;              // 0 message store, 1 block store (gvs_oram_*)
+  int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   std::vector<void*> allocs;
   std::string err;
 };
@@ -489,6 +502,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
   GVS_HIP(h, hipMemsetAsync(e.gtx, 0, ((uint64_t)e.Q * e.cm + B) * 128, s));
+  GVS_HIP(h, hipMemsetAsync(e.rkeys, 0xFF, (uint64_t)B * 8, s));  // null rows until written
   for (int k = 0; k < 2; ++k) {
     GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, ((uint64_t)e.W * e.c + B) * 128, s));
     if (e.X) GVS_HIP(h, hipMemsetAsync(e.xb2[k], 0, (uint64_t)e.X * 128, s));
@@ -1049,7 +1063,8 @@ static int finish(gvs_handle* h) {
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & 1u) {
-    h->err = "batch overflow: more recipients in one mailbox partition than its group slots";
+    h->err = h->kind == 2 ? "batch overflow: more distinct keys in one partition than its group slots"
+                          : "batch overflow: more recipients in one mailbox partition than its group slots";
     return GVS_ERR_BATCH_OVERFLOW;
   }
   if (e & kRErr) {
@@ -1132,11 +1147,29 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
     A(mtag, N);
     A(ptag, B);
   }
+  if (h->kind == 2) {  // key-value map: key directory, key sort, group slots
+    A(kdir, N * 2);
+    A(okeys, B);
+    A(opr, (uint64_t)B * 8);
+    A(opos, B);
+    A(ogt, (WC + B) * 8);
+    A(ogp, ((uint64_t)B + WC) * 8);
+    A(ogt_agg, B / kScanT);
+    A(ogt_carry, B / kScanT);
+    A(orow_agg, B / kScanT);
+    A(orow_carry, B / kScanT);
+    A(resp, (uint64_t)B * kSlotU4);
+  }
 #undef A
   hipStream_t s = h->stream;
   GVS_HIP(h, hipMemsetAsync(e.table, 0, N * 1024, s));
+  if (h->kind == 2) {
+    GVS_HIP(h, hipMemsetAsync(e.kdir, 0, N * 32, s));
+    GVS_HIP(h, hipMemsetAsync(e.ogt, 0, (WC + B) * 128, s));
+  }
   for (int k = 0; k < 2; ++k) GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, (WC + B) * 128, s));
   GVS_HIP(h, hipMemsetAsync(e.scal, 0, sizeof(Scal), s));
+  GVS_HIP(h, hipMemsetAsync(e.rkeys, 0xFF, (uint64_t)B * 8, s));  // null rows until written
   if (h->auth) {  // every block starts as a sealed all-zero row at epoch 0
     e.epoch = 0;
     hipLaunchKernelGGL(k_seal_init, dim3(1024), dim3(256), 0, s, seal_of(h, e), (const uint32_t*)h->te,
@@ -1200,6 +1233,83 @@ static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
 }
 
 struct gvs_oram {
+  gvs_handle* h = nullptr;
+};
+
+// One key-value batch: n ops (gvs_omap_op) at d_in, results (gvs_omap_result)
+// to d_out (gvs_omap.h).
+static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, uint4* d_out) {
+  hipStream_t s = h->stream;
+  const uint32_t B = e.B;
+  h->n_marks = 0;
+  mark(h, "start");
+  if (int r = reset_errors(h)) return r;
+  e.stamp_run = e.stamp_next++;
+  if (e.stamp_next == kNone) e.stamp_next = 1;
+  {
+    OcopyArgs a{d_in, e.img, e.kvmeta, e.okeys, e.scal, e.kc, n, B};
+    hipLaunchKernelGGL(k_ocopy, dim3(B / 256), dim3(256), 0, s, a);
+  }
+  mark(h, "copy");
+  if (int r = sort_keys<Key128, 4>(h, e.okeys, B)) return r;
+  hipLaunchKernelGGL(k_ogather, dim3(B / 256), dim3(256), 0, s, OposArgs{e.okeys, e.kvmeta, e.opr, B});
+  mark(h, "sort_k");
+  {
+    OgtArgs a{e.opr, e.opos, e.ogt, e.ogt_agg, e.ogt_carry, e.scal, B, e.W, log2u(e.W), e.c,
+              B / kScanT, e.stamp_run};
+    hipLaunchKernelGGL(k_scan_a<OgtOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<OgtOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<OgtOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "groups");
+  hipLaunchKernelGGL(k_okey, dim3(e.W), dim3(256), 0, s,
+                     OkeyArgs{e.ogt, e.kdir, e.ogp, e.scal, e.W, e.S, e.c, B, e.stamp_run});
+  mark(h, "keys");
+  {
+    OrowArgs a{e.opos, e.opr, e.ogp, e.rkeys, e.kvmeta, e.orow_agg, e.orow_carry, e.scal, B, B / kScanT};
+    hipLaunchKernelGGL(k_scan_a<OrowOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<OrowOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<OrowOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "rows");
+  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  mark(h, "sort_r");
+  {
+    RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,
+              B,       e.W,    e.S,           e.c,       B / kScanT,  e.stamp_run};
+    hipLaunchKernelGGL(k_scan_a<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
+  }
+  mark(h, "rtx");
+  launch_rpass2(h, e);
+  mark(h, "rpass");
+  {
+    KvArgs a{};
+    vscan_fields(a, e);
+    a.rpos = e.rpos;
+    a.meta = e.kvmeta;
+    a.img = e.img;
+    a.snap = e.snap;
+    a.snapdummy = e.snapdummy;
+    a.pbuf = e.pbuf;
+    a.psd = e.psd;
+    a.out = e.resp;
+    a.outdummy = e.kvdummy;
+    a.n = n;
+    a.S = e.S;
+    a.omap = 1;
+    vscan_abc<KvOp>(s, a);
+    hipLaunchKernelGGL(k_kv_c, dim3(a.nvb), dim3(256), 0, s, a);
+  }
+  if (d_out && n)
+    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
+  mark(h, "kv");
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+struct gvs_omap {
   gvs_handle* h = nullptr;
 };
 
@@ -1489,8 +1599,8 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
 
 // ---- block store: mc-oblivious-traits ORAM::access, batched
 
-int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
-  if (!cfg || !out) return GVS_ERR_INVALID_ARG;
+// a block store (kind 1) or key-value map (kind 2) handle
+static int kv_create(const gvs_oram_config* cfg, int kind, gvs_handle** out) {
   *out = nullptr;
   if (!is_pow2(cfg->capacity) || cfg->capacity < 4096 || cfg->capacity > (1ull << 32))
     return GVS_ERR_INVALID_ARG;
@@ -1502,15 +1612,10 @@ int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GVS_ERR_NO_DEVICE;
   if ((int)cfg->device >= ndev) return GVS_ERR_INVALID_ARG;
-  gvs_oram* o = new (std::nothrow) gvs_oram();
+  if (kind == 2 && (cfg->flags & GVS_FLAG_AUTH_STORAGE)) return GVS_ERR_INVALID_ARG;
   gvs_handle* h = new (std::nothrow) gvs_handle();
-  if (!o || !h) {
-    delete o;
-    delete h;
-    return GVS_ERR_OUT_OF_MEMORY;
-  }
-  o->h = h;
-  h->kind = 1;
+  if (!h) return GVS_ERR_OUT_OF_MEMORY;
+  h->kind = kind;
   h->mode = kSingle;
   h->device = (int)cfg->device;
   h->auth = (cfg->flags & GVS_FLAG_AUTH_STORAGE) != 0;
@@ -1521,7 +1626,7 @@ int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
   std::memcpy(h->cfg.secret_key, cfg->secret_key, 32);
   h->Bsub = h->Be = cfg->max_batch;
   auto fail = [&](int code) {
-    gvs_oram_destroy(o);
+    gvs_destroy(h);
     return code;
   };
   if (hipSetDevice(h->device) != hipSuccess) return fail(GVS_ERR_DEVICE);
@@ -1537,9 +1642,28 @@ int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
       return fail(GVS_ERR_DEVICE);
   }
   h->eng.resize(1);
-  if (int rc = kv_engine_init(h, h->eng[0], cfg->capacity, cfg->max_batch)) return fail(rc);
-  if (int rc = dalloc_t(h, &h->in_stage, (uint64_t)cfg->max_batch * kAbiU4)) return fail(rc);
-  if (int rc = dalloc_t(h, &h->out_stage, (uint64_t)cfg->max_batch * 64)) return fail(rc);
+  Engine& e = h->eng[0];
+  e.kc.hk0 = ld64(cfg->secret_key + 16);
+  e.kc.hk1 = ld64(cfg->secret_key + 24);
+  if (int rc = kv_engine_init(h, e, cfg->capacity, cfg->max_batch)) return fail(rc);
+  const uint64_t in_u4 = kind == 2 ? 66 : kAbiU4, out_u4 = kind == 2 ? kAbiU4 : 64;
+  if (int rc = dalloc_t(h, &h->in_stage, (uint64_t)cfg->max_batch * in_u4)) return fail(rc);
+  if (int rc = dalloc_t(h, &h->out_stage, (uint64_t)cfg->max_batch * out_u4)) return fail(rc);
+  *out = h;
+  return GVS_OK;
+}
+
+int gvs_oram_create(const gvs_oram_config* cfg, gvs_oram** out) {
+  if (!cfg || !out) return GVS_ERR_INVALID_ARG;
+  *out = nullptr;
+  gvs_handle* h;
+  if (int rc = kv_create(cfg, 1, &h)) return rc;
+  gvs_oram* o = new (std::nothrow) gvs_oram();
+  if (!o) {
+    gvs_destroy(h);
+    return GVS_ERR_OUT_OF_MEMORY;
+  }
+  o->h = h;
   *out = o;
   return GVS_OK;
 }
@@ -1584,5 +1708,62 @@ int gvs_oram_last_timings(gvs_oram* o, const char** names, float* ms, int cap) {
 }
 
 const char* gvs_oram_last_error(gvs_oram* o) { return o ? o->h->err.c_str() : "null handle"; }
+
+// ---- key-value map: mc-oblivious-traits ObliviousHashMap, batched
+
+int gvs_omap_create(const gvs_omap_config* cfg, gvs_omap** out) {
+  if (!cfg || !out) return GVS_ERR_INVALID_ARG;
+  *out = nullptr;
+  gvs_handle* h;
+  if (int rc = kv_create(reinterpret_cast<const gvs_oram_config*>(cfg), 2, &h)) return rc;
+  gvs_omap* o = new (std::nothrow) gvs_omap();
+  if (!o) {
+    gvs_destroy(h);
+    return GVS_ERR_OUT_OF_MEMORY;
+  }
+  o->h = h;
+  *out = o;
+  return GVS_OK;
+}
+
+int gvs_omap_destroy(gvs_omap* o) {
+  if (!o) return GVS_ERR_INVALID_ARG;
+  if (o->h) gvs_destroy(o->h);
+  delete o;
+  return GVS_OK;
+}
+
+int gvs_omap_access_batch(gvs_omap* o, const gvs_omap_op* ops, uint32_t n, gvs_omap_result* out) {
+  if (!o || (!ops && n) || (!out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
+  gvs_handle* h = o->h;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  GVS_HIP(h, hipSetDevice(h->device));
+  if (n)
+    GVS_HIP(h, hipMemcpyAsync(h->in_stage, ops, (size_t)n * sizeof(gvs_omap_op), hipMemcpyHostToDevice,
+                              h->stream));
+  if (int r = omap_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
+  if (n)
+    GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * sizeof(gvs_omap_result), hipMemcpyDeviceToHost,
+                              h->stream));
+  return finish(h);
+}
+
+int gvs_omap_access_batch_device(gvs_omap* o, const void* d_ops, uint32_t n, void* d_out) {
+  if (!o || (!d_ops && n) || (!d_out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
+  gvs_handle* h = o->h;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  GVS_HIP(h, hipSetDevice(h->device));
+  const uint4* in = n ? (const uint4*)d_ops : h->in_stage;
+  if (int r = omap_batch(h, h->eng[0], in, n, (uint4*)d_out)) return r;
+  return finish(h);
+}
+
+int gvs_omap_set_timing(gvs_omap* o, int on) { return o ? gvs_set_timing(o->h, on) : GVS_ERR_INVALID_ARG; }
+
+int gvs_omap_last_timings(gvs_omap* o, const char** names, float* ms, int cap) {
+  return o ? gvs_last_timings(o->h, names, ms, cap) : GVS_ERR_INVALID_ARG;
+}
+
+const char* gvs_omap_last_error(gvs_omap* o) { return o ? o->h->err.c_str() : "null handle"; }
 
 }  // extern "C"

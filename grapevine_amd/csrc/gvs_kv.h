@@ -86,7 +86,7 @@ struct KvArgs {
 };
 
 struct KvHdr {
-  uint32_t seq, flags, slot, kind, e0, ovf;
+  uint32_t seq, flags, slot, kind, e0, ovf, invalid;
   uint64_t prow;
 };
 
@@ -101,6 +101,7 @@ __device__ inline KvHdr kv_hdr(const KvArgs& a, uint32_t p) {
   h.kind = m.x;
   h.e0 = m.y;
   h.ovf = m.z;
+  h.invalid = m.w;
   return h;
 }
 
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
     uint32_t status = e ? kOmapFound : kOmapNotFound;
     status = selu32((creates && h.ovf) || (null && creates && a.omap), kOmapOverflow, status);
     status = selu32(null && !creates, kOmapNotFound, status);
+    status = selu32(null && h.invalid, kOmapInvalidKey, status);
     const bool ovf = status == kOmapOverflow;
     // the value handed back: the row's value (READ, WRITE, REMOVE, INSERT of
     // a present key); the default an INSERT put in; zero when absent

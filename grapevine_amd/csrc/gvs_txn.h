@@ -183,7 +183,9 @@ struct RtxArgs {
 struct RtxOp {
   using V = RtxV;
   using Args = RtxArgs;
-  __device__ static bool stop(const Args&) { return false; }  // phase A: always runs
+  // a batch that already failed (e.g. a slot overflow before its row keys
+  // were written) stops here
+  __device__ static bool stop(const Args& a) { return a.scal->error != 0u; }
   __device__ static V identity() { return V{0u, 0u}; }
   __device__ static V combine(const V& a, const V& b) {
     return b.reset ? b : V{a.reset, a.cnt + b.cnt};
@@ -191,6 +193,7 @@ struct RtxOp {
   __device__ static void row_of(const Args& a, uint32_t p, uint64_t& row, uint32_t& w) {
     const uint64_t k = a.rkeys[p];
     row = k >> 22;
+    if (row >= (uint64_t)a.W * a.S) row = kRNullRow;  // never index past the table
     w = row == kRNullRow ? a.W : (uint32_t)(row / a.S);
   }
   __device__ static V local(const Args& a, uint32_t p, uint4*) {

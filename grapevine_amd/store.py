@@ -29,6 +29,8 @@ EXPORTED = (
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
     "gvs_oram_create", "gvs_oram_destroy", "gvs_oram_access_batch", "gvs_oram_access_batch_device",
     "gvs_oram_set_timing", "gvs_oram_last_timings", "gvs_oram_last_error",
+    "gvs_omap_create", "gvs_omap_destroy", "gvs_omap_access_batch", "gvs_omap_access_batch_device",
+    "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw")
 
@@ -90,8 +92,17 @@ def load_library(path=None):
                                           ctypes.POINTER(ctypes.c_float), i32]
     lib.gvs_oram_last_error.argtypes = [vp]
     lib.gvs_oram_last_error.restype = ctypes.c_char_p
+    lib.gvs_omap_create.argtypes = [ctypes.POINTER(abi.GvsOramConfig), ctypes.POINTER(vp)]
+    lib.gvs_omap_destroy.argtypes = [vp]
+    lib.gvs_omap_access_batch.argtypes = [vp, vp, u32, vp]
+    lib.gvs_omap_access_batch_device.argtypes = [vp, vp, u32, vp]
+    lib.gvs_omap_set_timing.argtypes = [vp, i32]
+    lib.gvs_omap_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
+                                          ctypes.POINTER(ctypes.c_float), i32]
+    lib.gvs_omap_last_error.argtypes = [vp]
+    lib.gvs_omap_last_error.restype = ctypes.c_char_p
     for name in EXPORTED + (TEST_EXPORTED if hooks else ()):
-        if name not in ("gvs_last_error", "gvs_version", "gvs_oram_last_error"):
+        if name not in ("gvs_last_error", "gvs_version", "gvs_oram_last_error", "gvs_omap_last_error"):
             getattr(lib, name).restype = i32
     if path is None:
         _LIB = lib
@@ -260,4 +271,52 @@ class BlockStore:
         names = (ctypes.c_char_p * 16)()
         ms = (ctypes.c_float * 16)()
         c = self.lib.gvs_oram_last_timings(self.h, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(max(c, 0))}
+
+
+class KeyValueMap:
+    """The key-value map (gvs_omap_*): mc-oblivious-traits ObliviousHashMap,
+    batched.  `access(ops)` applies abi.OMAP_OP_DTYPE ops in order and returns
+    abi.OMAP_RESULT_DTYPE results (status, the value each op saw)."""
+
+    def __init__(self, config):
+        self.lib = load_library()
+        self.config = config
+        h = ctypes.c_void_p()
+        rc = self.lib.gvs_omap_create(ctypes.byref(config), ctypes.byref(h))
+        if rc != 0:
+            raise GvsError(rc, "gvs_omap_create failed (no GPU, bad config or out of memory)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gvs_omap_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise GvsError(rc, self.lib.gvs_omap_last_error(self.h).decode())
+
+    def access(self, ops):
+        ops = np.ascontiguousarray(ops, dtype=abi.OMAP_OP_DTYPE)
+        out = np.zeros(len(ops), dtype=abi.OMAP_RESULT_DTYPE)
+        self._check(self.lib.gvs_omap_access_batch(self.h, ops.ctypes.data, len(ops), out.ctypes.data))
+        return out
+
+    def access_device(self, d_ops, n, d_out):
+        self._check(self.lib.gvs_omap_access_batch_device(self.h, d_ops, n, d_out))
+
+    def set_timing(self, on=True):
+        self._check(self.lib.gvs_omap_set_timing(self.h, 1 if on else 0))
+
+    def last_timings(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        c = self.lib.gvs_omap_last_timings(self.h, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(max(c, 0))}

@@ -296,6 +296,65 @@ int gvs_oram_set_timing(gvs_oram *o, int on);
 int gvs_oram_last_timings(gvs_oram *o, const char **names, float *ms, int cap);
 const char *gvs_oram_last_error(gvs_oram *o);
 
+/* ---------------------------------------------------------------------------
+ * Key-value map: the mc-oblivious-traits ObliviousHashMap<16, 1024> surface,
+ * batched (access_and_insert / read / remove with u32
+ * OMAP_* statuses; the callback is a per-op choice of what to write).
+ *
+ * `capacity` rows of 1 KiB values; a 16-B key lives in the partition its
+ * keyed hash selects (W partitions of S rows, the message table's layout,
+ * DESIGN.md §10).  One call applies n <= max_batch ops in submission order:
+ *   GVS_OMAP_READ    read(key): FOUND and the value, or NOT_FOUND
+ *   GVS_OMAP_WRITE   access_and_insert with a callback that overwrites:
+ *                    FOUND / NOT_FOUND, the value before, then `value` stored
+ *   GVS_OMAP_INSERT  access_and_insert(key, default = `value`) with a callback
+ *                    that keeps: FOUND and the value, or NOT_FOUND and the
+ *                    default, which is inserted
+ *   GVS_OMAP_REMOVE  remove(key): FOUND and the removed value, or NOT_FOUND
+ * An all-zero key is OMAP_INVALID_KEY.  [D] New keys of a batch are admitted
+ * into their partition's free rows (free when the batch starts) in keyed-hash
+ * order; an INSERT / WRITE of a key that is not admitted gets OMAP_OVERFLOW
+ * and changes nothing.  More distinct keys in one partition in one batch
+ * than its group slots (mean + 8 sigma + 16 for uniformly hashed keys, at
+ * most S) fails the batch with GVS_ERR_BATCH_OVERFLOW before any state
+ * changes.  The launch sequence, grids, HBM bytes and kernel durations
+ * depend only on (capacity, max_batch, n).  Plain storage only (flags 0).
+ * ------------------------------------------------------------------------- */
+typedef struct gvs_omap gvs_omap;
+typedef gvs_oram_config gvs_omap_config;
+
+#define GVS_OMAP_READ 0u
+#define GVS_OMAP_WRITE 1u
+#define GVS_OMAP_INSERT 2u
+#define GVS_OMAP_REMOVE 3u
+
+/* statuses (mc-oblivious-traits OMAP_* codes) */
+#define GVS_OMAP_FOUND 0u
+#define GVS_OMAP_NOT_FOUND 1u
+#define GVS_OMAP_OVERFLOW 2u
+#define GVS_OMAP_INVALID_KEY 3u
+
+typedef struct gvs_omap_op {
+  uint8_t key[16];
+  uint32_t op;             /* GVS_OMAP_* */
+  uint32_t reserved[3];
+  uint8_t value[1024];     /* WRITE: the new value; INSERT: the default */
+} gvs_omap_op;             /* 1056 B */
+
+typedef struct gvs_omap_result {
+  uint8_t value[1024];     /* the value the op saw (see above); zero if none */
+  uint32_t status;         /* GVS_OMAP_FOUND .. GVS_OMAP_INVALID_KEY */
+  uint32_t reserved[3];
+} gvs_omap_result;         /* 1040 B */
+
+int gvs_omap_create(const gvs_omap_config *cfg, gvs_omap **out);
+int gvs_omap_destroy(gvs_omap *o);
+int gvs_omap_access_batch(gvs_omap *o, const gvs_omap_op *ops, uint32_t n, gvs_omap_result *out);
+int gvs_omap_access_batch_device(gvs_omap *o, const void *d_ops, uint32_t n, void *d_out);
+int gvs_omap_set_timing(gvs_omap *o, int on);
+int gvs_omap_last_timings(gvs_omap *o, const char **names, float *ms, int cap);
+const char *gvs_omap_last_error(gvs_omap *o);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,6 +80,14 @@ def lib():
         L.gvo_oram_access_batch.argtypes = [vp, vp, u32, vp]
         L.gvo_oram_access_batch.restype = ctypes.c_int
         L.gvo_oram_read_all.argtypes = [vp, vp]
+        L.gvo_omap_create.argtypes = [u64, ctypes.c_char_p]
+        L.gvo_omap_create.restype = vp
+        L.gvo_omap_destroy.argtypes = [vp]
+        L.gvo_omap_access_batch.argtypes = [vp, vp, u32, vp]
+        L.gvo_omap_access_batch.restype = ctypes.c_int
+        L.gvo_omap_size.argtypes = [vp]
+        L.gvo_omap_size.restype = u64
+        L.gvo_omap_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.gvo_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
         L.gvo_id_encode_shard.argtypes = [ctypes.c_char_p, u32, u32, u64, ctypes.c_char_p]
         L.gvo_id_decode_shard.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, u32,
@@ -419,3 +427,37 @@ class OramModel:
 
     def __del__(self):
         self.close()
+
+
+class OmapModel:
+    """Sequential key-value map (oracle/gvs_kv.c): ObliviousHashMap semantics
+    with the batch admission rule of include/gvstore.h."""
+
+    def __init__(self, capacity, secret):
+        self.L = lib()
+        self.o = self.L.gvo_omap_create(capacity, bytes(secret))
+        if not self.o:
+            raise MemoryError("oracle map")
+
+    def access(self, ops):
+        ops = np.ascontiguousarray(ops)
+        out = np.zeros(len(ops), dtype=abi.OMAP_RESULT_DTYPE)
+        rc = self.L.gvo_omap_access_batch(self.o, ops.ctypes.data, len(ops), out.ctypes.data)
+        return None if rc else out
+
+    def size(self):
+        return self.L.gvo_omap_size(self.o)
+
+    def close(self):
+        if self.o:
+            self.L.gvo_omap_destroy(self.o)
+            self.o = None
+
+    def __del__(self):
+        self.close()
+
+
+def omap_hash(secret, key):
+    hi, lo = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().gvo_omap_hash(bytes(secret), bytes(key), ctypes.byref(hi), ctypes.byref(lo))
+    return hi.value, lo.value
