@@ -282,10 +282,14 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     }
     if (AUTH) m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
     mm = __builtin_amdgcn_readfirstlane(mm);
-    bool dry_run = j0 == 0;  // wave 0's first chunk runs the loop once dry
-    while (mm || dry_run) {
-      const uint32_t bit = dry_run ? 0u : (mm & (0u - mm));
-      if (!dry_run) mm &= mm - 1u;
+    // wave 0's first chunk runs the loop once dry: an extra mask bit taken
+    // last by the same loop code (no peeled first iteration)
+    uint32_t mq = mm | (j0 == 0 ? (1u << kMU) : 0u);
+    while (mq) {
+      const uint32_t low = mq & (0u - mq);
+      mq &= mq - 1u;
+      const bool dry_run = low == (1u << kMU);
+      const uint32_t bit = dry_run ? 0u : low;
       uint4 cur = v[0];
 #pragma unroll
       for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
@@ -296,7 +300,6 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
       cur = sel4(lane == 0, hdr, sel4(lane == 1, make_uint4(0, 0, 0, 0), cur));
       uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
       st_drop(dst, lane, cur);
-      dry_run = false;
     }
 #pragma unroll
     for (int u = 0; u < kMU; ++u) va[u] = vb[u];
@@ -647,10 +650,12 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       for (int u = 0; u < kMU; ++u) sd[u] = shfl4(mine, u);
     }
     mm = __builtin_amdgcn_readfirstlane(mm);
-    bool dry_run = j0 == 0;
-    while (mm || dry_run) {
-      const uint32_t bit = dry_run ? 0u : (mm & (0u - mm));
-      if (!dry_run) mm &= mm - 1u;
+    uint32_t mq = mm | (j0 == 0 ? (1u << kMU) : 0u);  // the dry run: an extra bit, taken last
+    while (mq) {
+      const uint32_t low = mq & (0u - mq);
+      mq &= mq - 1u;
+      const bool dry_run = low == (1u << kMU);
+      const uint32_t bit = dry_run ? 0u : low;
       uint4 cur = v[0];
 #pragma unroll
       for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
@@ -678,7 +683,6 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
         v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
         sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
       }
-      dry_run = false;
     }
     if (AUTH) {
       const uint64_t r0 = (uint64_t)q * a.Sr + j0;

@@ -412,10 +412,17 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       // The first chunk of wave 0 runs each loop once "dry" on the workgroup's
       // own dry line, so every workgroup executes the same code whatever its
       // slots hold (instruction fetch shows in FETCH_SIZE, DESIGN.md §3 rule 6).
-      bool dry_p = t == 0 && j == 0 && wave == 0, dry_s = dry_p;
-      while (mp || dry_p) {  // rows the previous batch changed: its final state
-        const uint32_t bit = dry_p ? 0u : (mp & (0u - mp));
-        if (!dry_p) mp &= mp - 1u;
+      // The dry iteration is an extra mask bit (1 << U), taken last by the
+      // same loop code: a loop whose first iteration were special could be
+      // peeled by the compiler, and then not every workgroup would fetch the
+      // loop's code.
+      const bool first = t == 0 && j == 0 && wave == 0;
+      uint32_t mq = mp | (first ? (1u << U) : 0u);
+      while (mq) {  // rows the previous batch changed: its final state
+        const uint32_t low = mq & (0u - mq);
+        mq &= mq - 1u;
+        const bool dry_p = low == (1u << U);
+        const uint32_t bit = dry_p ? 0u : low;
         const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
         const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + u0];
         const uint32_t pos = s_pp[(uint32_t)k & (kSlotMax - 1u)];
@@ -427,11 +434,13 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
-        dry_p = false;
       }
-      while (ms || dry_s) {  // rows this batch touches: their snapshot
-        const uint32_t bit = dry_s ? 0u : (ms & (0u - ms));
-        if (!dry_s) ms &= ms - 1u;
+      uint32_t sq = ms | (first ? (1u << U) : 0u);
+      while (sq) {  // rows this batch touches: their snapshot
+        const uint32_t low = sq & (0u - sq);
+        sq &= sq - 1u;
+        const bool dry_s = low == (1u << U);
+        const uint32_t bit = dry_s ? 0u : low;
         const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31));
         const int16_t k = dry_s ? (int16_t)0 : s_sk[rb + j + (u0 & 31u)];
         uint4 cur = v[0];
@@ -440,7 +449,6 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
         uint4* dst = dry_s ? dry : sslot + (uint64_t)k * 64;
         st_drop(dst, lane, cur);
         if (lane < 8) st_drop(dry_s ? dry : a.snapid + (sbase + (uint64_t)k) * 8, lane, cur);
-        dry_s = false;
       }
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
       if (AUTH) {

@@ -10,9 +10,10 @@ the padded all-to-all).
 
 Each mix runs tools/oblivious_probe.py under rocprofv3 in a child process
 (one --kernel-trace run, one --pmc run per counter; counters are never
-combined with other tracing).  The tolerance is derived from noise alone: the
-spread, across the processes, of the same counter on the prefill batches that
-every process runs identically."""
+combined with other tracing).  The tolerance is derived from noise alone:
+the spread, across the processes, of the same counter on the prefill batches
+that every process runs identically, and the difference between two runs of
+the main mix with the same seed."""
 import csv
 import glob
 import os
@@ -112,14 +113,19 @@ def test_launch_sequence_and_grids_identical(traces):
         assert seq == ref, f"{shape}: mix {mix} launches differ from main"
 
 
-def noise_tolerance(per_mix, idx, n_meas):
-    """3x the spread of kernel `idx` over the identical prefill batches
-    (batch 0 excluded: cold caches), plus one counter quantum."""
+def noise_tolerance(per_mix, repeat, idx, n_meas):
+    """3x the counter's run-to-run noise for kernel `idx`, plus one counter
+    quantum.  Noise is measured on identical inputs only: the spread over the
+    prefill batches that every process runs identically (batch 0 excluded:
+    cold caches), and the difference between two processes that ran the main
+    mix with the same seed (every batch, measured ones included)."""
     n_pre = min(len(bs) for bs in per_mix.values()) - n_meas
     noise = 0.0
     for i in range(1, n_pre):
         vals = [bs[i][idx][1] for bs in per_mix.values()]
         noise = max(noise, max(vals) - min(vals))
+    for a, b in zip(per_mix["main"][1:], repeat[1:]):
+        noise = max(noise, abs(a[idx][1] - b[idx][1]))
     return noise, 3.0 * noise + 0.25
 
 
@@ -135,12 +141,17 @@ def test_hbm_bytes_identical(counter, shape, tmp_path):
         vals = [(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
                 if r.get("Counter_Name", counter) == counter]
         per_mix[mix] = split_batches(vals)
+    # main again, same seed: identical inputs, so any difference is noise
+    d = rocprof(["--pmc", counter], "main", str(tmp_path / f"{counter}_main_repeat"), shape)
+    rows = gvs_rows(os.path.join(d, "**", "*counter_collection.csv"))
+    repeat = split_batches([(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
+                            if r.get("Counter_Name", counter) == counter])
     n_meas = 3
     ref_b = per_mix["main"]
     kernels = [k for k, _ in ref_b[-1]]
     lines, bad = [], []
     for idx, k in enumerate(kernels):
-        noise, tol = noise_tolerance(per_mix, idx, n_meas)
+        noise, tol = noise_tolerance(per_mix, repeat, idx, n_meas)
         ref = sorted(b[idx][1] for b in ref_b[-n_meas:])[1]
         row = [f"{k[:28]:28s} ref={ref:12.1f} noise={noise:8.2f} tol={tol:8.2f}"]
         for mix, bs in per_mix.items():

@@ -32,6 +32,7 @@ case "$2" in
   bench) bench ;;
   obl) step oblivious 1100 $PT tests/test_oblivious.py -k "plain or launch" ;;
   tobl) tests && step oblivious 900 $PT tests/test_oblivious.py -k "plain or launch" ;;
+  oblall) step oblivious_all 1150 $PT tests/test_oblivious.py ;;
   all) tests && bench && timing ;;
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines
     step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
