@@ -195,8 +195,8 @@ def c1_single_thread():
 
 def cpu_baseline(budget_s, threads):
     """The reference's CPU path, restated: the grapevine handler over Path ORAM
-    (oracle/gvs_pathoram.c, Z = 4, recursive position map, 4 ORAM accesses per
-    request), cross-checked bit-for-bit against the sequential model in
+    (oracle/gvs_pathoram.c: CuckooHashTables over Path ORAM, Z = 4, recursive
+    position map, 6 ORAM accesses per request), cross-checked bit-for-bit against the sequential model in
     tests/test_pathoram.py.  One independent instance per host thread of this
     process's CPU share (the reference's maps are single-owner, &mut self);
     each is prefilled through its own accesses and then times the C3 mix for
@@ -207,7 +207,7 @@ def cpu_baseline(budget_s, threads):
     cpu = host_cpu()
     threads = threads or cpu["share"]
     c1 = c1_single_thread()
-    log2n = 20
+    log2n = 18  # two cuckoo tables at 50 % load: ~2.7 GB per instance
     cfg = abi.make_config(1 << log2n, max_batch=65536)
     mix = ffi.gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=0, bad_auth=0,
                          bad_recipient=0, hard_error=0, zero_recipient=0, n_identities=1 << 14)
@@ -244,7 +244,7 @@ def cpu_baseline(budget_s, threads):
             "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
             "cpu_share": cpu["share"],
             "c1_single_thread_req_s": c1,
-            "sample": f"Path ORAM restatement of the reference CPU path (oracle/gvs_pathoram.c), "
+            "sample": f"PathORAM + CuckooHashTable restatement of the reference CPU path (oracle/gvs_pathoram.c), "
                       f"2^{log2n} capacity (tree height reduced from C3's 2^24 to bound memory), "
                       f"{threads} independent instances on {threads} host threads "
                       f"(this process's CPU share of {cpu['logical_cpus']} logical CPUs), C3 mix, "

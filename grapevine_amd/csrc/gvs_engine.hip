@@ -465,7 +465,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(pbuf, (uint64_t)B * 64);
     A(psd, (uint64_t)B * 8);
     if (h->auth) A(ptag, B);
-    A(pdum, WC * 64);
+    A(pdum, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
     A(snapdummy, (uint64_t)B * 64);
     A(dryb, (uint64_t)e.W * 64);
     A(rtx_agg, B / kScanT);
@@ -820,6 +820,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.pbuf = e.pbuf;
   a.psd = e.psd;
   a.pdum = e.pdum;
+  a.psdum = h->auth ? e.pdum + (uint64_t)e.W * e.c * 64 : nullptr;
   a.snap = e.snap;
   a.snapid = e.snapid;
   a.dry = e.dryb;

@@ -249,6 +249,7 @@ struct R2Args {
   const uint4* pbuf;   // B final row states of the previous batch, by its sorted position
   const uint4* psd;    // B x 128 B: their target rows (x, y = physical row, z = valid), one line each
   const uint4* pdum;   // W*c x 1 KiB read for the slots no row uses
+  const uint4* psdum;  // AUTH: W*c x 128 B, their side-entry lines
   uint4* snap;         // W*c snapshots for this batch
   uint4* snapid;       // W*c x 128 B: each snapshot's first line (identity), for k_rr1
   uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
@@ -469,6 +470,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
   // unused slots: c reads of final states and c snapshot writes per partition
   for (uint32_t k = np + wave; k < a.c; k += 4) {
     uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
+    if (AUTH) x = xor4(x, uni4(a.psdum[(sbase + k) * 8]));  // as the side entry a P slot reads
     keep4(x);
   }
   for (uint32_t k = ns + wave; k < a.c; k += 4) {

@@ -8,15 +8,25 @@
  * mc-oblivious itself is absent from /root/reference and not in Cargo.lock,
  * so this is a restatement of its published algorithm, not a build of it.
  *
- *   message store : ORAM of N blocks x 1 KiB (block index = slot)
- *   mailbox rows  : ORAM of R = Q*S_r blocks x 1 KiB (recipient + 62 ids)
- *   directory     : ORAM of Q blocks x (S_r x 16 B): per row the recipient PRF
+ *   messages  : CuckooHashTable msg_id (16 B) -> record (1 KiB)
+ *   mailboxes : CuckooHashTable recipient PRF (16 B) -> row (recipient + 62 ids)
+ *   occupancy : ORAM of ceil(Q / 256) blocks of u32: recipients per mailbox
+ *               partition (the batched engine's capacity rule)
  *
- * Every request costs exactly four top-level ORAM accesses (directory,
- * mailbox row, message, directory), real or dummy, so READ / UPDATE / DELETE
- * are indistinguishable by access count (grapevine.proto:120-122).  Data moves inside an access use
- * memcpy rather than constant-time cmov, so this is an optimistic (fast)
- * baseline for the reference's CPU path.
+ * A CuckooHashTable (mc-oblivious's design, restated: BASELINE.json config 1
+ * "PathORAM + CuckooHashTable") is two Path ORAMs of buckets; a key has one
+ * bucket in each, chosen by keyed SipHash, and every access reads and writes
+ * both (two ORAM accesses, the second nested in the first so that both
+ * buckets are modified together).  An insert into two full buckets displaces
+ * a random item, which is re-placed by further single-bucket accesses (never
+ * seen at the 50 % load used here).
+ *
+ * Every request costs exactly six top-level ORAM accesses (occupancy, two
+ * per cuckoo access to the mailbox and the message tables, occupancy), real
+ * or dummy, so READ / UPDATE / DELETE are indistinguishable by access count
+ * (grapevine.proto:120-122).  Data moves inside an access use memcpy rather
+ * than constant-time cmov, so this is an optimistic (fast) baseline for the
+ * reference's CPU path.
  *
  * It is an independent second implementation of the handler: tests check it
  * bit-for-bit against the seqmodel (gvs_oracle.c) on seeded streams, and
@@ -228,11 +238,176 @@ static void oram_access(oram *o, uint64_t idx, access_fn fn, void *ctx) {
   o->scount = sc;
 }
 
-/* ------------------------------------------------------------- the model */
+/* ---------------------------------------------------- cuckoo hash table */
 
-typedef struct dir_entry { /* 16 B per mailbox row: recipient PRF, 0 = free */
-  uint64_t h_hi, h_lo;
-} dir_entry;
+#define CK_PER 2        /* items per bucket */
+#define CK_KICKS 64     /* displacement steps before giving up */
+#define CK_VMAX 1024    /* value bytes at most */
+
+typedef struct cuckoo {
+  oram *t[2];
+  uint64_t nb;        /* buckets per table */
+  uint32_t vsz, isz;  /* value bytes; item bytes (16-byte key, value) */
+  uint64_t hk[2][2];  /* SipHash keys of the two tables */
+  uint64_t *rng;
+  uint64_t kicks;
+} cuckoo;
+
+/* The op applied to a key's value (zeroed when absent): returns what becomes
+ * of the item. */
+enum { CK_LEAVE = 0, CK_KEEP = 1, CK_REMOVE = 2 };
+typedef int (*ck_fn)(void *ctx, uint8_t *val, int present);
+
+static int zero(const uint8_t *p, size_t n) {
+  uint8_t a = 0;
+  for (size_t i = 0; i < n; ++i) a |= p[i];
+  return a == 0;
+}
+
+static void cuckoo_free(cuckoo *c) {
+  if (!c) return;
+  oram_free(c->t[0]);
+  oram_free(c->t[1]);
+  free(c);
+}
+
+/* room for `cap` items at 50 % load */
+static cuckoo *cuckoo_new(uint64_t cap, uint32_t vsz, uint64_t *rng) {
+  cuckoo *c = (cuckoo *)calloc(1, sizeof *c);
+  if (!c) return NULL;
+  c->nb = (cap + CK_PER - 1) / CK_PER;
+  if (c->nb == 0) c->nb = 1;
+  c->vsz = vsz;
+  c->isz = 16 + vsz;
+  c->rng = rng;
+  for (int t = 0; t < 2; ++t) {
+    c->hk[t][0] = sm64(rng);
+    c->hk[t][1] = sm64(rng);
+    c->t[t] = oram_new(c->nb, CK_PER * c->isz, rng);
+    if (!c->t[t]) {
+      cuckoo_free(c);
+      return NULL;
+    }
+  }
+  return c;
+}
+
+static uint64_t ck_bucket(const cuckoo *c, int t, const uint8_t *key) {
+  return gvo_siphash24(c->hk[t][0], c->hk[t][1], key, 16) % c->nb;
+}
+
+typedef struct {
+  cuckoo *c;
+  const uint8_t *key;
+  ck_fn fn;
+  void *ctx;
+  uint64_t b1;
+  uint8_t *blk0;
+  int present;
+  int has_pend;           /* an item displaced from table 0 */
+  uint8_t pend[16 + CK_VMAX];
+} ck_acc;
+
+static void ck_in1(void *p, uint8_t *blk1) {
+  ck_acc *a = (ck_acc *)p;
+  cuckoo *c = a->c;
+  uint8_t *blk[2] = {a->blk0, blk1};
+  uint8_t *hit = NULL, *fr = NULL;
+  for (int t = 0; t < 2; ++t)
+    for (uint32_t i = 0; i < CK_PER; ++i) {
+      uint8_t *it = blk[t] + (size_t)i * c->isz;
+      const int empty = zero(it, 16);
+      if (!empty && memcmp(it, a->key, 16) == 0) hit = it;
+      if (empty && !fr) fr = it;
+    }
+  uint8_t tmp[CK_VMAX];
+  uint8_t *val = hit ? hit + 16 : tmp;
+  if (!hit) memset(tmp, 0, c->vsz);
+  a->present = hit != NULL;
+  const int r = a->fn(a->ctx, val, hit != NULL);
+  if (hit && r == CK_REMOVE) {
+    memset(hit, 0, c->isz);
+  } else if (!hit && r == CK_KEEP) {
+    uint8_t *dst = fr;
+    if (!dst) { /* both buckets full: displace a random item of table 0's */
+      dst = blk[0] + (size_t)(sm64(c->rng) % CK_PER) * c->isz;
+      memcpy(a->pend, dst, c->isz);
+      a->has_pend = 1;
+    }
+    memcpy(dst, a->key, 16);
+    memcpy(dst + 16, tmp, c->vsz);
+  }
+}
+
+static void ck_in0(void *p, uint8_t *blk0) {
+  ck_acc *a = (ck_acc *)p;
+  a->blk0 = blk0;
+  oram_access(a->c->t[1], a->b1, ck_in1, a);
+}
+
+typedef struct {
+  cuckoo *c;
+  uint8_t *item;  /* in: the item to place; out: the one it displaced */
+  int placed;
+} ck_kick;
+
+static void ck_kick_fn(void *p, uint8_t *blk) {
+  ck_kick *k = (ck_kick *)p;
+  const cuckoo *c = k->c;
+  uint8_t tmp[16 + CK_VMAX];
+  for (uint32_t i = 0; i < CK_PER; ++i) {
+    uint8_t *it = blk + (size_t)i * c->isz;
+    if (zero(it, 16)) {
+      memcpy(it, k->item, c->isz);
+      k->placed = 1;
+      return;
+    }
+  }
+  uint8_t *v = blk + (size_t)(sm64(c->rng) % CK_PER) * c->isz;
+  memcpy(tmp, v, c->isz);
+  memcpy(v, k->item, c->isz);
+  memcpy(k->item, tmp, c->isz);
+}
+
+/* One access to `key`: both buckets, fn applied to its value.  Returns
+ * whether the key was present. */
+static int cuckoo_access(cuckoo *c, const uint8_t key[16], ck_fn fn, void *ctx) {
+  ck_acc a;
+  a.c = c;
+  a.key = key;
+  a.fn = fn;
+  a.ctx = ctx;
+  a.b1 = ck_bucket(c, 1, key);
+  a.has_pend = 0;
+  a.present = 0;
+  oram_access(c->t[0], ck_bucket(c, 0, key), ck_in0, &a);
+  if (a.has_pend) { /* the displaced item goes to its other table, and so on */
+    ck_kick k = {c, a.pend, 0};
+    int t = 1;
+    for (int step = 0; step < CK_KICKS && !k.placed; ++step, t ^= 1) {
+      c->kicks++;
+      oram_access(c->t[t], ck_bucket(c, t, k.item), ck_kick_fn, &k);
+    }
+    if (!k.placed) abort(); /* table overflow: not reached at 50 % load */
+  }
+  return a.present;
+}
+
+static int ck_leave(void *ctx, uint8_t *val, int present) {
+  (void)ctx, (void)val, (void)present;
+  return CK_LEAVE;
+}
+
+/* a dummy access: the buckets of a random key, nothing changed */
+static void cuckoo_dummy(cuckoo *c) {
+  uint8_t key[16];
+  const uint64_t a = sm64(c->rng), b = sm64(c->rng);
+  memcpy(key, &a, 8);
+  memcpy(key + 8, &b, 8);
+  cuckoo_access(c, key, ck_leave, NULL);
+}
+
+/* ------------------------------------------------------------- the model */
 
 struct gvp_model {
   gvs_config cfg;
@@ -242,14 +417,9 @@ struct gvp_model {
   uint64_t count, ctr, n_mailboxes, head, tail, ring_size;
   uint32_t *ring;
   uint64_t rng;
-  oram *msg, *rows, *dir;
+  cuckoo *msg, *mbox;
+  oram *occ;
 };
-
-static int zero(const uint8_t *p, size_t n) {
-  uint8_t a = 0;
-  for (size_t i = 0; i < n; ++i) a |= p[i];
-  return a == 0;
-}
 
 gvp_model *gvp_create(const gvs_config *cfg) {
   gvp_model *m = (gvp_model *)calloc(1, sizeof *m);
@@ -266,10 +436,10 @@ gvp_model *gvp_create(const gvs_config *cfg) {
   m->ring_size = m->N + m->B;
   m->ring = (uint32_t *)malloc(m->ring_size * sizeof(uint32_t));
   m->rng = 0x70617468u;
-  m->msg = oram_new(m->N, 1024, &m->rng);
-  m->rows = oram_new(m->R, 1024, &m->rng);
-  m->dir = oram_new(m->Q, m->Sr * (uint32_t)sizeof(dir_entry), &m->rng);
-  if (!m->ring || !m->msg || !m->rows || !m->dir) {
+  m->msg = cuckoo_new(m->N, sizeof(gvs_record), &m->rng);
+  m->mbox = cuckoo_new(m->R < m->N ? m->R : m->N, 1024, &m->rng);
+  m->occ = oram_new((m->Q + 255) / 256, 1024, &m->rng);
+  if (!m->ring || !m->msg || !m->mbox || !m->occ) {
     gvp_destroy(m);
     return NULL;
   }
@@ -281,70 +451,75 @@ gvp_model *gvp_create(const gvs_config *cfg) {
 void gvp_destroy(gvp_model *m) {
   if (!m) return;
   free(m->ring);
-  oram_free(m->msg);
-  oram_free(m->rows);
-  oram_free(m->dir);
+  cuckoo_free(m->msg);
+  cuckoo_free(m->mbox);
+  oram_free(m->occ);
   free(m);
 }
 
-/* ---- directory access: lookup, lookup-or-allocate, free ---- */
+/* ---- partition occupancy: read, then add delta ---- */
 typedef struct {
-  uint64_t hi, lo;
-  int op;        /* 0 lookup, 1 lookup or allocate, 2 free row `row`, 3 none (dummy) */
-  uint32_t Sr;
-  int32_t row;   /* out (op 0/1), in (op 2) */
-  int fresh;     /* op 1: the row was allocated by this access */
-} dir_ctx;
-static void dir_fn(void *c, uint8_t *blk) {
-  dir_ctx *x = (dir_ctx *)c;
-  dir_entry *e = (dir_entry *)blk;
-  if (x->op == 3) return;
-  if (x->op == 2) {
-    if (x->row >= 0) memset(&e[x->row], 0, sizeof(dir_entry));
-    return;
-  }
-  int32_t found = -1, first_free = -1;
-  for (uint32_t i = 0; i < x->Sr; ++i) {
-    const int used = (e[i].h_hi | e[i].h_lo) != 0;
-    if (used && e[i].h_hi == x->hi && e[i].h_lo == x->lo) found = (int32_t)i;
-    if (!used && first_free < 0) first_free = (int32_t)i;
-  }
-  x->row = found;
-  x->fresh = 0;
-  if (found < 0 && x->op == 1 && first_free >= 0) {
-    e[first_free].h_hi = x->hi;
-    e[first_free].h_lo = x->lo;
-    x->row = first_free;
-    x->fresh = 1;
-  }
+  uint32_t off;
+  int32_t delta;
+  uint32_t count; /* out: before the delta */
+} occ_ctx;
+static void occ_fn(void *c, uint8_t *blk) {
+  occ_ctx *x = (occ_ctx *)c;
+  uint32_t *e = (uint32_t *)blk;
+  x->count = e[x->off];
+  e[x->off] = (uint32_t)((int32_t)e[x->off] + x->delta);
 }
+/* q < 0: a dummy access (a random block, nothing changed) */
+static uint32_t occ_do(gvp_model *m, int64_t q, int32_t delta) {
+  const uint64_t nblk = (m->Q + 255) / 256;
+  occ_ctx c = {0, 0, 0};
+  uint64_t blk = sm64(&m->rng) % nblk;
+  if (q >= 0) {
+    blk = (uint64_t)q / 256;
+    c.off = (uint32_t)q % 256;
+    c.delta = delta;
+  }
+  oram_access(m->occ, blk, occ_fn, &c);
+  return c.count;
+}
+
 static uint32_t part_of(const gvp_model *m, uint64_t hi) {
   return m->logQ ? (uint32_t)(hi >> (64 - m->logQ)) : 0u;
 }
-static void dir_do(gvp_model *m, uint32_t q, dir_ctx *c) {
-  c->Sr = m->Sr;
-  if (c->op == 3) q = (uint32_t)(sm64(&m->rng) % m->Q);
-  oram_access(m->dir, q, dir_fn, c);
+static void rkey(uint64_t hi, uint64_t lo, uint8_t key[16]) {
+  memcpy(key, &hi, 8);
+  memcpy(key + 8, &lo, 8);
 }
 
-/* ---- mailbox row access ---- */
+/* ---- mailbox row access (the value: recipient + 62 ids) ---- */
 typedef struct {
-  int op;        /* 0 read, 1 append-if-room, 2 pop head, 3 remove id, 4 fresh + append */
+  int op;        /* 0 read, 1 append (create a fresh row if `room`), 2 pop head, 3 remove id */
+  int room;      /* op 1: the partition can take a new recipient */
   uint8_t x[32], id[16];
   uint32_t len_before, len_after;
-  int done;      /* append: there was room; pop: popped; remove: found */
+  int done;      /* append: appended; pop: popped; remove: found */
+  int fresh;     /* op 1: a new row */
   uint8_t head[16];
 } row_ctx;
-static void row_fn(void *c, uint8_t *blk) {
+static int row_fn(void *c, uint8_t *blk, int present) {
   row_ctx *x = (row_ctx *)c;
   uint8_t *ids = blk + 32;
-  if (x->op == 4) memset(blk, 0, 1024), memcpy(blk, x->x, 32);
+  x->done = 0;
+  x->fresh = 0;
+  x->len_before = x->len_after = 0;
+  if (!present) {
+    if (x->op != 1 || !x->room) return CK_LEAVE;
+    memcpy(blk, x->x, 32);
+    memcpy(ids, x->id, 16);
+    x->done = x->fresh = 1;
+    x->len_after = 1;
+    return CK_KEEP;
+  }
   uint32_t len = 0;
   while (len < GVS_MAILBOX_SLOTS && !zero(ids + 16 * len, 16)) ++len;
   x->len_before = len;
   memcpy(x->head, ids, 16);
-  x->done = 0;
-  if ((x->op == 1 || x->op == 4) && len < GVS_MAILBOX_SLOTS) {
+  if (x->op == 1 && len < GVS_MAILBOX_SLOTS) {
     memcpy(ids + 16 * len, x->id, 16);
     ++len;
     x->done = 1;
@@ -363,56 +538,57 @@ static void row_fn(void *c, uint8_t *blk) {
         break;
       }
   }
-  if (len == 0 && x->op != 0) memset(blk, 0, 1024); /* an emptied row is cleared */
   x->len_after = len;
+  if (x->op == 0) return CK_LEAVE;
+  return len == 0 ? CK_REMOVE : CK_KEEP; /* an emptied row leaves the table */
 }
-static void row_do(gvp_model *m, uint32_t q, int32_t row, row_ctx *c) {
-  uint64_t idx;
-  if (row >= 0) idx = (uint64_t)q * m->Sr + (uint32_t)row;
-  else {
-    idx = sm64(&m->rng) % m->R; /* dummy access: same cost */
-    c->op = 0;
+/* key NULL: a dummy access */
+static int row_do(gvp_model *m, const uint8_t *key, row_ctx *c) {
+  if (!key) {
+    cuckoo_dummy(m->mbox);
+    return 0;
   }
-  oram_access(m->rows, idx, row_fn, c);
+  return cuckoo_access(m->mbox, key, row_fn, c);
 }
 
-/* ---- message access: read, or check-and-modify for by-id ops ---- */
+/* ---- message access by id ---- */
 typedef struct {
-  int op;                 /* 0 read, 1 write rec, 2 clear, 3 by-id op of req */
+  int op;                 /* 0 read, 1 insert rec, 2 remove, 3 by-id op of req */
   const gvs_request *rq;
-  const uint8_t *want_id; /* op 0/2: expected id (may be NULL) */
   gvs_record rec, out;
   uint32_t status;
 } msg_ctx;
-static void msg_fn(void *c, uint8_t *blk) {
+static int msg_fn(void *c, uint8_t *blk, int present) {
   msg_ctx *x = (msg_ctx *)c;
   gvs_record *r = (gvs_record *)blk;
   memcpy(&x->out, r, sizeof *r);
-  if (x->op == 1) memcpy(r, &x->rec, sizeof *r);
-  else if (x->op == 2) memset(r, 0, sizeof *r);
-  else if (x->op == 3) {
-    const gvs_request *q = x->rq;
-    const uint32_t t = q->request_type;
-    const int exists = memcmp(r->msg_id, q->msg_id, 16) == 0 && !zero(r->msg_id, 16);
-    const int auth = exists && (memcmp(q->auth_identity, r->sender, 32) == 0 ||
-                                memcmp(q->auth_identity, r->recipient, 32) == 0);
-    x->status = GVS_STATUS_SUCCESS;
-    if (!auth) x->status = GVS_STATUS_NOT_FOUND;
-    else if (t != GVS_REQUEST_READ && memcmp(q->recipient, r->recipient, 32) != 0)
-      x->status = GVS_STATUS_INVALID_RECIPIENT;
-    if (x->status == GVS_STATUS_SUCCESS && t == GVS_REQUEST_UPDATE) {
-      memcpy(r->payload, q->payload, GVS_PAYLOAD_BYTES);
-      r->timestamp = q->timestamp;
-      memcpy(&x->out, r, sizeof *r);
-    } else if (x->status == GVS_STATUS_SUCCESS && t == GVS_REQUEST_DELETE) {
-      memset(r, 0, sizeof *r);
-    }
+  if (x->op == 1) {
+    memcpy(r, &x->rec, sizeof *r);
+    return CK_KEEP;
   }
+  if (x->op == 2) return present ? CK_REMOVE : CK_LEAVE;
+  if (x->op != 3) return CK_LEAVE;
+  const gvs_request *q = x->rq;
+  const uint32_t t = q->request_type;
+  const int auth = present && (memcmp(q->auth_identity, r->sender, 32) == 0 ||
+                               memcmp(q->auth_identity, r->recipient, 32) == 0);
+  x->status = GVS_STATUS_SUCCESS;
+  if (!auth) x->status = GVS_STATUS_NOT_FOUND;
+  else if (t != GVS_REQUEST_READ && memcmp(q->recipient, r->recipient, 32) != 0)
+    x->status = GVS_STATUS_INVALID_RECIPIENT;
+  if (x->status == GVS_STATUS_SUCCESS && t == GVS_REQUEST_UPDATE) {
+    memcpy(r->payload, q->payload, GVS_PAYLOAD_BYTES);
+    r->timestamp = q->timestamp;
+    memcpy(&x->out, r, sizeof *r);
+    return CK_KEEP;
+  }
+  if (x->status == GVS_STATUS_SUCCESS && t == GVS_REQUEST_DELETE) return CK_REMOVE;
+  return CK_LEAVE;
 }
-static void msg_do(gvp_model *m, int64_t slot, msg_ctx *c) {
-  uint64_t idx = slot >= 0 ? (uint64_t)slot : sm64(&m->rng) % m->N;
-  if (slot < 0) c->op = 0;
-  oram_access(m->msg, idx, msg_fn, c);
+/* id NULL: a dummy access */
+static void msg_do(gvp_model *m, const uint8_t *id, msg_ctx *c) {
+  if (!id) cuckoo_dummy(m->msg);
+  else cuckoo_access(m->msg, id, msg_fn, c);
 }
 
 static void fail(gvs_response *o, uint32_t st, uint64_t ts) {
@@ -435,8 +611,9 @@ static void free_slot(gvp_model *m, uint32_t slot) {
   m->count--;
 }
 
-/* Every request: four ORAM accesses (directory, row, message, directory),
- * real or dummy.  Order differs between creates/next ops and by-id ops. */
+/* Every request: six ORAM accesses (occupancy, mailbox table x2, message
+ * table x2, occupancy), real or dummy.  Order differs between creates/next
+ * ops and by-id ops. */
 
 static void g_create(gvp_model *m, const gvs_request *rq, gvs_response *o) {
   const int bad = zero(rq->recipient, 32);
@@ -444,22 +621,25 @@ static void g_create(gvp_model *m, const gvs_request *rq, gvs_response *o) {
   gvo_recipient_hash(m->hash_key, rq->recipient, &hi, &lo);
   const uint32_t q = part_of(m, hi);
   const int full = m->count >= m->N;
-  dir_ctx d = {hi, lo, (bad || full) ? 3 : 1, 0, -1, 0};
-  dir_do(m, q, &d);
-  row_ctx r;
-  memset(&r, 0, sizeof r);
+  const int skip = bad || full;
+  const uint32_t used = occ_do(m, skip ? -1 : (int64_t)q, 0);
   gvs_record rec;
   memset(&rec, 0, sizeof rec);
   const uint32_t slot = m->ring[m->head % m->ring_size];  /* candidate */
   gvo_id_encode(m->prp_key, slot, m->ctr, rec.msg_id);
-  r.op = d.fresh ? 4 : 1;
+  row_ctx r;
+  memset(&r, 0, sizeof r);
+  r.op = 1;
+  r.room = used < m->Sr;
   memcpy(r.x, rq->recipient, 32);
   memcpy(r.id, rec.msg_id, 16);
-  row_do(m, q, (bad || full) ? -1 : d.row, &r);
+  uint8_t key[16];
+  rkey(hi, lo, key);
+  const int present = row_do(m, skip ? NULL : key, &r);
   uint32_t status = GVS_STATUS_SUCCESS;
   if (bad) status = GVS_STATUS_INVALID_RECIPIENT;
   else if (full) status = GVS_STATUS_TOO_MANY_MESSAGES;
-  else if (d.row < 0) status = GVS_STATUS_TOO_MANY_RECIPIENTS;
+  else if (!present && !r.room) status = GVS_STATUS_TOO_MANY_RECIPIENTS;
   else if (!r.done) status = GVS_STATUS_TOO_MANY_MESSAGES_FOR_RECIPIENT;
   msg_ctx mc;
   memset(&mc, 0, sizeof mc);
@@ -472,50 +652,46 @@ static void g_create(gvp_model *m, const gvs_request *rq, gvs_response *o) {
     memcpy(rec.payload, rq->payload, GVS_PAYLOAD_BYTES);
     mc.op = 1;
     mc.rec = rec;
-    msg_do(m, slot, &mc);
+    msg_do(m, rec.msg_id, &mc);
     m->count++;
-    if (d.fresh) m->n_mailboxes++;
+    if (r.fresh) m->n_mailboxes++;
     ok(o, &rec);
   } else {
-    msg_do(m, -1, &mc);
+    msg_do(m, NULL, &mc);
     fail(o, status, rq->timestamp);
   }
-  dir_ctx d2 = {0, 0, 3, 0, -1, 0};
-  dir_do(m, 0, &d2);
+  occ_do(m, r.fresh ? (int64_t)q : -1, 1);
 }
 
 static void g_next(gvp_model *m, const gvs_request *rq, gvs_response *o, int del) {
   uint64_t hi, lo;
   gvo_recipient_hash(m->hash_key, rq->auth_identity, &hi, &lo);
   const uint32_t q = part_of(m, hi);
-  dir_ctx d = {hi, lo, 0, 0, -1, 0};
-  dir_do(m, q, &d);
+  occ_do(m, -1, 0);
   row_ctx r;
   memset(&r, 0, sizeof r);
   r.op = del ? 2 : 0;
-  row_do(m, q, d.row, &r);
-  const int have = d.row >= 0 && r.len_before > 0;
+  uint8_t key[16];
+  rkey(hi, lo, key);
+  const int present = row_do(m, key, &r);
+  const int have = present && r.len_before > 0;
   msg_ctx mc;
   memset(&mc, 0, sizeof mc);
-  int64_t slot = -1;
-  if (have) {
-    uint32_t s;
-    uint64_t ctr;
-    gvo_id_decode(m->prp_key, r.head, m->N, &s, &ctr);
-    slot = s;
-    mc.op = del ? 2 : 0;
-  }
-  msg_do(m, slot, &mc);
-  dir_ctx d2 = {hi, lo, (have && del && r.len_after == 0) ? 2 : 3, 0, d.row, 0};
-  dir_do(m, q, &d2);
+  mc.op = del ? 2 : 0;
+  msg_do(m, have ? r.head : NULL, &mc);
+  const int emptied = have && del && r.len_after == 0;
+  occ_do(m, emptied ? (int64_t)q : -1, -1);
   if (!have) {
     fail(o, GVS_STATUS_NOT_FOUND, rq->timestamp);
     return;
   }
   ok(o, &mc.out);
   if (del) {
-    free_slot(m, (uint32_t)slot);
-    if (r.len_after == 0) m->n_mailboxes--;
+    uint32_t s;
+    uint64_t ctr;
+    gvo_id_decode(m->prp_key, r.head, m->N, &s, &ctr);
+    free_slot(m, s);
+    if (emptied) m->n_mailboxes--;
   }
 }
 
@@ -528,21 +704,21 @@ static void g_byid(gvp_model *m, const gvs_request *rq, gvs_response *o) {
   mc.op = 3;
   mc.rq = rq;
   mc.status = GVS_STATUS_NOT_FOUND;
-  msg_do(m, valid ? (int64_t)slot : -1, &mc);
-  if (!valid) mc.status = GVS_STATUS_NOT_FOUND;
+  msg_do(m, valid ? rq->msg_id : NULL, &mc);
   const int del = mc.status == GVS_STATUS_SUCCESS && rq->request_type == GVS_REQUEST_DELETE;
   uint64_t hi, lo;
   gvo_recipient_hash(m->hash_key, rq->recipient, &hi, &lo);
   const uint32_t q = part_of(m, hi);
-  dir_ctx d = {hi, lo, del ? 0 : 3, 0, -1, 0};
-  dir_do(m, q, &d);
+  occ_do(m, -1, 0);
   row_ctx r;
   memset(&r, 0, sizeof r);
   r.op = 3;
   memcpy(r.id, rq->msg_id, 16);
-  row_do(m, q, del ? d.row : -1, &r);
-  dir_ctx d2 = {hi, lo, (del && r.len_after == 0) ? 2 : 3, 0, d.row, 0};
-  dir_do(m, q, &d2);
+  uint8_t key[16];
+  rkey(hi, lo, key);
+  row_do(m, del ? key : NULL, &r);
+  const int emptied = del && r.done && r.len_after == 0;
+  occ_do(m, emptied ? (int64_t)q : -1, -1);
   if (mc.status != GVS_STATUS_SUCCESS) {
     fail(o, mc.status, rq->timestamp);
     return;
@@ -550,7 +726,7 @@ static void g_byid(gvp_model *m, const gvs_request *rq, gvs_response *o) {
   ok(o, &mc.out);
   if (del) {
     free_slot(m, slot);
-    if (r.len_after == 0) m->n_mailboxes--;
+    if (emptied) m->n_mailboxes--;
   }
 }
 
@@ -591,5 +767,6 @@ int gvp_process_batch(gvp_model *m, const gvs_request *reqs, uint32_t n, gvs_res
 uint64_t gvp_messages(const gvp_model *m) { return m->count; }
 uint64_t gvp_mailboxes(const gvp_model *m) { return m->n_mailboxes; }
 uint64_t gvp_oram_accesses(const gvp_model *m) {
-  return m->msg->accesses + m->rows->accesses + m->dir->accesses;
+  return m->msg->t[0]->accesses + m->msg->t[1]->accesses + m->mbox->t[0]->accesses +
+         m->mbox->t[1]->accesses + m->occ->accesses;
 }

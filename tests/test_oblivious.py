@@ -71,11 +71,15 @@ def short(name):
 def split_batches(vals):
     """Per-batch lists of (kernel, value); launches before the first batch
     (k_seal_init at store creation) are dropped.  Routed stores start each
-    batch with the router."""
+    batch with the router, one k_route_dest..k_route_fill run per source: a
+    batch starts at the k_route_dest that follows a non-router kernel."""
     first = "k_route_dest" if any(k == "k_route_dest" for k, _ in vals) else "k_copy"
-    out, cur = [], None
+    out, cur, prev = [], None, ""
     for k, v in vals:
-        if k == first:
+        starts = k == first and not (first == "k_route_dest" and prev.startswith("k_route_")
+                                     and prev != "k_route_gather")
+        prev = k
+        if starts:
             if cur:
                 out.append(cur)
             cur = []

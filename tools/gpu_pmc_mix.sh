@@ -6,9 +6,10 @@ O=gpurun_out/pmc_mix
 mkdir -p "$O"
 CTRS=${PMC_CTRS:-TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum}
 KERN=${PMC_KERN:-k_rr2_c}
+ARGS=${PMC_ARGS:-}  # e.g. --auth
 for mix in main all_miss_read; do
   timeout -k 10 300 rocprofv3 --pmc $CTRS -d "$O/$mix" -o run --output-format csv -- \
-    python3 tools/oblivious_probe.py $mix --fill-batches 4 --log2n 20 --batch 65536 > "$O/$mix.log" 2>&1 || exit 1
+    python3 tools/oblivious_probe.py $mix --fill-batches 4 --log2n 20 --batch 65536 $ARGS > "$O/$mix.log" 2>&1 || exit 1
 done
 PMC_KERN=$KERN python3 - <<'PY'
 import csv, glob, collections, os
