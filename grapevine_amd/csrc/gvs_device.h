@@ -265,10 +265,10 @@ __device__ inline uint4 shfl4(uint4 v, int src) {
 __device__ inline bool eq4(uint4 a, uint4 b) {
   return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
-__device__ inline bool nz4(uint4 a) { return (a.x | a.y | a.z | a.w) != 0u; }
+__host__ __device__ inline bool nz4(uint4 a) { return (a.x | a.y | a.z | a.w) != 0u; }
 
-__device__ inline uint64_t u4lo(uint4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
-__device__ inline uint64_t u4hi(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
+__host__ __device__ inline uint64_t u4lo(uint4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
+__host__ __device__ inline uint64_t u4hi(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
 
 // Pin a loaded value: the load must happen here even if the value is only
 // used on a rarely taken path (keeps full-table read passes full).

@@ -169,7 +169,7 @@ struct gvs_handle {
   uint32_t S = 1;       // shards in the store
   uint32_t C = 0;       // routed slots per (source, shard)
   uint32_t Bsub = 0;    // requests per source per call (cfg.max_batch)
-  uint32_t Be = 0;      // ops per shard pipeline (Bsub, or next pow2 >= S*C)
+  uint32_t Be = 0;      // ops per shard pipeline (Bsub, or shard_batch(S*C + X))
   std::vector<Engine> eng;
   std::vector<Router> rt;
   ncclComm_t comm = nullptr;
@@ -251,8 +251,7 @@ static int validate(const gvs_config* c) {
   for (int i = 0; i < 2; ++i)
     if (c->reserved[i] != 0) return GVS_ERR_INVALID_ARG;
   if (c->expiry_per_batch &&
-      (!is_pow2(c->expiry_per_batch) || c->expiry_per_batch > c->max_batch / 2 ||
-       c->shard_count > 1))
+      (!is_pow2(c->expiry_per_batch) || c->expiry_per_batch > c->max_batch / 2))
     return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
@@ -267,6 +266,16 @@ static uint32_t auto_capacity(uint32_t B, uint32_t S) {
   uint64_t c = (uint64_t)std::ceil(mu + 8.0 * std::sqrt(mu) + 64.0);
   c = (c + 63) / 64 * 64;
   return (uint32_t)(c < B ? c : B);
+}
+
+// Ops per shard pipeline for m routed slots plus expiry deletes (0: too many).
+// The oracle's cluster model (oracle/gvs_oracle.c gvo_shard_batch) agrees.
+static uint32_t shard_batch(uint64_t m) {
+  uint64_t p2 = 1024;
+  while (p2 < m) p2 <<= 1;
+  const uint64_t r = (m + 8191) / 8192 * 8192;
+  const uint64_t be = std::max<uint64_t>(1024, std::min(p2, r));
+  return be > (1u << (kSeqBits - 1)) ? 0u : (uint32_t)be;
 }
 
 // Transaction slots per message partition (gvs_txn.h): the distinct rows a
@@ -561,25 +570,19 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
     delete h;
     return GVS_ERR_INVALID_ARG;
   }
-  // the expiry sweep's deletes occupy the last X slots of a shard pipeline's
-  // batch; routed pipelines fill those slots with the routed requests
-  // (gvs_create_sharded accepts shard_count 1), so expiry is single-mode only
-  if (mode != kSingle && cfg->expiry_per_batch) {
-    delete h;
-    return GVS_ERR_INVALID_ARG;
-  }
   if (mode == kSingle) {
     h->C = 0;
     h->Be = h->Bsub;
   } else {
+    // a shard pipeline: the S*C routed slots, then the expiry sweep's X
+    // deletes; the smaller of the next power of two and the next multiple of
+    // 8192 (the sorts take any multiple of their tile, gvs_kernels.h)
     h->C = cfg->route_capacity ? cfg->route_capacity : auto_capacity(h->Bsub, h->S);
-    uint64_t be = 1024;
-    while (be < (uint64_t)h->S * h->C) be <<= 1;
-    if (be > (1u << (kSeqBits - 1))) {
+    h->Be = shard_batch((uint64_t)h->S * h->C + cfg->expiry_per_batch);
+    if (h->Be == 0) {
       delete h;
       return GVS_ERR_INVALID_ARG;
     }
-    h->Be = (uint32_t)be;
   }
   auto fail = [&](int code) {
     std::string e = h->err;
@@ -629,27 +632,36 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
 
 // ------------------------------------------------------------------ pipeline
 
-// Bitonic sort of n keys (n a power of two >= 1024): tiles of L = 1024 E keys
-// sorted in registers/LDS, then for each larger merge level the global steps
-// (two per launch) and the tile-local finish.
+// Bitonic sort of n keys (n a multiple of L = 1024 E, gvs_kernels.h): tiles
+// sorted in registers/LDS, then for each merge level k up to the power of two
+// >= n the global steps (two per launch) and the tile-local finish.
+static uint32_t lower_count(uint32_t n, uint32_t blk, uint32_t half) {
+  return (n / blk) * half + std::min(n % blk, half);  // indices b*blk + o < n, o < half
+}
+
 template <typename K, int E>
 static void sort_tiles(hipStream_t s, K* d, uint32_t n) {
   constexpr uint32_t L = 1024u * E;
   hipLaunchKernelGGL((k_bitonic_tile<K, E>), dim3(n / L), dim3(1024), 0, s, d, 0u, 1);
-  for (uint32_t k = 2 * L; k <= n; k <<= 1) {
+  for (uint32_t k = 2 * L; (k >> 1) < n; k <<= 1) {
     uint32_t j = k >> 1;
-    for (; j >= 2 * L; j >>= 2)  // two steps per launch while both are global
-      hipLaunchKernelGGL(k_bitonic_global2<K>, dim3((n / 4 + 255) / 256), dim3(256), 0, s, d, n, k, j);
-    if (j >= L)
-      hipLaunchKernelGGL(k_bitonic_global<K>, dim3((n / 2 + 255) / 256), dim3(256), 0, s, d, n, k, j);
+    for (; j >= 2 * L; j >>= 2) {  // two steps per launch while both are global
+      const uint32_t nq = lower_count(n, 2 * j, j >> 1);
+      hipLaunchKernelGGL(k_bitonic_global2<K>, dim3((nq + 255) / 256), dim3(256), 0, s, d, n, k, j, nq);
+    }
+    if (j >= L) {
+      const uint32_t np = lower_count(n, 2 * j, j);
+      hipLaunchKernelGGL(k_bitonic_global<K>, dim3((np + 255) / 256), dim3(256), 0, s, d, n, k, j, np);
+    }
     hipLaunchKernelGGL((k_bitonic_tile<K, E>), dim3(n / L), dim3(1024), 0, s, d, k, 0);
   }
 }
 
 template <typename K, int EMAX>
 static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
-  if (n < 1024 || !is_pow2(n)) return GVS_ERR_INTERNAL;
-  const uint32_t e = n / 1024 < (uint32_t)EMAX ? n / 1024 : (uint32_t)EMAX;
+  if (n < 1024 || n % 1024) return GVS_ERR_INTERNAL;
+  uint32_t e = EMAX;  // the largest tile that divides n
+  while ((n / 1024) % e) e >>= 1;
   switch (e) {
     case 1: sort_tiles<K, 1>(h->stream, d, n); break;
     case 2: sort_tiles<K, 2>(h->stream, d, n); break;
@@ -1098,7 +1110,8 @@ static int check_epoch(gvs_handle* h) {
 }
 
 static uint32_t max_submit(const gvs_handle* h) {
-  return h->Bsub * (h->mode == kLocal ? h->S : 1u) - h->eng[0].X;
+  // sharded: the expiry deletes have their own slots past the routed ones
+  return h->mode == kSingle ? h->Bsub - h->eng[0].X : h->Bsub * (h->mode == kLocal ? h->S : 1u);
 }
 
 
@@ -1595,6 +1608,41 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
   return GVS_OK;
 }
 
+
+// The router's placement on the host, with the device's route_dest (see
+// include/gvstore_test.h): slot[i] = d * C + rank of request i among this
+// source's requests for shard d, or 0xFFFFFFFF past C.
+int gvs_route_plan(const gvs_config* cfg, const gvs_request* reqs, uint32_t n, uint32_t* slot,
+                   uint32_t* capacity, uint32_t* shard_batch_out) {
+  if (!cfg || (n && (!reqs || !slot))) return GVS_ERR_INVALID_ARG;
+  if (int rc = validate(cfg)) return rc;
+  const uint32_t S = cfg->shard_count ? cfg->shard_count : 1u, B = cfg->max_batch;
+  if (n > B) return GVS_ERR_INVALID_ARG;
+  const uint32_t C = cfg->route_capacity ? cfg->route_capacity : auto_capacity(B, S);
+  RouteArgs a{};
+  a.in = reinterpret_cast<const uint4*>(reqs);
+  a.n = n;
+  a.B = B;
+  a.S = S;
+  a.C = C;
+  a.N = cfg->msg_capacity;
+  a.kc.pk0 = ld64(cfg->secret_key);
+  a.kc.pk1 = ld64(cfg->secret_key + 8);
+  a.kc.hk0 = ld64(cfg->secret_key + 16);
+  a.kc.hk1 = ld64(cfg->secret_key + 24);
+  a.kc.nshards = S;
+  std::vector<uint32_t> cnt(S, 0);
+  bool over = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t d = route_dest(a, i);
+    const uint32_t r = cnt[d]++;
+    over |= r >= C;
+    slot[i] = r < C ? d * C + r : kNone;
+  }
+  if (capacity) *capacity = C;
+  if (shard_batch_out) *shard_batch_out = S > 1 ? shard_batch((uint64_t)S * C + cfg->expiry_per_batch) : B;
+  return over ? GVS_ERR_BATCH_OVERFLOW : GVS_OK;
+}
 #endif  // GVS_TEST_HOOKS
 
 

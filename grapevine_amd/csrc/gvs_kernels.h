@@ -60,8 +60,18 @@ __device__ inline K cmpex_keep(const K& mine, const K& other, bool keep_min) {
   return key_sel(lt == keep_min, other, mine);
 }
 
-// Bitonic sort inside tiles of L = 1024 * E keys (full = 1), or the last
-// steps j = L/2 .. 1 of merge level kmerge (full = 0).  Thread t holds keys
+// Bitonic sort of n keys, n a multiple of the tile size L = 1024 * E (not
+// necessarily a power of two).  Tiles are sorted ascending by the classic
+// network (full = 1: direction of element i at level k from bit k of its
+// index inside the tile, so every tile ends ascending).  Merge levels k > L
+// use the all-ascending form: the first step of a level pairs i with its
+// mirror i ^ (k - 1) in the k-block, the later steps pair i with i + j.  The
+// keys past n count as +inf: every comparator puts the smaller key at the
+// lower index, so a pair whose upper index is >= n never exchanges and those
+// keys are neither read nor written.
+//
+// k_bitonic_tile: a whole tile sort (full = 1), or the last steps j = L/2 .. 1
+// of merge level kmerge (full = 0, ascending).  Thread t holds keys
 // t*E .. t*E + E - 1 in registers: steps j < E are register compare-exchanges,
 // steps E <= j < 64 E exchange with lane t ^ (j / E) by shuffles, and only
 // steps j >= 64 E go through LDS with a barrier each (Key128, 4096-key tiles:
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
       for (uint32_t j = j_top; j >= 64u * E; j >>= 1) {
         for (uint32_t p = t; p < (L >> 1); p += 1024u) {
           const uint32_t i = ((p / j) * 2u * j) + (p % j);
-          const bool asc = ((base + i) & k) == 0u;
+          const bool asc = !full || (i & k) == 0u;
           const K a = s[i], b = s[i + j];
           const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
           s[i] = key_sel(sw, b, a);
@@ -104,7 +114,7 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
       const bool lower = (lane & m) == 0u;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const bool asc = ((base + t * E + e) & k) == 0u;
+        const bool asc = !full || ((t * E + e) & k) == 0u;
         r[e] = cmpex_keep(r[e], shfl_xor_key(r[e], m), lower == asc);
       }
     }
@@ -115,7 +125,7 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           if ((e & j) == 0u) {
-            const bool asc = ((base + t * E + e) & k) == 0u;
+            const bool asc = !full || ((t * E + e) & k) == 0u;
             const K a = r[e], b = r[e | j];
             const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
             r[e] = key_sel(sw, b, a);
@@ -129,46 +139,52 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
   for (int e = 0; e < E; ++e) data[base + t * E + e] = r[e];
 }
 
-// Two steps (j, j/2) of merge level k over the whole array: each thread owns
-// the four keys i0, i0 + j/2, i0 + j, i0 + 3j/2.
+// Two steps (j, j/2) of merge level k over the array: each thread owns the
+// four keys whose lowest index is x0 = (block of 2j) + o, o < j/2.  First
+// step of the level (flip, j = k/2): quadruple {x0, x0 + h, m - h, m} with
+// m = x0 ^ (2j - 1) its mirror; else {x0, x0 + h, x0 + j, x0 + j + h}.
+// nq = quadruples with x0 < n.
 template <typename K>
 __global__ __launch_bounds__(256) void k_bitonic_global2(K* data, uint32_t n, uint32_t k,
-                                                         uint32_t j) {
+                                                         uint32_t j, uint32_t nq) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= (n >> 2)) return;
+  if (p >= nq) return;
   const uint32_t h = j >> 1;
-  // a group of 2j indices holds h quadruples x0, x0 + h, x0 + j, x0 + j + h
   const uint32_t g = p / h, o = p % h;
-  const uint32_t x0 = g * 2u * j + o;  // bits h and j of x0 are zero
-  const uint32_t x1 = x0 + h, x2 = x0 + j, x3 = x0 + j + h;
-  const bool asc = (x0 & k) == 0u;
-  K v0 = data[x0], v1 = data[x1], v2 = data[x2], v3 = data[x3];
-  auto cx = [&](K& a, K& b) {
-    const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
-    const K ta = a;
-    a = key_sel(sw, b, a);
-    b = key_sel(sw, ta, b);
+  const uint32_t x0 = g * 2u * j + o;
+  const bool flip = (j << 1) == k;
+  const uint32_t m = x0 ^ (2u * j - 1u);
+  uint32_t x[4] = {x0, x0 + h, flip ? m - h : x0 + j, flip ? m : x0 + j + h};
+  K v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = x[q] < n ? data[x[q]] : v[0];
+  auto cx = [&](int a, int b) {  // x[a] < x[b]; a key past n is +inf
+    const bool sw = x[b] < n && key_lt(v[b], v[a]);
+    const K ta = v[a];
+    v[a] = key_sel(sw, v[b], v[a]);
+    v[b] = key_sel(sw, ta, v[b]);
   };
-  cx(v0, v2);
-  cx(v1, v3);
-  cx(v0, v1);
-  cx(v2, v3);
-  data[x0] = v0;
-  data[x1] = v1;
-  data[x2] = v2;
-  data[x3] = v3;
+  cx(0, flip ? 3 : 2);
+  cx(1, flip ? 2 : 3);
+  cx(0, 1);
+  cx(2, 3);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (x[q] < n) data[x[q]] = v[q];
 }
 
+// One step j of merge level k: pair (i, i ^ (2j - 1)) on the level's first
+// step, else (i, i + j); np = pairs with i < n.
 template <typename K>
 __global__ __launch_bounds__(256) void k_bitonic_global(K* data, uint32_t n, uint32_t k,
-                                                        uint32_t j) {
-  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= (n >> 1)) return;
-  uint32_t i = ((p / j) * 2u * j) + (p % j);
-  uint32_t pj = i + j;
-  bool asc = ((i & k) == 0u);
+                                                        uint32_t j, uint32_t np) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const uint32_t i = ((p / j) * 2u * j) + (p % j);
+  const uint32_t pj = (j << 1) == k ? i ^ (2u * j - 1u) : i + j;
+  if (pj >= n) return;  // +inf partner: no exchange (depends on n only)
   const K a = data[i], b = data[pj];
-  const bool sw = asc ? key_lt(b, a) : key_lt(a, b);
+  const bool sw = key_lt(b, a);
   // both keys are stored whatever the comparison says: a store only on a
   // swap would make the written bytes depend on the key order
   data[i] = key_sel(sw, b, a);

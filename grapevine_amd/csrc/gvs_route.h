@@ -35,8 +35,9 @@ struct RouteArgs {
   KeyCtx kc;
 };
 
-// request i -> owning shard (S = padding, i >= n)
-__device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
+// request i -> owning shard (S = padding, i >= n).  Host and device: the
+// test library's gvs_route_plan runs this same function on the CPU.
+__host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
   if (i >= a.n) return a.S;
   const uint4* r = a.in + (uint64_t)i * kAbiU4;
   const uint4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3], c4 = r[4];

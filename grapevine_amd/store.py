@@ -32,7 +32,8 @@ EXPORTED = (
     "gvs_omap_create", "gvs_omap_destroy", "gvs_omap_access_batch", "gvs_omap_access_batch_device",
     "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
 )
-TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw")
+TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
+                 "gvs_route_plan")
 
 
 def test_hooks_enabled():
@@ -79,6 +80,8 @@ def load_library(path=None):
         lib.gvs_raw_size.argtypes = [vp, u32, u32, ctypes.POINTER(u64)]
         lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
         lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
+        P32 = ctypes.POINTER(u32)
+        lib.gvs_route_plan.argtypes = [ctypes.POINTER(abi.GvsConfig), vp, u32, vp, P32, P32]
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p
@@ -107,6 +110,21 @@ def load_library(path=None):
     if path is None:
         _LIB = lib
     return lib
+
+
+def route_plan(config, reqs):
+    """The router's placement of one source's batch, on the host (test
+    library, gvs_route_plan): -> (slot per request, C, shard pipeline size,
+    overflowed)."""
+    lib = load_library(_TEST_LIB_PATH)
+    reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+    slot = np.zeros(len(reqs), dtype=np.uint32)
+    cap, be = ctypes.c_uint32(), ctypes.c_uint32()
+    rc = lib.gvs_route_plan(ctypes.byref(config), reqs.ctypes.data, len(reqs), slot.ctypes.data,
+                            ctypes.byref(cap), ctypes.byref(be))
+    if rc not in (0, abi.GVS_ERR_BATCH_OVERFLOW):
+        raise GvsError(rc, "gvs_route_plan failed")
+    return slot, cap.value, be.value, rc == abi.GVS_ERR_BATCH_OVERFLOW
 
 
 def comm_unique_id():

@@ -142,10 +142,12 @@ typedef struct gvs_config {
   uint32_t shard_index;         /* this process's shard (gvs_create_sharded) */
   uint32_t route_capacity;      /* C: request slots per (source, shard) pair and
                                    batch; 0 = automatic */
-  uint32_t expiry_per_batch;    /* X: expiry-sweep deletes per batch;
-                                   0 = off, else a power of two <= max_batch / 2,
-                                   unsharded stores only.  Callers then submit at
-                                   most max_batch - X requests per batch. */
+  uint32_t expiry_per_batch;    /* X: expiry-sweep deletes per batch and shard
+                                   (DESIGN.md §9); 0 = off, else a power of two
+                                   <= max_batch / 2.  Unsharded callers then submit
+                                   at most max_batch - X requests per batch; a
+                                   sharded store gives the deletes slots of their
+                                   own in each shard's pipeline. */
   uint32_t reserved[2];         /* must be 0 */
 } gvs_config;
 
@@ -211,7 +213,9 @@ int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
  * per workgroup), and the following batch deletes them, if still
  * older than its cutoff, through X trailing delete slots: the message row, its
  * mailbox entry and its slot are freed as by a recipient's DELETE.  0 = none.
- * Requires gvs_config.expiry_per_batch > 0 for any effect. */
+ * Requires gvs_config.expiry_per_batch > 0 for any effect.  Sharded: every
+ * shard sweeps its own table; gvs_create_sharded ranks must all set the same
+ * cutoff before the same batch. */
 int gvs_set_expiry_cutoff(gvs_handle *h, uint64_t cutoff);
 
 /* Single-request shim in the shape of ObliviousHashMap::access_and_insert. */

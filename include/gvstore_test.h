@@ -29,6 +29,15 @@ int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset
 int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset,
                   const void *src, uint64_t bytes);
 
+/* The router's placement of one source's batch, computed on
+ * the host by the device's own routing function: slot[i] = d * C + (rank of
+ * request i among this batch's requests for shard d), or 0xFFFFFFFF when that
+ * rank is >= C (the batch then overflows: GVS_ERR_BATCH_OVERFLOW).  Also
+ * reports C and the shard pipeline size.  No device is touched; the CPU
+ * multi-process tests use it to run the real placement over gloo. */
+int gvs_route_plan(const gvs_config *cfg, const gvs_request *reqs, uint32_t n, uint32_t *slot,
+                   uint32_t *capacity, uint32_t *shard_batch);
+
 #ifdef __cplusplus
 }
 #endif

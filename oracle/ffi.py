@@ -107,6 +107,9 @@ def lib():
         L.gvo_cluster_shard.restype = vp
         L.gvo_cluster_process.argtypes = [vp, vp, u32, vp]
         L.gvo_cluster_process.restype = ctypes.c_int
+        L.gvo_cluster_set_expiry_cutoff.argtypes = [vp, u64]
+        L.gvo_shard_batch.argtypes = [u64]
+        L.gvo_shard_batch.restype = u32
         for f in ("gvo_cluster_messages", "gvo_cluster_mailboxes"):
             getattr(L, f).argtypes = [vp]
             getattr(L, f).restype = u64
@@ -159,6 +162,11 @@ def route(config, reqs):
 
 def route_capacity(batch, n_shards):
     return lib().gvo_route_capacity(batch, n_shards)
+
+
+def shard_batch(slots):
+    """Ops per shard pipeline for `slots` routed slots plus expiry deletes."""
+    return lib().gvo_shard_batch(slots)
 
 
 def aes128_encrypt(key16: bytes, block16: bytes) -> bytes:
@@ -327,6 +335,9 @@ class Cluster:
         if rc != 0:
             raise ValueError(f"oracle cluster rejected batch: {rc}")
         return out
+
+    def set_expiry_cutoff(self, cutoff):
+        self.L.gvo_cluster_set_expiry_cutoff(self.c, int(cutoff))
 
     def seed(self, s):
         self.rng = ctypes.c_uint64(s)

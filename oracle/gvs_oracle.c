@@ -180,7 +180,7 @@ static int is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 gvo_model *gvo_create(const gvs_config *cfg) {
   if (!cfg || !is_pow2(cfg->msg_capacity) || cfg->msg_capacity < 256 ||
       !is_pow2(cfg->mailbox_partitions) || cfg->mailbox_partition_slots == 0 ||
-      !is_pow2(cfg->max_batch))
+      cfg->max_batch < 1024 || cfg->max_batch % 1024) /* a shard pipeline: any multiple */
     return NULL;
   gvo_model *m = (gvo_model *)calloc(1, sizeof *m);
   if (!m) return NULL;
@@ -222,7 +222,8 @@ gvo_model *gvo_create(const gvs_config *cfg) {
   m->W = (uint32_t)(m->N / S);
   m->X = cfg->expiry_per_batch;
   if (m->X) {
-    if (!is_pow2(m->X) || m->X > m->B / 2) {
+    /* a shard model's B is its pipeline (gvo_shard_batch), X slots included */
+    if (!is_pow2(m->X) || m->X > (cfg->shard_count > 1 ? m->B - 1 : m->B / 2)) {
       gvo_destroy(m);
       return NULL;
     }
@@ -742,8 +743,20 @@ struct gvo_cluster {
   uint32_t *dest, *cnt;
 };
 
+/* Ops per shard pipeline for m routed slots plus expiry deletes: the smaller
+ * of the next power of two and the next multiple of 8192, at least 1024
+ * (gvs_engine.hip shard_batch). */
+uint32_t gvo_shard_batch(uint64_t m) {
+  uint64_t p2 = 1024;
+  while (p2 < m) p2 <<= 1;
+  const uint64_t r = (m + 8191) / 8192 * 8192;
+  const uint64_t be = p2 < r ? p2 : r;
+  return (uint32_t)(be < 1024 ? 1024 : be);
+}
+
 gvo_cluster *gvo_cluster_create(const gvs_config *cfg) {
   if (!cfg || cfg->shard_count < 1) return NULL;
+  if (cfg->expiry_per_batch > cfg->max_batch / 2) return NULL;
   gvo_cluster *c = (gvo_cluster *)calloc(1, sizeof *c);
   if (!c) return NULL;
   c->cfg = *cfg;
@@ -763,9 +776,7 @@ gvo_cluster *gvo_cluster_create(const gvs_config *cfg) {
     gvs_config sc = *cfg;
     sc.shard_count = c->S;
     sc.shard_index = k;
-    uint32_t be = 1024;
-    while (be < c->S * c->C) be <<= 1;
-    sc.max_batch = be;
+    sc.max_batch = gvo_shard_batch((uint64_t)c->S * c->C + cfg->expiry_per_batch);
     c->shard[k] = gvo_create(&sc);
     if (!c->shard[k]) {
       gvo_cluster_destroy(c);
@@ -811,6 +822,10 @@ int gvo_cluster_process(gvo_cluster *c, const gvs_request *reqs, uint32_t n, gvs
       if (c->dest[i] == d) out[i] = c->subout[m++];
   }
   return GVS_OK;
+}
+
+void gvo_cluster_set_expiry_cutoff(gvo_cluster *c, uint64_t cutoff) {
+  for (uint32_t k = 0; k < c->S; ++k) gvo_set_expiry_cutoff(c->shard[k], cutoff);
 }
 
 uint64_t gvo_cluster_messages(const gvo_cluster *c) {

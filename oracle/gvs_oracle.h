@@ -96,6 +96,8 @@ gvo_model *gvo_cluster_shard(gvo_cluster *c, uint32_t k);
  * GVS_ERR_BATCH_OVERFLOW (nothing applied) if one source has more than C
  * requests for one shard. */
 int gvo_cluster_process(gvo_cluster *c, const gvs_request *reqs, uint32_t n, gvs_response *out);
+void gvo_cluster_set_expiry_cutoff(gvo_cluster *c, uint64_t cutoff);
+uint32_t gvo_shard_batch(uint64_t m); /* ops per shard pipeline for m slots */
 uint64_t gvo_cluster_messages(const gvo_cluster *c);
 uint64_t gvo_cluster_mailboxes(const gvo_cluster *c);
 void gvo_cluster_gen_batch(const gvo_cluster *c, const gvo_gen_params *p, uint64_t *rng,

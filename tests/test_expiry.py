@@ -177,3 +177,71 @@ def test_gpu_expiry_parity(n_msgs, Q, Sr, X, auth):
     dt = diff_tables(store.dump_messages(), m.dump_messages())
     assert not dt, "\n".join(dt)
     assert expired > 0
+
+
+def cluster(S=2, n_msgs=4096, Q=16, Sr=32, B=1024, X=128, C=0):
+    cfg = abi.make_config(n_msgs, mailbox_partitions=Q, mailbox_partition_slots=Sr, max_batch=B,
+                          expiry_per_batch=X, shard_count=S, route_capacity=C)
+    return cfg, ffi.Cluster(cfg)
+
+
+def test_sharded_expiry_every_shard_sweeps_its_own_table():
+    """Sharded stores: each shard's pipeline carries its own X expiry slots
+    after the S*C routed ones, so callers still submit S*B requests."""
+    S, B, X = 2, 1024, 128
+    cfg, cl = cluster(S=S, B=B, X=X)
+    assert ffi.shard_batch(S * cl.capacity + X) >= S * cl.capacity + X
+    cl.seed(5)
+    fill_p = ffi.gen_params(create=100, read=0, update=0, delete=0, miss=0, bad_auth=0,
+                            bad_recipient=0, hard_error=0, zero_recipient=0, n_identities=128)
+    for _ in range(2):
+        assert cl.process_batch(cl.gen_batch(S * B, fill_p)) is not None
+    n0 = cl.messages
+    per_shard0 = [cl.shard(k).messages for k in range(S)]
+    assert min(per_shard0) > 200
+    cl.set_expiry_cutoff(TS0 + 10**7)
+    for _ in range(3):
+        assert cl.process_batch(np.zeros(0, dtype=abi.REQUEST_DTYPE)) is not None
+    # one sweep, then X deletes per shard and batch (W = 16 x 8 records)
+    assert n0 - cl.messages == 2 * S * X
+    assert all(per_shard0[k] - cl.shard(k).messages == 2 * X for k in range(S))
+
+
+def test_shard_batch_rule():
+    # the smaller of the next power of two and the next multiple of 8192
+    assert ffi.shard_batch(1536) == 2048
+    assert ffi.shard_batch(5376) == 8192
+    assert ffi.shard_batch(72192) == 73728      # C3 routed 8 ways: not 131072
+    assert ffi.shard_batch(18048) == 24576
+    assert ffi.shard_batch(100) == 1024
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,B,X", [(2, 1024, 128), (4, 1024, 64)])
+def test_gpu_sharded_expiry_parity(S, B, X):
+    from grapevine_amd.store import ObliviousStore
+    cfg, cl = cluster(S=S, B=B, X=X)
+    store = ObliviousStore(cfg)
+    assert store.stats()["shard_batch"] == ffi.shard_batch(S * cl.capacity + X)
+    cl.seed(43 + S)
+    n = S * B
+    params = ffi.gen_params(create=40, read=20, update=20, delete=20, n_identities=300)
+    expired = 0
+    for b in range(12):
+        cutoff = TS0 + max(0, cl.ops - int(1.5 * n)) if b >= 2 else 0
+        cl.set_expiry_cutoff(cutoff)
+        store.set_expiry_cutoff(cutoff)
+        before = cl.messages
+        reqs = cl.gen_batch(n, params)
+        want = cl.process_batch(reqs)
+        got = store.process_batch(reqs)
+        d = diff_responses(got, want, reqs)
+        assert not d, f"batch {b}: " + "\n".join(d)
+        st = store.stats()
+        assert (st["messages"], st["mailboxes"]) == (cl.messages, cl.mailboxes), b
+        creates = int(((reqs["request_type"] == 1) & (want["status_code"] == 1)).sum())
+        deletes = int(((reqs["request_type"] == 4) & (want["status_code"] == 1)).sum())
+        expired += before + creates - deletes - cl.messages
+    dt = diff_tables(store.dump_messages(), cl.dump_messages())
+    assert not dt, "\n".join(dt)
+    assert expired > 0

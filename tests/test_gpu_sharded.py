@@ -92,3 +92,16 @@ def test_rccl_single_rank_routed_path():
     model.seed(50)
     run_stream(store, model, ffi.gen_params(n_identities=300), batches=6, n=1024)
     store.close()
+
+
+def test_local_shards_pipeline_not_a_power_of_two():
+    """S*C = 2 x 9024 routed slots: the shard pipeline is 24576 ops (a multiple
+    of the sort tiles, not the next power of two 32768), so the sorts run
+    their non-power-of-two network and the table passes a ragged batch."""
+    S, B = 2, 16384
+    store, cl = sharded_pair(S, N=1 << 16, B=B, Q=64, Sr=64)
+    st = store.stats()
+    assert st["shard_batch"] == ffi.shard_batch(S * cl.capacity) == 24576
+    cl.seed(51)
+    run_stream(store, cl, ffi.gen_params(n_identities=3000), batches=4, n=S * B)
+    run_stream(store, cl, ffi.gen_params(n_identities=3000), batches=1, n=S * B - 777)

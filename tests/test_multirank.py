@@ -2,15 +2,19 @@
 DESIGN.md §6 run as one process per rank, with the oracle standing in for
 each rank's shard pipeline.
 
-Each rank owns shard `rank`.  Every step, each rank takes its own batch,
-routes each request to its owning shard (the engine's rule, restated in
-oracle/gvs_oracle.c gvo_route) into S buckets of exactly C slots padded with
-zero requests, exchanges the buckets with all_to_all, runs its shard on the
-S*C received slots, returns the responses with a second all_to_all and puts
-them back in request order.  The result must equal the single-process
-cluster model on the concatenated batch, rank by rank and bit for bit, and
-every shard's state must equal the cluster's shard.  Timing follows bench.py
-(barrier, max over ranks)."""
+Each rank owns shard `rank`.  Every step, each rank takes its own batch and
+places each request with the engine's own router (gvs_route_plan of the test
+library: the device's route_dest run on the host) into S buckets of exactly
+C slots padded with zero requests; the placement is cross-checked against the
+oracle's restatement (gvo_route).  The ranks agree on overflow with a MAX
+all-reduce (the engine's error agreement): if any rank's bucket overflows,
+every rank rejects the batch and nothing is applied, as the cluster model
+says.  Otherwise the buckets go all_to_all, each rank runs its shard on the
+S*C received slots (a shard pipeline of gvs_route_plan's size), the responses
+return with a second all_to_all and are put back in request order.  The
+result must equal the single-process cluster model on the concatenated
+batch, rank by rank and bit for bit, and every shard's state must equal the
+cluster's shard.  Timing follows bench.py (barrier, max over ranks)."""
 import json
 import os
 import socket
@@ -28,52 +32,58 @@ WORKER = textwrap.dedent("""
     import torch
     import torch.distributed as dist
     sys.path.insert(0, {root!r})
-    from grapevine_amd import abi, dist as gdist
+    from grapevine_amd import abi, dist as gdist, store as gstore
     from oracle import ffi
     ri = gdist.init("gloo")
     S, r, B = ri.world, ri.rank, 1024
     base = dict(mailbox_partitions=8, mailbox_partition_slots=32, max_batch=B, shard_count=S)
     ccfg = abi.make_config(4096, **base)
     replica = ffi.Cluster(ccfg)              # whole-store oracle, identical on every rank
-    C = replica.capacity
-    be = 1024
-    while be < S * C:
-        be *= 2
+    _, C, be, _ = gstore.route_plan(ccfg, np.zeros(0, dtype=abi.REQUEST_DTYPE))
+    assert C == replica.capacity and be == ffi.shard_batch(S * C)
     scfg = abi.make_config(4096, **dict(base, max_batch=be, shard_index=r))
     shard = ffi.Model(scfg)                  # this rank's shard
     replica.seed(1234)
     p = ffi.gen_params(n_identities=300, hard_error=2, zero_recipient=2)
+    hot = ffi.gen_params(create=100, read=0, update=0, delete=0, hot=70, n_identities=300)
     rec = abi.REQUEST_DTYPE.itemsize
     gdist.barrier(ri)
     t0 = time.perf_counter()
-    checked = 0
-    for step in range(4):
+    checked = rejected = 0
+    for step in range(6):
+        # step 2: one source's batch is hot on one recipient (overflows its bucket)
         glob = replica.gen_batch(S * B, p)       # every source's batch, concatenated
-        want = replica.process_batch(glob)
+        if step == 2:
+            glob[:B] = replica.gen_batch(B, hot)
+        want = replica.process_batch(glob)       # None: the cluster rejects the batch
         mine = glob[r * B:(r + 1) * B]
-        dest = ffi.route(ccfg, mine)
+        slot, _, _, over = gstore.route_plan(ccfg, mine)
+        dest = ffi.route(ccfg, mine)             # the oracle's restatement agrees
+        placed = slot != 0xFFFFFFFF
+        assert (slot[placed] // C == dest[placed]).all()
+        flag = torch.tensor([1 if over else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item():
+            assert want is None and step == 2
+            rejected += 1
+            continue
+        assert want is not None
         send = np.zeros(S * C, dtype=abi.REQUEST_DTYPE)
-        pos = np.zeros(B, dtype=np.int64)
-        fill = np.zeros(S, dtype=np.int64)
-        for i, d in enumerate(dest):
-            assert fill[d] < C                   # no overflow at this capacity
-            pos[i] = d * C + fill[d]
-            send[pos[i]] = mine[i]
-            fill[d] += 1
+        send[slot] = mine
         recv = torch.empty(S * C * rec, dtype=torch.uint8)
         dist.all_to_all_single(recv, torch.from_numpy(send.view(np.uint8).copy()))
         sub = recv.numpy().view(abi.REQUEST_DTYPE)
         out = shard.process_batch(sub)           # pads are type 0: hard errors
         back = torch.empty(S * C * rec, dtype=torch.uint8)
         dist.all_to_all_single(back, torch.from_numpy(out.view(np.uint8).copy()))
-        got = back.numpy().view(abi.RESPONSE_DTYPE)[pos]
+        got = back.numpy().view(abi.RESPONSE_DTYPE)[slot]
         assert got.tobytes() == want[r * B:(r + 1) * B].tobytes(), step
         checked += B
     el = gdist.max_over_ranks(ri, time.perf_counter() - t0)
     total = gdist.sum_over_ranks(ri, checked)
     rs = replica.shard(r)
     with open(os.path.join({out!r}, "rank%d.json" % r), "w") as f:
-        json.dump(dict(rank=r, world=S, elapsed=el, total=total, capacity=C,
+        json.dump(dict(rank=r, world=S, elapsed=el, total=total, capacity=C, rejected=rejected,
                        digest_ok=shard.digest() == rs.digest(),
                        messages=shard.messages, replica_messages=rs.messages,
                        cluster_messages=replica.messages), f)
@@ -106,7 +116,8 @@ def test_sharded_protocol_gloo(tmp_path, world):
     rows = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(world)]
     assert sorted(x["rank"] for x in rows) == list(range(world))
     assert len({x["elapsed"] for x in rows}) == 1          # max over ranks, same everywhere
-    assert all(x["total"] == world * 4 * 1024 for x in rows)  # weak scaling: work adds up
+    assert all(x["total"] == world * 5 * 1024 for x in rows)  # weak scaling: work adds up
+    assert all(x["rejected"] == 1 for x in rows)            # overflow agreed by every rank
     assert all(x["digest_ok"] for x in rows)
     assert all(x["messages"] == x["replica_messages"] for x in rows)
     assert sum(x["messages"] for x in rows) == rows[0]["cluster_messages"] > 0

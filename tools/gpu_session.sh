@@ -33,6 +33,7 @@ case "$2" in
   obl) step oblivious 1100 $PT tests/test_oblivious.py -k "plain or launch" ;;
   tobl) tests && step oblivious 900 $PT tests/test_oblivious.py -k "plain or launch" ;;
   oblx) step oblivious_x 1000 $PT tests/test_oblivious.py -k "auth or routed" ;;
+  tdiag) tests && bash "$0" "$1" m2diag ;;
   m2diag)  # write/read request counters of the auth mailbox pass under two mixes
     PMC_ARGS=--auth PMC_KERN=k_m2x,k_rpass2 PMC_CTRS="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum" \
       step pmc_mix 400 bash tools/gpu_pmc_mix.sh
