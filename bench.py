@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="CPU baseline instances (host threads); 0 = this process's CPU share")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--host-steps", type=int, default=8,
+                   help="batches timed through the host API (gvs_process_batches) after the device run")
     p.add_argument("--routed", action="store_true",
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
@@ -291,7 +293,8 @@ def main():
     pool[:, 0] |= 1
     known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000,
                     per_batch=B - a.expiry)
-    batches = gen_batches(torch, dev, B, a.warmup + a.steps, known, pool, g, 1_800_000_000)
+    n_host = a.host_steps + (2 if a.host_steps else 0)  # pipelined, then two one by one
+    batches = gen_batches(torch, dev, B, a.warmup + a.steps + n_host, known, pool, g, 1_800_000_000)
     d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
     d_outs = [torch.empty((B, 1040), dtype=torch.uint8, device=dev) for _ in range(a.steps)]
     nreq = B - a.expiry  # requests per batch (the expiry deletes take the last X slots)
@@ -329,6 +332,29 @@ def main():
               "messages_before": msgs_before, "messages_after": st["messages"],
               "conserved": expired == 0 if not a.expiry else expired >= 0,
               "expired": expired}
+
+    host_path = None
+    if a.host_steps:
+        # the host API on batches in pageable host memory: gvs_process_batches
+        # (pinned staging, copies on their own stream, double-buffered) and,
+        # for comparison, gvs_process_batch one batch at a time
+        hb = [batches[a.warmup + a.steps + i][:nreq].cpu().numpy().view(abi.REQUEST_DTYPE).reshape(-1)
+              for i in range(n_host)]
+        gdist.barrier(ri)
+        t0 = time.perf_counter()
+        store.process_batches(hb[:a.host_steps])
+        t_pipe = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
+        gdist.barrier(ri)
+        t0 = time.perf_counter()
+        for x in hb[a.host_steps:]:
+            store.process_batch(x)
+        t_seq = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
+        host_path = {"value": world * nreq * a.host_steps / t_pipe, "unit": "req/s",
+                     "batches": a.host_steps, "ms_per_batch": t_pipe / a.host_steps * 1e3,
+                     "api": "gvs_process_batches (double-buffered, pinned staging)",
+                     "one_by_one_req_s": world * nreq * 2 / t_seq,
+                     "one_by_one_ms_per_batch": t_seq / 2 * 1e3,
+                     "note": "requests and responses in pageable host memory, PCIe and host copies included"}
 
     if rank == 0:
         total = world * nreq * a.steps
@@ -405,6 +431,7 @@ def main():
                                "frac": batch_gbs / HBM_PEAK_GBS,
                                "formula": "2*N*1024 + 4*R*1024 + B*(1088 + 1088), per ms_per_step"},
             "cpu_baseline": cpu,
+            "host_path": host_path,
             "checks": checks,
             "stage_ms": stage_ms,
             "store": {"messages": st["messages"], "mailboxes": st["mailboxes"],

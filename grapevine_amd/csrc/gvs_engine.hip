@@ -18,6 +18,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gvstore.h"
@@ -161,6 +162,19 @@ struct Router {
 
 }  // namespace
 
+// Double-buffered host path (gvs_process_batches): pinned host staging, two
+// device staging pairs, a copy stream and per-slot events.
+struct HostPipe {
+  bool ready = false;
+  uint4* din[2] = {};
+  uint4* dout[2] = {};
+  uint8_t* hin[2] = {};
+  uint8_t* hout[2] = {};
+  uint32_t* herr = nullptr;  // pinned: the agreed error word of the batch in each slot
+  hipStream_t copy = nullptr;
+  hipEvent_t h2d[2] = {}, done[2] = {}, d2h[2] = {};
+};
+
 struct gvs_handle {
   gvs_config cfg{};
   Mode mode = kSingle;
@@ -185,6 +199,7 @@ struct gvs_handle {
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
+  HostPipe pipe;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -1015,10 +1030,12 @@ static int agree_errors(gvs_handle* h) {
 // Enqueue one batch: n requests in the caller layout at d_in, responses in the
 // caller layout to d_out (kLocal: n <= S*Bsub, source k = requests
 // [k*Bsub, (k+1)*Bsub)).
-static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out) {
+static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out,
+                     bool reset = true) {
   h->n_marks = 0;
   mark(h, "start");
-  if (int r = reset_errors(h)) return r;
+  if (reset)
+    if (int r = reset_errors(h)) return r;
   if (h->mode == kSingle) {
     Engine& e = h->eng[0];
     if (int r = phase_a2(h, e, d_in, kAbiU4, n)) return r;
@@ -1055,16 +1072,9 @@ static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out)
   return GVS_OK;
 }
 
-static int finish(gvs_handle* h) {
-  if (h->mode == kRccl) {
-    if (int r = agree_errors(h)) return r;  // late flags (M2) too: same verdict on every rank
-  } else if (h->mode == kLocal) {
-    if (int r = agree_errors(h)) return r;
-  }
-  uint32_t e = 0;
-  GVS_HIP(h, hipMemcpyAsync(&e, &h->eng[0].scal->error, sizeof e, hipMemcpyDeviceToHost,
-                            h->stream));
-  GVS_HIP(h, hipStreamSynchronize(h->stream));
+// The status of a batch from its (agreed) error word; records the handle's
+// state (poisoned, message).  0: applied.
+static int decode_error(gvs_handle* h, uint32_t e) {
   if (e & 8u) {
     h->poisoned = true;
     h->err = "integrity failure: a stored row does not match its tag (authenticated storage)";
@@ -1092,12 +1102,47 @@ static int finish(gvs_handle* h) {
     h->err = "internal error flag " + std::to_string(e);
     return GVS_ERR_INTERNAL;
   }
+  return GVS_OK;
+}
+
+// host-side state an applied batch advances
+struct HostState {
+  uint32_t epoch[kShardsMax], par[kShardsMax], stamp_prev[kShardsMax];
+};
+static HostState save_state(const gvs_handle* h) {
+  HostState st{};
+  for (size_t k = 0; k < h->eng.size(); ++k) {
+    st.epoch[k] = h->eng[k].epoch;
+    st.par[k] = h->eng[k].par;
+    st.stamp_prev[k] = h->eng[k].stamp_prev;
+  }
+  return st;
+}
+static void restore_state(gvs_handle* h, const HostState& st) {
+  for (size_t k = 0; k < h->eng.size(); ++k) {
+    h->eng[k].epoch = st.epoch[k];
+    h->eng[k].par = st.par[k];
+    h->eng[k].stamp_prev = st.stamp_prev[k];
+  }
+}
+static void advance(gvs_handle* h) {
   for (auto& en : h->eng) {
     en.epoch += 1;  // every row was rewritten at epoch + 1
     // this batch's slots now hold the pending final states
     en.par ^= 1u;
     en.stamp_prev = en.stamp_run;
   }
+}
+
+static int finish(gvs_handle* h) {
+  if (h->mode != kSingle)
+    if (int r = agree_errors(h)) return r;  // late flags (M2) too: same verdict on every shard
+  uint32_t e = 0;
+  GVS_HIP(h, hipMemcpyAsync(&e, &h->eng[0].scal->error, sizeof e, hipMemcpyDeviceToHost,
+                            h->stream));
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  if (int r = decode_error(h, e)) return r;
+  advance(h);
   return GVS_OK;
 }
 
@@ -1350,6 +1395,16 @@ int gvs_destroy(gvs_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->comm) (void)ncclCommDestroy(h->comm);
+  HostPipe& hp = h->pipe;
+  if (hp.copy) (void)hipStreamSynchronize(hp.copy);
+  for (int b = 0; b < 2; ++b) {
+    if (hp.hin[b]) (void)hipHostFree(hp.hin[b]);
+    if (hp.hout[b]) (void)hipHostFree(hp.hout[b]);
+    for (hipEvent_t ev : {hp.h2d[b], hp.done[b], hp.d2h[b]})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  if (hp.herr) (void)hipHostFree(hp.herr);
+  if (hp.copy) (void)hipStreamDestroy(hp.copy);
   for (void* p : h->allocs) (void)hipFree(p);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1390,6 +1445,121 @@ int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_re
     GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * sizeof(gvs_response),
                               hipMemcpyDeviceToHost, h->stream));
   return finish(h);
+}
+
+// memcpy over up to 8 host threads (pinned staging of 64K-request batches:
+// one thread moves ~10 GB/s, too slow to hide behind a ~7 ms batch)
+static void par_memcpy(void* dst, const void* src, size_t bytes) {
+  const size_t kMin = 4u << 20;
+  unsigned nt = std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
+  if (bytes < 2 * kMin || nt < 2) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  nt = (unsigned)std::min<size_t>(nt, bytes / kMin);
+  const size_t chunk = (bytes + nt - 1) / nt;
+  std::vector<std::thread> th;
+  for (unsigned k = 1; k < nt; ++k) {
+    const size_t o = k * chunk, len = std::min(chunk, bytes - std::min(bytes, o));
+    if (len)
+      th.emplace_back([=] { std::memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, len); });
+  }
+  std::memcpy(dst, src, std::min(chunk, bytes));
+  for (auto& t : th) t.join();
+}
+
+static int pipe_init(gvs_handle* h) {
+  HostPipe& p = h->pipe;
+  if (p.ready) return GVS_OK;
+  const uint64_t cap = (uint64_t)h->Bsub * (h->mode == kLocal ? h->S : 1u);
+  for (int b = 0; b < 2; ++b) {
+    if (int rc = dalloc_t(h, &p.din[b], cap * kAbiU4)) return rc;
+    if (int rc = dalloc_t(h, &p.dout[b], cap * kAbiU4)) return rc;
+    GVS_HIP(h, hipHostMalloc((void**)&p.hin[b], cap * sizeof(gvs_request), hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.hout[b], cap * sizeof(gvs_response), hipHostMallocDefault));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.h2d[b], hipEventDisableTiming));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.done[b], hipEventDisableTiming));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.d2h[b], hipEventDisableTiming));
+  }
+  GVS_HIP(h, hipHostMalloc((void**)&p.herr, 2 * sizeof(uint32_t), hipHostMallocDefault));
+  GVS_HIP(h, hipStreamCreateWithFlags(&p.copy, hipStreamNonBlocking));
+  p.ready = true;
+  return GVS_OK;
+}
+
+// k batches from host memory, double-buffered: batch t+1's requests are
+// staged and copied in, and batch t-1's responses copied out, while batch t
+// runs.  Batches apply in order; the error word is not reset between them,
+// so after a failed batch the following ones enqueued behind it do nothing,
+// and the host state is rolled back to the failed batch.
+int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* counts,
+                        uint32_t k, gvs_response* out, uint32_t* applied) {
+  if (applied) *applied = 0;
+  if (!h || h->kind != 0 || (k && (!counts || !reqs || !out))) return GVS_ERR_INVALID_ARG;
+  for (uint32_t t = 0; t < k; ++t)
+    if (counts[t] > max_submit(h)) return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (k == 0) return GVS_OK;
+  GVS_HIP(h, hipSetDevice(h->device));
+  if (int r = pipe_init(h)) return r;
+  HostPipe& p = h->pipe;
+  hipStream_t s = h->stream;
+  if (int r = reset_errors(h)) return r;
+  HostState snap[2];
+  uint64_t off[2] = {0, 0};
+  uint64_t next_off = 0;
+  uint32_t enq = 0;  // batches enqueued
+  int stop = GVS_OK;
+  for (uint32_t t = 0;; ++t) {
+    bool more = t < k && stop == GVS_OK;
+    if (more)
+      if (int r = check_epoch(h)) {
+        stop = r;
+        more = false;
+      }
+    if (more) {  // enqueue batch t in slot b
+      const uint32_t b = t & 1u, n = counts[t];
+      if (t >= 2) GVS_HIP(h, hipEventSynchronize(p.h2d[b]));  // hin[b] free again
+      par_memcpy(p.hin[b], reqs + next_off, (size_t)n * sizeof(gvs_request));
+      if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(p.copy, p.done[b], 0));  // din[b] consumed
+      if (n)
+        GVS_HIP(h, hipMemcpyAsync(p.din[b], p.hin[b], (size_t)n * sizeof(gvs_request),
+                                  hipMemcpyHostToDevice, p.copy));
+      GVS_HIP(h, hipEventRecord(p.h2d[b], p.copy));
+      GVS_HIP(h, hipStreamWaitEvent(s, p.h2d[b], 0));
+      if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(s, p.d2h[b], 0));  // dout[b] copied out
+      snap[b] = save_state(h);
+      if (int r = run_batch(h, p.din[b], n, p.dout[b], false)) return r;
+      if (h->mode != kSingle)
+        if (int r = agree_errors(h)) return r;
+      GVS_HIP(h, hipMemcpyAsync(&p.herr[b], &h->eng[0].scal->error, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, s));
+      GVS_HIP(h, hipEventRecord(p.done[b], s));
+      GVS_HIP(h, hipStreamWaitEvent(p.copy, p.done[b], 0));
+      if (n)
+        GVS_HIP(h, hipMemcpyAsync(p.hout[b], p.dout[b], (size_t)n * sizeof(gvs_response),
+                                  hipMemcpyDeviceToHost, p.copy));
+      GVS_HIP(h, hipEventRecord(p.d2h[b], p.copy));
+      advance(h);  // as if applied; rolled back below if it was not
+      off[b] = next_off;
+      next_off += n;
+      enq = t + 1;
+    }
+    if (t >= 1 && t - 1 < enq) {  // collect batch t-1
+      const uint32_t pb = (t - 1) & 1u;
+      GVS_HIP(h, hipEventSynchronize(p.d2h[pb]));
+      if (const uint32_t e = p.herr[pb]) {
+        restore_state(h, snap[pb]);
+        GVS_HIP(h, hipStreamSynchronize(s));  // batch t, if enqueued, did nothing
+        GVS_HIP(h, hipStreamSynchronize(p.copy));
+        return decode_error(h, e);
+      }
+      par_memcpy(out + off[pb], p.hout[pb], (size_t)counts[t - 1] * sizeof(gvs_response));
+      if (applied) *applied = t;
+    }
+    if (!more && t >= enq) break;
+  }
+  return stop;
 }
 
 int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void* d_out) {

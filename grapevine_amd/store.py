@@ -23,7 +23,7 @@ _LIB_PATH = os.path.join(_HERE, "libgvstore.so")
 _TEST_LIB_PATH = os.path.join(_HERE, "libgvstore_test.so")
 
 EXPORTED = (
-    "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch",
+    "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch", "gvs_process_batches",
     "gvs_process_batch_device", "gvs_access", "gvs_get_stats",
     "gvs_synchronize", "gvs_set_option", "gvs_get_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
@@ -65,6 +65,7 @@ def load_library(path=None):
     lib.gvs_destroy.argtypes = [vp]
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
+    lib.gvs_process_batches.argtypes = [vp, vp, vp, u32, vp, ctypes.POINTER(u32)]
     lib.gvs_access.argtypes = [vp, vp, vp]
     lib.gvs_get_stats.argtypes = [vp, ctypes.POINTER(abi.GvsStats)]
     lib.gvs_synchronize.argtypes = [vp]
@@ -181,6 +182,23 @@ class ObliviousStore:
         out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
         self._check(self.lib.gvs_process_batch(self.h, reqs.ctypes.data, len(reqs), out.ctypes.data))
         return out
+
+    def process_batches(self, batches):
+        """Several batches from host memory, double-buffered (gvs_process_batches).
+        -> list of response arrays.  On a failing batch raises GvsError with
+        `.applied` = the number of batches applied before it."""
+        counts = np.array([len(b) for b in batches], dtype=np.uint32)
+        reqs = np.ascontiguousarray(np.concatenate(batches) if len(batches) else
+                                    np.zeros(0, dtype=abi.REQUEST_DTYPE), dtype=abi.REQUEST_DTYPE)
+        out = np.zeros(len(reqs), dtype=abi.RESPONSE_DTYPE)
+        applied = ctypes.c_uint32(0)
+        rc = self.lib.gvs_process_batches(self.h, reqs.ctypes.data, counts.ctypes.data, len(counts),
+                                          out.ctypes.data, ctypes.byref(applied))
+        if rc != 0:
+            err = GvsError(rc, (self.lib.gvs_last_error(self.h) or b"").decode())
+            err.applied = applied.value
+            raise err
+        return np.split(out, np.cumsum(counts)[:-1]) if len(counts) else []
 
     def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
         self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))

@@ -201,6 +201,17 @@ int gvs_create_sharded(const gvs_config *cfg, const uint8_t comm_id[GVS_COMM_ID_
 int gvs_process_batch(gvs_handle *h, const gvs_request *reqs, uint32_t n,
                       gvs_response *out);
 
+/* k batches from host memory in one call, double-buffered: the requests of
+ * batch t+1 are staged (pinned) and copied in, and the responses of batch t-1
+ * copied out, while batch t runs, so PCIe and host copies hide behind the
+ * table passes.  Batch t has counts[t] requests; the requests of all batches
+ * are consecutive in `reqs` and their responses likewise in `out`.  Batches
+ * apply in order, each with the semantics of gvs_process_batch; at the first
+ * batch that fails, the call returns its error, that batch and the later
+ * ones are not applied, and *applied (optional) holds the number applied. */
+int gvs_process_batches(gvs_handle *h, const gvs_request *reqs, const uint32_t *counts,
+                        uint32_t k, gvs_response *out, uint32_t *applied);
+
 /* Same, with device-resident buffers (n * sizeof(gvs_request) and
  * n * sizeof(gvs_response) bytes on the handle's device).  Used by the
  * benchmark so that the timed region excludes PCIe. */

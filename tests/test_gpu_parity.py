@@ -109,3 +109,51 @@ def test_golden_fixtures(name):
         st = store.stats()
         assert (st["messages"], st["mailboxes"]) == (msgs, mboxes), (name, k)
     store.close()
+
+
+def test_host_pipeline_matches_oracle():
+    """gvs_process_batches: several host batches double-buffered (staging and
+    PCIe of batch t+1 / t-1 behind batch t) equal the same batches one by one."""
+    from parity import diff_tables
+    store, model = make_pair(4096, 16, 32, 1024)
+    model.seed(13)
+    p = ffi.gen_params(n_identities=300)
+    for sizes in ([1024, 1024, 1024, 1024, 1024], [1, 0, 700, 1024], [1024]):
+        batches = [model.gen_batch(n, p) for n in sizes]
+        want = [model.process_batch(b) for b in batches]
+        got = store.process_batches(batches)
+        for k, (g, w, b) in enumerate(zip(got, want, batches)):
+            d = diff_responses(g, w, b)
+            assert not d, f"{sizes} batch {k}: " + "\n".join(d)
+        st = store.stats()
+        assert (st["messages"], st["mailboxes"]) == (model.messages, model.mailboxes)
+    assert not diff_tables(store.dump_messages(), model.dump_messages())
+
+
+def test_host_pipeline_stops_at_failing_batch():
+    """A batch that overflows a router bucket stops the pipeline there: the
+    batches before it are applied, it and the later ones are not, and the
+    store goes on from that state."""
+    from grapevine_amd.store import GvsError
+    S = 4
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024,
+                          shard_count=S, route_capacity=320)
+    store, cl = ObliviousStore(cfg), ffi.Cluster(cfg)
+    cl.seed(14)
+    p = ffi.gen_params(n_identities=300)
+    hot = ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60, n_identities=300)
+    ok = [cl.gen_batch(S * 1024, p) for _ in range(2)]
+    want = [cl.process_batch(b) for b in ok]
+    bad = cl.gen_batch(S * 1024, hot)
+    assert cl.process_batch(bad) is None
+    later = cl.gen_batch(S * 1024, p)
+    with pytest.raises(GvsError) as ei:
+        store.process_batches(ok + [bad, later])
+    assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW and ei.value.applied == 2
+    assert store.stats()["messages"] == cl.messages
+    assert store.stats()["batches"] == 2 and store.stats()["epoch"] == 2
+    # `later` was not applied: it runs now, as the oracle's next batch
+    got = store.process_batches([later])
+    d = diff_responses(got[0], cl.process_batch(later), later)
+    assert not d, "\n".join(d)
+    assert store.dump_messages().tobytes() == cl.dump_messages().tobytes()
