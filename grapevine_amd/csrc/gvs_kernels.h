@@ -579,47 +579,35 @@ __global__ __launch_bounds__(1024) void k_alloc_b(AllocArgs a) {
   const Scal* sc = a.scal;
   const uint64_t count1 = sc->count1, ctr0 = sc->ctr;
 
-  ROp r = {};
-  r.kind = kind;
-  r.status = os.pre_status;
-  r.slot = kNone;
-  r.id[0] = os.id[0]; r.id[1] = os.id[1]; r.id[2] = os.id[2]; r.id[3] = os.id[3];
-  for (int k = 0; k < 8; ++k) r.x[k] = os.x[k];
-  uint32_t cls = 3;
+  // every case computed, the op's own selected (no branch over op kinds: a
+  // block of padding ops would skip the code, and instruction fetch shows in
+  // FETCH_SIZE)
   uint64_t L, R;
   id_encode(a.kc, cs == kNone ? 0u : cs, ctr0 + S_i, L, R);  // fixed work for every op
-  if (kind == KIND_CREATE && os.pre_status == kPending) {
-    if (count1 + S_i >= a.N) r.status = 7;  // TOO_MANY_MESSAGES (checked before 5/6)
-    else if (cs == kNone) r.status = m1.status;  // 5 or 6 from the mailbox pass
-    else {
-      r.slot = cs;
-      r.status = kPending;
-      r.id[0] = (uint32_t)L; r.id[1] = (uint32_t)(L >> 32);
-      r.id[2] = (uint32_t)R; r.id[3] = (uint32_t)(R >> 32);
-      cls = 1;
-    }
-  } else if (kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL) {
-    r.status = m1.status;
-    if (m1.status == kPending) {
-      r.slot = m1.slot;
-      r.id[0] = m1.id[0]; r.id[1] = m1.id[1]; r.id[2] = m1.id[2]; r.id[3] = m1.id[3];
-      cls = 0;
-    }
-  } else if (kind == KIND_READ || kind == KIND_UPDATE || kind == KIND_DELETE) {
-    r.slot = os.slot;
-    if (os.slot != kNone) cls = 2;
-  }
+  const bool c_cr = kind == KIND_CREATE && os.pre_status == kPending;
+  const bool cr_full = count1 + S_i >= a.N, cr_ok = !cr_full && cs != kNone;
+  const bool c_nx = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
+  const bool nx_ok = m1.status == kPending;
+  const bool c_id = kind == KIND_READ || kind == KIND_UPDATE || kind == KIND_DELETE;
+  ROp r = {};
+  r.kind = kind;
+  // CREATE: TOO_MANY_MESSAGES (7) checked before 5/6 from the mailbox pass
+  const uint32_t st_cr = selu32(cr_full, 7u, selu32(cs == kNone, m1.status, kPending));
+  r.status = selu32(c_cr, st_cr, selu32(c_nx, m1.status, os.pre_status));
+  r.slot = selu32(c_cr && cr_ok, cs, selu32(c_nx && nx_ok, m1.slot, selu32(c_id, os.slot, kNone)));
+  const uint32_t nid[4] = {(uint32_t)L, (uint32_t)(L >> 32), (uint32_t)R, (uint32_t)(R >> 32)};
+  for (int k = 0; k < 4; ++k)
+    r.id[k] = selu32(c_cr && cr_ok, nid[k], selu32(c_nx && nx_ok, m1.id[k], os.id[k]));
+  for (int k = 0; k < 8; ++k) r.x[k] = os.x[k];
+  const bool c_id_ok = c_id && os.slot != kNone;
+  const uint32_t cls = selu32(c_cr && cr_ok, 1u, selu32(c_nx && nx_ok, 0u, selu32(c_id_ok, 2u, 3u)));
   st_drop_rec(a.rop, i, r);  // read by the scans in sorted order
-  uint64_t rowp = kRNullRow;
-  uint32_t part = a.W;
-  if (cls < 3) {
-    const uint32_t sl = r.slot;
-    part = sl % a.W;
-    rowp = (uint64_t)part * a.S + sl / a.W;
-  } else {
-    cls = 0;
-  }
-  a.rkeys[i] = r_key(rowp, cls, i);
+  const bool real = cls < 3u;
+  const uint32_t sl = r.slot;
+  const uint64_t rowc = (uint64_t)(sl % a.W) * a.S + sl / a.W;  // computed for every op
+  const uint64_t rowp = real ? rowc : kRNullRow;
+  const uint32_t rcls = selu32(real, cls, 0u);
+  a.rkeys[i] = r_key(rowp, rcls, i);
 }
 
 constexpr uint32_t kXepMax = 8;  // expiry records per workgroup (one store instruction)

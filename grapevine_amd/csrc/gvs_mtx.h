@@ -170,7 +170,8 @@ __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uin
     if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
-    const int k = occ ? find_group_m(g, ng, hi, w1 >> 23) : -1;
+    const int kf = find_group_m(g, ng, hi, w1 >> 23);  // every row: no code skipped
+    const int k = occ ? kf : -1;
     atomicAdd(s_occ, occ ? 1u : 0u);
     // rows without a group write the sink entry g[kGroupMax]: the same code
     // runs whatever the batch holds (instruction fetch shows in FETCH_SIZE)
@@ -407,19 +408,15 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     // by-id delete: the position of its id in the mailbox (for the write pass)
     const uint64_t hit = __ballot(lane >= 2 && lane < 2 + len && eq4(pv, myid));
     const uint32_t pos = hit ? (uint32_t)__builtin_ctzll(hit) - 2u : 63u;
-    uint32_t status = kPending, slot = kNone, flags = 0, opos = 63u;
-    uint4 oid = make_uint4(0, 0, 0, 0);
-    if (!null && cls == 0u) {
-      status = found ? kPending : 2u;
-      slot = found ? dec : kNone;
-      flags = (found && mpos_sub(mp.x)) ? CF_POP : 0u;
-      oid = sel4(found, idv, oid);
-    } else if (!null && cls == 1u) {
-      status = cok ? kPending : ((exists1 || admitted) ? 5u : 6u);
-      flags = cok ? CF_MBOX_OK : 0u;
-    } else if (!null) {
-      opos = pos;
-    }
+    // selects, no branch over the op class (null ops sort last: a wave of
+    // them would skip the code, and instruction fetch shows in FETCH_SIZE)
+    const bool c0 = !null && cls == 0u, c1 = !null && cls == 1u, c2 = !null && cls > 1u;
+    const uint32_t st1 = selu32(cok, kPending, selu32(exists1 || admitted, 5u, 6u));
+    const uint32_t status = selu32(c0, selu32(found, kPending, 2u), selu32(c1, st1, kPending));
+    const uint32_t slot = selu32(c0 && found, dec, kNone);
+    const uint32_t flags = selu32(c0 && found && mpos_sub(mp.x), CF_POP, selu32(c1 && cok, CF_MBOX_OK, 0u));
+    const uint32_t opos = selu32(c2, pos, 63u);
+    const uint4 oid = sel4(c0 && found, idv, make_uint4(0, 0, 0, 0));
     if (lane < 8)
       st_drop(a.m1out, (uint64_t)seq * 8 + lane,
               sel4(lane == 0, make_uint4(status, slot, flags, opos), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0))));
@@ -707,10 +704,12 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     }
   }
   __syncthreads();
-  // result slots no row took: every slot of M2TX is read once
-  for (uint32_t k = wave; k < a.cm; k += 4) {
-    if (s_ld[k]) continue;
-    uint4 x = ld_row<true>(&res[(uint64_t)k * kVLineU4 + 8 + lane]);
+  // result slots no row took: every slot of M2TX is read once; the wave that
+  // reaches k = cm reads the dry line, so the code runs in every workgroup
+  for (uint32_t k = wave; k <= a.cm; k += 4) {
+    const bool dry_run = k == a.cm;
+    if (!dry_run && s_ld[k]) continue;
+    uint4 x = ld_row<true>(dry_run ? &dry[lane] : &res[(uint64_t)k * kVLineU4 + 8 + lane]);
     keep4(x);
   }
   // every workgroup adds, zero included: a fixed set of atomics

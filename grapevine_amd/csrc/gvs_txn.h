@@ -675,38 +675,39 @@ struct Rr1Op {
     const bool nd_ok = in.nd_valid && r0_exists && eq4(in.nd, in.r0[0]);
     const bool is_next = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
     const bool is_create = kind == KIND_CREATE;
-    uint32_t status = rstatus, setk = kSetNone, flags = 0;
+    // Every case is computed and the op's own one selected (no branch over op
+    // kinds: a wave of padding ops would skip the code, and instruction fetch
+    // shows in FETCH_SIZE; routed shard pipelines end in a data-dependent
+    // number of padding ops).
+    const bool c_next = !null && is_next, c_cr = !null && !is_next && is_create;
+    const bool c_byid = !null && !is_next && !is_create;
+    // next: M1 resolved it to this row, which must hold that id
+    const uint32_t st_next = (r0_exists && eq4(in.r0[0], rid)) ? 1u : 8u;
+    const uint32_t sk_next = (kind == KIND_NEXT_DEL && st_next == 1u) ? kSetZero : kSetNone;
+    // create: the allocator hands out free rows, empty after the pops
+    const uint32_t st_cr = (r0_exists && !nd_ok) ? 8u : 1u;
+    const uint32_t sk_cr = st_cr == 1u ? kSetRec : kSetNone;
+    // by-id READ / UPDATE / DELETE: the row as the creates and pops of this
+    // batch left it (class order: pops, creates, then these)
+    const bool cr_ok = in.cr_valid && !(r0_exists && !nd_ok);
+    uint4 idb[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) idb[i] = sel4(cr_ok, in.cr[i], sel4(nd_ok, make_uint4(0, 0, 0, 0), in.r0[i]));
+    const bool exists1 = nz4(idb[0]);
+    const bool cand = exists1 && eq4(qid, idb[0]) &&
+                      ((eq4(q1, idb[1]) && eq4(q2, idb[2])) || (eq4(q1, idb[3]) && eq4(q2, idb[4])));
+    const bool rcpt_ok = eq4(q3, idb[3]) && eq4(q4, idb[4]);
+    const bool expiry = seq >= a.xbase;
+    const bool apply = cand && rcpt_ok && !expiry;
+    const uint32_t sk_b = selu32(apply && kind == KIND_UPDATE, kSetRec,
+                                 selu32(apply && kind == KIND_DELETE, kFreeze, kSetNone));
+    const uint32_t fl_b = kRsClass2 | (cand ? kRsCand : 0u) | (rcpt_ok ? kRsRcptOk : 0u) | (expiry ? kRsExpiry : 0u);
+    const uint32_t status = selu32(c_next, st_next, selu32(c_cr, st_cr, rstatus));
+    const uint32_t setk = selu32(c_next, sk_next, selu32(c_cr, sk_cr, selu32(c_byid, sk_b, kSetNone)));
+    uint32_t flags = selu32(c_byid, fl_b, 0u);
     uint4 ident[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) ident[i] = in.r0[i];
-    if (!null && is_next) {
-      // M1 resolved it to this row: the row must hold that id
-      status = (r0_exists && eq4(in.r0[0], rid)) ? 1u : 8u;
-      setk = (kind == KIND_NEXT_DEL && status == 1u) ? kSetZero : kSetNone;
-    } else if (!null && is_create) {
-      // the allocator hands out free rows: the row is empty after the pops
-      status = (r0_exists && !nd_ok) ? 8u : 1u;
-      setk = status == 1u ? kSetRec : kSetNone;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) ident[i] = in.cr[i];
-    } else if (!null) {
-      // by-id READ / UPDATE / DELETE: the row as the creates and pops of this
-      // batch left it (class order: pops, creates, then these)
-      const bool cr_ok = in.cr_valid && !(r0_exists && !nd_ok);
-#pragma unroll
-      for (int i = 0; i < 5; ++i)
-        ident[i] = sel4(cr_ok, in.cr[i], sel4(nd_ok, make_uint4(0, 0, 0, 0), in.r0[i]));
-      const bool exists1 = nz4(ident[0]);
-      const bool cand = exists1 && eq4(qid, ident[0]) &&
-                        ((eq4(q1, ident[1]) && eq4(q2, ident[2])) || (eq4(q1, ident[3]) && eq4(q2, ident[4])));
-      const bool rcpt_ok = eq4(q3, ident[3]) && eq4(q4, ident[4]);
-      const bool expiry = seq >= a.xbase;
-      flags |= kRsClass2 | (cand ? kRsCand : 0u) | (rcpt_ok ? kRsRcptOk : 0u) | (expiry ? kRsExpiry : 0u);
-      if (cand && rcpt_ok && !expiry) {
-        if (kind == KIND_UPDATE) setk = kSetRec;
-        if (kind == KIND_DELETE) setk = kFreeze;
-      }
-    }
+    for (int i = 0; i < 5; ++i) ident[i] = sel4(c_cr, in.cr[i], sel4(c_byid, idb[i], in.r0[i]));
     flags |= (head ? kRsHead : 0u) | (last ? kRsLast : 0u) | (null ? kRsNull : 0u) | (setk << 8);
     uint4 rec[8];
     rec[0] = make_uint4(seq, flags, status, kind);
@@ -1042,12 +1043,8 @@ struct Rr2Op {
 __device__ inline uint4 fail_rec(uint4 imgv, uint32_t status) {
   const uint32_t lane = lane_id();
   const uint4 ts = shfl4(imgv, 5);
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (lane == 5 && status != 0u) {
-    r.x = ts.x;
-    r.y = ts.y;
-  }
-  return r;
+  const bool keep = lane == 5 && status != 0u;  // selects: no code skipped for hard errors
+  return make_uint4(selu32(keep, ts.x, 0u), selu32(keep, ts.y, 0u), 0u, 0u);
 }
 
 // k_rr2_c: each wave walks its 16 ops in order from its carry: statuses of
@@ -1136,16 +1133,15 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
     // the row state before this op
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 1u, 0u), cf);
     const uint4 pv = sel4(head, sv, cv);
-    uint32_t status = h.status;
-    if (h.flags & kRsClass2) {
-      // by-id op: the row must still hold the record it named (no DELETE
-      // before it in this batch); an expiry delete also needs the record's
-      // current time below the cutoff
-      const uint64_t ts = ((uint64_t)__shfl(pv.y, 5) << 32) | __shfl(pv.x, 5);
-      const bool fresh = (h.flags & kRsExpiry) && !(ts < a.cutoff);
-      const bool found = (h.flags & kRsCand) && !pf.y && !fresh;
-      status = !found ? 2u : ((h.kind != KIND_READ && !(h.flags & kRsRcptOk)) ? 4u : 1u);
-    }
+    // by-id op: the row must still hold the record it named (no DELETE before
+    // it in this batch); an expiry delete also needs the record's current
+    // time below the cutoff.  Computed for every op and selected (padding ops
+    // sort last: a branch would leave their waves' code unfetched).
+    const uint64_t ts = ((uint64_t)__shfl(pv.y, 5) << 32) | __shfl(pv.x, 5);
+    const bool fresh = (h.flags & kRsExpiry) && !(ts < a.cutoff);
+    const bool found = (h.flags & kRsCand) && !pf.y && !fresh;
+    const uint32_t st2 = selu32(!found, 2u, selu32(h.kind != KIND_READ && !(h.flags & kRsRcptOk), 4u, 1u));
+    const uint32_t status = selu32((h.flags & kRsClass2) != 0u, st2, h.status);
     const bool ok = status == 1u;
     const uint4 own = Rr2Op::own_value(h, sv, iv, idv);
     const uint4 resp = sel4(!ok, fail_rec(iv, status), sel4(rs_setkind(h.flags) == kSetRec, own, pv));

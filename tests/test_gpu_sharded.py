@@ -105,3 +105,28 @@ def test_local_shards_pipeline_not_a_power_of_two():
     cl.seed(51)
     run_stream(store, cl, ffi.gen_params(n_identities=3000), batches=4, n=S * B)
     run_stream(store, cl, ffi.gen_params(n_identities=3000), batches=1, n=S * B - 777)
+
+
+def test_rccl_single_rank_with_expiry():
+    """gvs_create_sharded with one rank and expiry: the X expiry slots sit after
+    the routed ones (shard_batch(C + X)), never over a client's request."""
+    import os
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    X, B = 128, 1024
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=B,
+                          shard_count=1, shard_index=0, expiry_per_batch=X)
+    store = ObliviousStore(cfg, comm_id=comm_unique_id())
+    cl = ffi.Cluster(cfg)
+    st = store.stats()
+    assert st["shard_batch"] == ffi.shard_batch(cl.capacity + X) >= B + X
+    cl.seed(52)
+    p = ffi.gen_params(create=40, read=20, update=20, delete=20, n_identities=200)
+    for b in range(8):
+        cutoff = 1_700_000_000 + max(0, cl.ops - 1500) if b >= 2 else 0
+        cl.set_expiry_cutoff(cutoff)
+        store.set_expiry_cutoff(cutoff)
+        reqs = cl.gen_batch(B, p)  # a full batch: expiry takes no client slot
+        d = diff_responses(store.process_batch(reqs), cl.process_batch(reqs), reqs)
+        assert not d, f"batch {b}: " + "\n".join(d)
+        assert store.stats()["messages"] == cl.messages
+    store.close()

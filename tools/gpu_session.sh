@@ -38,6 +38,8 @@ case "$2" in
     PMC_ARGS=--auth PMC_KERN=k_m2x,k_rpass2 PMC_CTRS="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum" \
       step pmc_mix 400 bash tools/gpu_pmc_mix.sh
     step oblivious_x 1000 $PT tests/test_oblivious.py -k "auth or routed" ;;
+  probe) step hbm_probe 300 tools/hbm_probe 16 ;;
+  tob) tests && step oblivious_all 1000 $PT tests/test_oblivious.py && step hbm_probe 300 tools/hbm_probe 16 && bench ;;
   oblall) step oblivious_all 1150 $PT tests/test_oblivious.py ;;
   all) tests && bench && timing ;;
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines

@@ -80,6 +80,23 @@ __global__ __launch_bounds__(256, MINW) void k_pipe(v4u* a, uint32_t rows) {
   }
 }
 
+// grid-stride with U independent 16-B accesses in flight per thread: thread t
+// of block b handles elements (b * U + u) * 256 + t, then jumps the grid
+template <int U, bool NT, bool COPY>
+__global__ __launch_bounds__(256) void k_wide(const v4u* s, v4u* d, size_t n) {
+  const size_t step = (size_t)gridDim.x * U * 256;
+  for (size_t base = (size_t)blockIdx.x * U * 256 + threadIdx.x; base < n; base += step) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = base + u * 256 < n ? ld<NT>(s + base + u * 256) : v4u{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!COPY) v[u].x ^= 1u;
+      if (base + u * 256 < n) st<NT>(d + base + u * 256, v[u]);
+    }
+  }
+}
+
 // out-of-place copy, grid-stride
 template <bool NT>
 __global__ __launch_bounds__(256) void k_copy(const v4u* s, v4u* d, size_t n) {
@@ -152,6 +169,19 @@ int main(int argc, char** argv) {
   }
   // copy between two halves
   const size_t h = n / 2;
+  for (int g : {2048, 4096, 8192}) {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "wide copy U4 nt grid=%d", g);
+    timeit(nm, 2.0 * h * 16, [&] { hipLaunchKernelGGL((k_wide<4, true, true>), dim3(g), dim3(256), 0, 0, a, a + h, h); });
+    std::snprintf(nm, sizeof nm, "wide copy U8 plain grid=%d", g);
+    timeit(nm, 2.0 * h * 16, [&] { hipLaunchKernelGGL((k_wide<8, false, true>), dim3(g), dim3(256), 0, 0, a, a + h, h); });
+    std::snprintf(nm, sizeof nm, "wide copy U8 nt grid=%d", g);
+    timeit(nm, 2.0 * h * 16, [&] { hipLaunchKernelGGL((k_wide<8, true, true>), dim3(g), dim3(256), 0, 0, a, a + h, h); });
+    std::snprintf(nm, sizeof nm, "wide inplace U8 nt grid=%d", g);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_wide<8, true, false>), dim3(g), dim3(256), 0, 0, a, a, n); });
+    std::snprintf(nm, sizeof nm, "wide inplace U8 plain grid=%d", g);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_wide<8, false, false>), dim3(g), dim3(256), 0, 0, a, a, n); });
+  }
   timeit("copy nt half->half grid=4096", 2.0 * h * 16, [&] {
     hipLaunchKernelGGL(k_copy<true>, dim3(4096), dim3(256), 0, 0, a, a + h, h);
   });
