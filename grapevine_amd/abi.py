@@ -91,6 +91,10 @@ class GvsStats(ctypes.Structure):
         "free_ring_tail", "msg_partitions", "msg_partition_slots", "shards", "route_capacity",
         "shard_batch", "epoch")]
 
+# wire codec (gvs_process_wire_batch, include/gvstore.h)
+WIRE_REQUEST_BYTES, WIRE_RESPONSE_BYTES, WIRE_SLOT_MAX = 1099, 1042, 2048
+WIRE_OK, WIRE_DECODE_ERROR, WIRE_BAD_FIELD = 0, 1, 2
+
 COMM_ID_BYTES = 128
 FLAG_AUTH_STORAGE = 1  # GVS_FLAG_AUTH_STORAGE: AES-CTR + BLAKE2b sealed tables
 ERR_INTEGRITY = -7     # GVS_ERR_INTEGRITY

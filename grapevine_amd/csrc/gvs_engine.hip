@@ -28,6 +28,7 @@
 #include "gvs_mtx.h"
 #include "gvs_kv.h"
 #include "gvs_omap.h"
+#include "gvs_wire.h"
 
 using namespace gvs;
 
@@ -175,6 +176,18 @@ struct HostPipe {
   hipEvent_t h2d[2] = {}, done[2] = {}, d2h[2] = {};
 };
 
+// Device staging of the host wire path (gvs_process_wire_batch), allocated on
+// first use for max_submit messages of kWireSlotMax bytes each way.
+struct WireStage {
+  uint8_t* in = nullptr;
+  uint8_t* out = nullptr;
+  uint32_t* in_lens = nullptr;
+  uint32_t* out_lens = nullptr;
+  uint64_t* times = nullptr;
+  uint4* sigs = nullptr;
+  uint32_t* status = nullptr;
+};
+
 struct gvs_handle {
   gvs_config cfg{};
   Mode mode = kSingle;
@@ -200,6 +213,7 @@ struct gvs_handle {
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   HostPipe pipe;
+  WireStage wire;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -1568,6 +1582,123 @@ int gvs_process_batch_device(gvs_handle* h, const void* d_reqs, uint32_t n, void
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   if (int r = run_batch(h, (const uint4*)d_reqs, n, (uint4*)d_out)) return r;
+  return finish(h);
+}
+
+// ------------------------------------------------------------ wire codec
+
+static bool wire_strides_ok(uint32_t in_stride, uint32_t out_stride) {
+  return in_stride >= 1 && in_stride <= kWireSlotMax && out_stride >= kWireResp &&
+         out_stride <= kWireSlotMax;
+}
+
+static void enqueue_wire_decode(gvs_handle* h, const void* d_wire, uint32_t stride,
+                                const uint32_t* d_lens, uint32_t n, const uint64_t* d_times,
+                                void* d_reqs, void* d_sigs, uint32_t* d_status) {
+  if (!n) return;
+  WireDecArgs a{(const uint8_t*)d_wire, stride, n, d_lens, d_times, (uint4*)d_reqs,
+                (uint4*)d_sigs, d_status};
+  hipLaunchKernelGGL(k_wire_decode, dim3((n + 3) / 4), dim3(256), 0, h->stream, a);
+}
+
+static void enqueue_wire_encode(gvs_handle* h, const void* d_resps, uint32_t n, void* d_wire,
+                                uint32_t stride, uint32_t* d_lens) {
+  if (!n) return;
+  WireEncArgs a{(const uint4*)d_resps, n, stride, (uint8_t*)d_wire, d_lens};
+  hipLaunchKernelGGL(k_wire_encode, dim3((n + 3) / 4), dim3(256), 0, h->stream, a);
+}
+
+int gvs_wire_decode_device(gvs_handle* h, const void* d_wire, uint32_t stride,
+                           const uint32_t* d_lens, uint32_t n, const uint64_t* d_times,
+                           void* d_reqs, void* d_sigs, uint32_t* d_status) {
+  if (!h || stride < 1 || stride > kWireSlotMax ||
+      (n && (!d_wire || !d_lens || !d_times || !d_reqs)))
+    return GVS_ERR_INVALID_ARG;
+  GVS_HIP(h, hipSetDevice(h->device));
+  enqueue_wire_decode(h, d_wire, stride, d_lens, n, d_times, d_reqs, d_sigs, d_status);
+  GVS_HIP(h, hipGetLastError());
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return GVS_OK;
+}
+
+int gvs_wire_encode_device(gvs_handle* h, const void* d_resps, uint32_t n, void* d_wire,
+                           uint32_t stride, uint32_t* d_lens) {
+  if (!h || stride < kWireResp || stride > kWireSlotMax || (n && (!d_resps || !d_wire || !d_lens)))
+    return GVS_ERR_INVALID_ARG;
+  GVS_HIP(h, hipSetDevice(h->device));
+  enqueue_wire_encode(h, d_resps, n, d_wire, stride, d_lens);
+  GVS_HIP(h, hipGetLastError());
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return GVS_OK;
+}
+
+// decode -> the batch -> encode, all on the engine stream; the request and
+// response slabs live in the handle's host-API staging.
+static int wire_batch(gvs_handle* h, const void* d_in, uint32_t in_stride, const uint32_t* d_in_lens,
+                      uint32_t n, const uint64_t* d_times, void* d_out, uint32_t out_stride,
+                      uint32_t* d_out_lens, void* d_sigs, uint32_t* d_status) {
+  enqueue_wire_decode(h, d_in, in_stride, d_in_lens, n, d_times, h->in_stage, d_sigs, d_status);
+  if (int r = run_batch(h, h->in_stage, n, h->out_stage)) return r;
+  enqueue_wire_encode(h, h->out_stage, n, d_out, out_stride, d_out_lens);
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
+}
+
+int gvs_process_wire_batch_device(gvs_handle* h, const void* d_in, uint32_t in_stride,
+                                  const uint32_t* d_in_lens, uint32_t n, const uint64_t* d_times,
+                                  void* d_out, uint32_t out_stride, uint32_t* d_out_lens,
+                                  void* d_sigs) {
+  if (!h || h->kind != 0 || !wire_strides_ok(in_stride, out_stride) || n > max_submit(h) ||
+      (n && (!d_in || !d_in_lens || !d_times || !d_out || !d_out_lens)))
+    return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
+  GVS_HIP(h, hipSetDevice(h->device));
+  if (int r = reset_errors(h)) return r;
+  if (int r = wire_batch(h, d_in, in_stride, d_in_lens, n, d_times, d_out, out_stride,
+                         d_out_lens, d_sigs, nullptr))
+    return r;
+  return finish(h);
+}
+
+int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
+                           const uint32_t* in_lens, uint32_t n, const uint64_t* times,
+                           uint8_t* out, uint32_t out_stride, uint32_t* out_lens, uint8_t* sigs,
+                           uint32_t* decode_status) {
+  if (!h || h->kind != 0 || !wire_strides_ok(in_stride, out_stride) || n > max_submit(h) ||
+      (n && (!in || !in_lens || !times || !out || !out_lens)))
+    return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
+  GVS_HIP(h, hipSetDevice(h->device));
+  WireStage& w = h->wire;
+  if (!w.in) {
+    const uint64_t cap = max_submit(h);
+    if (int rc = dalloc_t(h, &w.in, cap * kWireSlotMax)) return rc;
+    if (int rc = dalloc_t(h, &w.out, cap * kWireSlotMax)) return rc;
+    if (int rc = dalloc_t(h, &w.in_lens, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.out_lens, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.times, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.sigs, cap * 4)) return rc;
+    if (int rc = dalloc_t(h, &w.status, cap)) return rc;
+  }
+  hipStream_t s = h->stream;
+  if (n) {
+    GVS_HIP(h, hipMemcpyAsync(w.in, in, (size_t)n * in_stride, hipMemcpyHostToDevice, s));
+    GVS_HIP(h, hipMemcpyAsync(w.in_lens, in_lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    GVS_HIP(h, hipMemcpyAsync(w.times, times, (size_t)n * 8, hipMemcpyHostToDevice, s));
+  }
+  if (int r = reset_errors(h)) return r;
+  if (int r = wire_batch(h, w.in, in_stride, w.in_lens, n, w.times, w.out, out_stride,
+                         w.out_lens, w.sigs, w.status))
+    return r;
+  if (n) {
+    GVS_HIP(h, hipMemcpyAsync(out, w.out, (size_t)n * out_stride, hipMemcpyDeviceToHost, s));
+    GVS_HIP(h, hipMemcpyAsync(out_lens, w.out_lens, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (sigs) GVS_HIP(h, hipMemcpyAsync(sigs, w.sigs, (size_t)n * 64, hipMemcpyDeviceToHost, s));
+    if (decode_status)
+      GVS_HIP(h, hipMemcpyAsync(decode_status, w.status, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  }
   return finish(h);
 }
 

@@ -31,6 +31,8 @@ EXPORTED = (
     "gvs_oram_set_timing", "gvs_oram_last_timings", "gvs_oram_last_error",
     "gvs_omap_create", "gvs_omap_destroy", "gvs_omap_access_batch", "gvs_omap_access_batch_device",
     "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
+    "gvs_process_wire_batch", "gvs_process_wire_batch_device", "gvs_wire_decode_device",
+    "gvs_wire_encode_device",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
                  "gvs_route_plan")
@@ -65,6 +67,10 @@ def load_library(path=None):
     lib.gvs_destroy.argtypes = [vp]
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
+    lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, u32, vp, vp, vp]
+    lib.gvs_process_wire_batch_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, u32, vp, vp]
+    lib.gvs_wire_decode_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, vp]
+    lib.gvs_wire_encode_device.argtypes = [vp, vp, u32, vp, u32, vp]
     lib.gvs_process_batches.argtypes = [vp, vp, vp, u32, vp, ctypes.POINTER(u32)]
     lib.gvs_access.argtypes = [vp, vp, vp]
     lib.gvs_get_stats.argtypes = [vp, ctypes.POINTER(abi.GvsStats)]
@@ -202,6 +208,35 @@ class ObliviousStore:
 
     def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
         self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))
+
+    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=abi.WIRE_RESPONSE_BYTES):
+        """Wire QueryRequests (list of bytes, or an (n, L) uint8 array of
+        canonical messages) through the device codec and the store
+        (gvs_process_wire_batch).  -> (list of response bytes, (n, 64)
+        signatures, per-request GVS_WIRE_* decode status).  A hard error's
+        response is b"" (the handler answers it with a gRPC error)."""
+        if isinstance(msgs, np.ndarray):
+            n, width = msgs.shape
+            lens = np.full(n, width, np.uint32)
+            stride = in_stride or width
+            slab = np.zeros((n, stride), np.uint8)
+            slab[:, :width] = msgs
+        else:
+            n = len(msgs)
+            lens = np.array([len(m) for m in msgs], np.uint32)
+            stride = in_stride or max(int(lens.max()) if n else 1, 1)
+            slab = np.zeros((n, stride), np.uint8)
+            for k, m in enumerate(msgs):
+                slab[k, :len(m)] = np.frombuffer(bytes(m), np.uint8)
+        times = np.ascontiguousarray(np.broadcast_to(np.asarray(times, np.uint64), (n,)))
+        out = np.zeros((n, out_stride), np.uint8)
+        out_lens = np.zeros(n, np.uint32)
+        sigs = np.zeros((n, 64), np.uint8)
+        status = np.zeros(n, np.uint32)
+        self._check(self.lib.gvs_process_wire_batch(
+            self.h, slab.ctypes.data, stride, lens.ctypes.data, n, times.ctypes.data,
+            out.ctypes.data, out_stride, out_lens.ctypes.data, sigs.ctypes.data, status.ctypes.data))
+        return [out[k, :out_lens[k]].tobytes() for k in range(n)], sigs, status
 
     def access(self, req):
         out = self.process_batch(np.asarray([req], dtype=abi.REQUEST_DTYPE) if not isinstance(req, np.ndarray) else req.reshape(1))

@@ -84,34 +84,70 @@ def encode_requests(reqs, signatures=None):
     return out
 
 
-def _read_varint(b, i):
-    v, s = 0, 0
-    while True:
-        c = b[i]
+class DecodeError(ValueError):
+    """The bytes are not a message prost would decode."""
+
+
+# field number -> wire type of the known fields (prost structs,
+# types/src/lib.rs:27-120): 0 varint, 1 fixed64, 2 length-delimited, 5 fixed32
+_REQ_SPEC = {1: 5, 2: 2, 3: 2, 4: 2}
+_REQREC_SPEC = {1: 2, 2: 2, 3: 2}
+_RESP_SPEC = {1: 2, 2: 5}
+_REC_SPEC = {1: 2, 2: 2, 3: 2, 4: 1, 5: 2}
+
+WIRE_OK, WIRE_DECODE_ERROR, WIRE_BAD_FIELD = abi.WIRE_OK, abi.WIRE_DECODE_ERROR, abi.WIRE_BAD_FIELD
+
+
+def _varint(b, i, end):
+    """prost decode_varint: at most 10 bytes, the 10th at most 1."""
+    v = 0
+    for c in range(10):
+        if i >= end:
+            break
+        x = b[i]
         i += 1
-        v |= (c & 0x7F) << s
-        s += 7
-        if not c & 0x80:
+        v |= (x & 0x7F) << (7 * c)
+        if x < 0x80:
+            if c == 9 and x > 1:
+                raise DecodeError("invalid varint")
             return v, i
+    raise DecodeError("invalid varint")
 
 
-def _fields(b):
-    i, out = 0, {}
-    while i < len(b):
-        key, i = _read_varint(b, i)
+def _walk(b, i, end, spec, out, nested=None):
+    """Decode fields in b[i:end) the way prost's generated merge does: a known
+    field must carry its wire type, unknown fields are skipped, the last
+    occurrence of a scalar / bytes field wins, and an embedded message named in
+    `nested` ({field: (spec, dict)}) is merged over all its occurrences.
+    [D] Groups (wire types 3/4) are rejected (prost would skip unknown ones)."""
+    while i < end:
+        key, i = _varint(b, i, end)
+        if key > 0xFFFFFFFF:
+            raise DecodeError("invalid key value")
         f, wt = key >> 3, key & 7
+        if f == 0 or wt in (3, 4) or wt > 5:
+            raise DecodeError(f"invalid tag {f} / wire type {wt}")
+        if f in spec and spec[f] != wt:
+            raise DecodeError(f"field {f}: wire type {wt}, expected {spec[f]}")
         if wt == 0:
-            v, i = _read_varint(b, i)
-        elif wt == 1:
-            v, i = int.from_bytes(b[i:i + 8], "little"), i + 8
-        elif wt == 5:
-            v, i = int.from_bytes(b[i:i + 4], "little"), i + 4
-        elif wt == 2:
-            ln, i = _read_varint(b, i)
-            v, i = bytes(b[i:i + ln]), i + ln
+            _, i = _varint(b, i, end)
+        elif wt in (1, 5):
+            sz = 8 if wt == 1 else 4
+            if end - i < sz:
+                raise DecodeError("buffer underflow")
+            if f in spec:
+                out[f] = int.from_bytes(bytes(b[i:i + sz]), "little")
+            i += sz
         else:
-            raise ValueError(f"unsupported wire type {wt}")
-        out[f] = v  # proto3: last one wins
+            ln, i = _varint(b, i, end)
+            if ln > end - i:
+                raise DecodeError("buffer underflow")
+            if f in spec:
+                if nested and f in nested:
+                    _walk(b, i, i + ln, nested[f][0], nested[f][1])
+                else:
+                    out[f] = bytes(b[i:i + ln])
+            i += ln
     return out
 
 
@@ -122,12 +158,24 @@ def _fixed(v, size, name):
     return np.frombuffer(v, np.uint8)
 
 
-def decode_requests(msgs, timestamps=None):
-    """Wire QueryRequests -> (gvs_request slab, (n, 64) signatures).
+def decode_request(m):
+    """One wire QueryRequest -> (fields, record fields) with prost semantics;
+    raises DecodeError."""
+    f, rec = {}, {}
+    _walk(bytes(m), 0, len(m), _REQ_SPEC, f, {4: (_REQREC_SPEC, rec)})
+    return f, rec
+
+
+def decode_requests(msgs, timestamps=None, strict=True):
+    """Wire QueryRequests -> (gvs_request slab, (n, 64) signatures[, status]).
 
     `msgs` is a list of bytes or an (n, 1099) uint8 array; `timestamps` is the
-    server time to stamp on each request (README.md:143-144)."""
-    canon = isinstance(msgs, np.ndarray) and msgs.ndim == 2 and msgs.shape[1] == REQUEST_WIRE_BYTES
+    server time to stamp on each request (README.md:143-144).  strict: a
+    message that fails to decode or has a field of the wrong size raises.
+    Otherwise it becomes an all-zero request of type 0 (a hard error in the
+    store) and a per-message GVS_WIRE_* status array is returned too: the
+    device codec's rule (gvs_process_wire_batch, include/gvstore.h)."""
+    canon = strict and isinstance(msgs, np.ndarray) and msgs.ndim == 2 and msgs.shape[1] == REQUEST_WIRE_BYTES
     if canon:
         for off, tag in _REQ_HDR:
             if not (msgs[:, off:off + len(tag)] == np.frombuffer(tag, np.uint8)).all():
@@ -142,32 +190,61 @@ def decode_requests(msgs, timestamps=None):
         q["msg_id"] = msgs[:, 110:126]
         q["recipient"] = msgs[:, 128:160]
         q["payload"] = msgs[:, 163:1099]
+        status = np.zeros(n, np.uint32)
     else:
         rows = [bytes(m) for m in msgs]
         n = len(rows)
         q = np.zeros(n, abi.REQUEST_DTYPE)
         sig = np.zeros((n, 64), np.uint8)
+        status = np.zeros(n, np.uint32)
         for k, m in enumerate(rows):
-            f = _fields(m)
-            rec = _fields(f.get(4, b""))
+            try:
+                f, rec = decode_request(m)
+            except DecodeError:
+                if strict:
+                    raise
+                status[k] = WIRE_DECODE_ERROR
+                continue
+            try:
+                vals = (_fixed(f.get(2), 32, "auth_identity"), _fixed(f.get(3), 64, "auth_signature"),
+                        _fixed(rec.get(1), 16, "msg_id"), _fixed(rec.get(2), 32, "recipient"),
+                        _fixed(rec.get(3), abi.PAYLOAD_BYTES, "payload"))
+            except ValueError:
+                if strict:
+                    raise
+                status[k] = WIRE_BAD_FIELD
+                continue
             q[k]["request_type"] = f.get(1, 0)
-            q[k]["auth_identity"] = _fixed(f.get(2), 32, "auth_identity")
-            sig[k] = _fixed(f.get(3), 64, "auth_signature")
-            q[k]["msg_id"] = _fixed(rec.get(1), 16, "msg_id")
-            q[k]["recipient"] = _fixed(rec.get(2), 32, "recipient")
-            q[k]["payload"] = _fixed(rec.get(3), abi.PAYLOAD_BYTES, "payload")
+            q[k]["auth_identity"], sig[k], q[k]["msg_id"], q[k]["recipient"], q[k]["payload"] = vals
     if timestamps is not None:
-        q["timestamp"] = timestamps
-    return q, sig
+        q["timestamp"] = np.where(status == 0, timestamps, 0)
+    return (q, sig) if strict else (q, sig, status)
+
+
+def encode_response(r):
+    """One gvs_response -> the bytes prost writes for its QueryResponse, or b""
+    for a hard error (status 0: the handler answers with a gRPC error).  A zero
+    timestamp is omitted (1033 B); otherwise 1042 B."""
+    if int(r["status_code"]) == 0:
+        return b""
+    rec = r["record"]
+    ts = int(rec["timestamp"])
+    body = (b"\x0a\x10" + bytes(rec["msg_id"]) + b"\x12\x20" + bytes(rec["sender"]) +
+            b"\x1a\x20" + bytes(rec["recipient"]) +
+            (b"\x21" + ts.to_bytes(8, "little") if ts else b"") +
+            b"\x2a\xa8\x07" + bytes(rec["payload"]))
+    ln = len(body)
+    return (b"\x0a" + bytes([(ln & 0x7F) | 0x80, ln >> 7]) + body + b"\x15" +
+            int(r["status_code"]).to_bytes(4, "little"))
 
 
 def decode_responses(msgs):
-    """Wire QueryResponses -> gvs_response slab (generic reader)."""
+    """Wire QueryResponses -> gvs_response slab (prost rules, strict)."""
     n = len(msgs)
     r = np.zeros(n, abi.RESPONSE_DTYPE)
     for k, m in enumerate(msgs):
-        f = _fields(bytes(m))
-        rec = _fields(f.get(1, b""))
+        f, rec = {}, {}
+        _walk(bytes(m), 0, len(m), _RESP_SPEC, f, {1: (_REC_SPEC, rec)})
         r[k]["record"]["msg_id"] = _fixed(rec.get(1), 16, "msg_id")
         r[k]["record"]["sender"] = _fixed(rec.get(2), 32, "sender")
         r[k]["record"]["recipient"] = _fixed(rec.get(3), 32, "recipient")

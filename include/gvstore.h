@@ -218,6 +218,56 @@ int gvs_process_batches(gvs_handle *h, const gvs_request *reqs, const uint32_t *
 int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
                              void *d_out);
 
+/* ---- wire codec ---------------------------------
+ * The protobuf messages of api/proto/grapevine.proto:123-176 as the prost
+ * structs of types/src/lib.rs:27-120 encode them.  A fully populated
+ * QueryRequest is 1099 B; a QueryResponse with nonzero timestamp and status is
+ * 1042 B (api/tests/grapevine_types.rs:22-31,46-55).
+ *
+ * Decoding follows prost: fields in any order, unknown fields skipped, the
+ * last occurrence of a field wins, the embedded RequestRecord merged over its
+ * occurrences; malformed varints, lengths past the message, a known field
+ * with another wire type, field number 0 and groups are decode errors.  A
+ * message that fails to decode, or whose auth_identity / auth_signature /
+ * msg_id / recipient / payload are not 32 / 64 / 16 / 32 / 936 bytes, becomes
+ * an all-zero request of type 0 (a hard error: grapevine.proto:57-64).
+ * Encoding writes what prost writes: 1042 B (1033 B if the timestamp is 0),
+ * or length 0 for a hard error (status 0), which the handler turns into a
+ * gRPC error.  Message k occupies bytes [k*stride, k*stride + len_k) of its
+ * slab; strides are at most GVS_WIRE_SLOT_MAX, output strides at least
+ * GVS_WIRE_RESPONSE_BYTES.  Every slot is read, and every output slot
+ * written, whole. */
+#define GVS_WIRE_REQUEST_BYTES 1099
+#define GVS_WIRE_RESPONSE_BYTES 1042
+#define GVS_WIRE_SLOT_MAX 2048
+#define GVS_WIRE_OK 0u            /* decode_status values */
+#define GVS_WIRE_DECODE_ERROR 1u  /* prost would fail to decode the message */
+#define GVS_WIRE_BAD_FIELD 2u     /* decoded, but a field has the wrong size */
+
+/* n wire requests (host buffers) through decode -> gvs_process_batch ->
+ * encode on the device.  times[k] is the server time of request k
+ * (README.md:143-144).  sigs (optional) receives the 64-B auth_signature of
+ * each request (zero when it failed to decode) for the caller's challenge
+ * check; decode_status (optional) one GVS_WIRE_* per request. */
+int gvs_process_wire_batch(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
+                           const uint32_t *in_lens, uint32_t n, const uint64_t *times,
+                           uint8_t *out, uint32_t out_stride, uint32_t *out_lens,
+                           uint8_t *sigs, uint32_t *decode_status);
+/* The same with device buffers (in: n*in_stride B, in_lens: n u32, times: n
+ * u64, out: n*out_stride B, out_lens: n u32, sigs: optional n*64 B). */
+int gvs_process_wire_batch_device(gvs_handle *h, const void *d_in, uint32_t in_stride,
+                                  const uint32_t *d_in_lens, uint32_t n, const uint64_t *d_times,
+                                  void *d_out, uint32_t out_stride, uint32_t *d_out_lens,
+                                  void *d_sigs);
+/* The codec alone, device buffers: wire requests -> gvs_request[n] (+ sigs,
+ * + per-request GVS_WIRE_* status, both optional); gvs_response[n] -> wire
+ * responses.  Synchronous on the handle's stream. */
+int gvs_wire_decode_device(gvs_handle *h, const void *d_wire, uint32_t stride,
+                           const uint32_t *d_lens, uint32_t n, const uint64_t *d_times,
+                           void *d_reqs, void *d_sigs, uint32_t *d_status);
+int gvs_wire_encode_device(gvs_handle *h, const void *d_resps, uint32_t n, void *d_wire,
+                           uint32_t stride, uint32_t *d_lens);
+
 /* Message expiry (README.md:86-99: the untrusted host supplies the time and
  * the expiry period).  From the next batch on, messages whose timestamp is
  * < cutoff expire: each batch's message pass records up to X of them (fixed

@@ -1,0 +1,168 @@
+"""GPU parity of the device wire codec (SURVEY.md §8(f) rank 1;
+include/gvstore.h gvs_process_wire_batch / gvs_wire_*_device).
+
+  * decode: canonical and non-canonical QueryRequest encodings (reordered,
+    repeated, merged records, unknown fields, non-minimal varints) and
+    malformed ones -> the device's gvs_request slab, signatures and per-message
+    status equal the host codec's prost-rule decoder (grapevine_amd/wire.py,
+    pinned against google.protobuf in tests/test_wire.py), bit for bit;
+  * encode: responses with and without timestamp, and hard errors -> the
+    bytes prost writes (wire.encode_response), whole output slots checked;
+  * end to end: wire requests through decode -> store -> encode on the GPU
+    equal the CPU oracle's responses encoded on the host.
+"""
+import numpy as np
+import pytest
+
+from grapevine_amd import abi, wire
+from grapevine_amd.store import ObliviousStore
+from oracle import ffi
+
+import wire_cases
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def host(t, dtype, shape):
+    return t.cpu().numpy().view(dtype).reshape(shape)
+
+
+def small_store():
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024)
+    return ObliviousStore(cfg), ffi.Model(cfg)
+
+
+def slab(msgs, stride):
+    s = np.zeros((len(msgs), stride), np.uint8)
+    for k, m in enumerate(msgs):
+        s[k, :len(m)] = np.frombuffer(m, np.uint8)
+    return s, np.array([len(m) for m in msgs], np.uint32)
+
+
+@pytest.mark.parametrize("stride", [1200, 2048])
+def test_decode_matches_prost_rules(stride):
+    store, _ = small_store()
+    cases = [(n, m) for n, m in wire_cases.all_variants(21 + stride, 12) if len(m) <= stride]
+    msgs = [m for _, m in cases]
+    n = len(msgs)
+    times = np.arange(1, n + 1, dtype=np.uint64) * 1_000_003
+    s, lens = slab(msgs, stride)
+    d_in, d_lens, d_t = dev(s), dev(lens), dev(times)
+    d_req = torch.zeros(n * 1040, dtype=torch.uint8, device="cuda")
+    d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n * 4,), 0xEE, dtype=torch.uint8, device="cuda")
+    rc = store.lib.gvs_wire_decode_device(store.h, d_in.data_ptr(), stride, d_lens.data_ptr(), n,
+                                          d_t.data_ptr(), d_req.data_ptr(), d_sig.data_ptr(),
+                                          d_st.data_ptr())
+    assert rc == 0
+    got_q = host(d_req, abi.REQUEST_DTYPE, (n,))
+    got_sig = host(d_sig, np.uint8, (n, 64))
+    got_st = host(d_st, np.uint32, (n,))
+    want_q, want_sig, want_st = wire.decode_requests(msgs, timestamps=times, strict=False)
+    for k, (name, _) in enumerate(cases):
+        assert got_st[k] == want_st[k], (k, name, got_st[k], want_st[k])
+        assert got_q[k].tobytes() == want_q[k].tobytes(), (k, name)
+        assert got_sig[k].tobytes() == want_sig[k].tobytes(), (k, name)
+    assert (got_st == 0).sum() > n // 4 and (got_st == 1).any() and (got_st == 2).any()
+    store.close()
+
+
+def test_length_beyond_stride_is_a_decode_error():
+    store, _ = small_store()
+    m = wire_cases.canonical(wire_cases.fields(__import__("random").Random(3)))
+    s, lens = slab([m], 1100)
+    lens[0] = 1101
+    d_req = torch.zeros(1040, dtype=torch.uint8, device="cuda")
+    d_st = torch.zeros(4, dtype=torch.uint8, device="cuda")
+    assert store.lib.gvs_wire_decode_device(store.h, dev(s).data_ptr(), 1100, dev(lens).data_ptr(), 1,
+                                            dev(np.array([7], np.uint64)).data_ptr(), d_req.data_ptr(),
+                                            None, d_st.data_ptr()) == 0
+    assert host(d_st, np.uint32, (1,))[0] == abi.WIRE_DECODE_ERROR
+    assert not d_req.any().item()
+    store.close()
+
+
+@pytest.mark.parametrize("stride", [1042, 1100])
+def test_encode_matches_prost(stride):
+    store, _ = small_store()
+    rng = np.random.default_rng(5)
+    n = 301
+    r = np.zeros(n, abi.RESPONSE_DTYPE)
+    raw = r.view(np.uint8).reshape(n, 1040)
+    raw[:, :1024] = rng.integers(0, 256, (n, 1024), dtype=np.uint8)
+    r["record"]["timestamp"][::5] = 0
+    r["status_code"] = rng.integers(1, 9, n)
+    r["status_code"][3::7] = 0
+    d_out = torch.full((n * stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
+    assert store.lib.gvs_wire_encode_device(store.h, dev(r).data_ptr(), n, d_out.data_ptr(), stride,
+                                            d_len.data_ptr()) == 0
+    out = host(d_out, np.uint8, (n, stride))
+    lens = host(d_len, np.uint32, (n,))
+    for k in range(n):
+        want = wire.encode_response(r[k])
+        assert lens[k] == len(want), k
+        assert out[k, :lens[k]].tobytes() == want, k
+        assert not out[k, lens[k]:].any(), k  # the rest of the slot is zero-filled
+    store.close()
+
+
+def to_wire(reqs, rng):
+    """The oracle's request stream as canonical wire messages, with a few
+    replaced by non-canonical encodings of the same request or by malformed
+    messages."""
+    msgs = []
+    for k, q in enumerate(reqs):
+        f = dict(rt=int(q["request_type"]), auth=bytes(q["auth_identity"]), sig=rng.bytes(64),
+                 id=bytes(q["msg_id"]), rc=bytes(q["recipient"]), pl=bytes(q["payload"]))
+        m = wire_cases.canonical(f)
+        pick = rng.random()
+        if pick < 0.05:
+            m = wire_cases.ld(4, wire_cases.record(f, (2, 3, 1))) + m[:105]
+        elif pick < 0.08:
+            m = m[:rng.integers(1, len(m))]
+        msgs.append(m)
+    return msgs
+
+
+@pytest.mark.parametrize("host_api", [True, False])
+def test_wire_batches_end_to_end(host_api):
+    store, model = small_store()
+    model.seed(31)
+    params = ffi.gen_params(n_identities=200, hot=10)
+    rng = np.random.default_rng(17)
+    for b in range(4):
+        reqs = model.gen_batch(1024, params)
+        msgs = to_wire(reqs, rng)
+        times = reqs["timestamp"].copy()
+        q, sig, st = wire.decode_requests(msgs, timestamps=times, strict=False)
+        want = [wire.encode_response(r) for r in model.process_batch(q)]
+        if host_api:
+            got, got_sig, got_st = store.process_wire_batch(msgs, times, in_stride=1104)
+            assert (got_st == st).all()
+            assert got_sig.tobytes() == sig.tobytes()
+        else:
+            s, lens = slab(msgs, 1104)
+            n = len(msgs)
+            d_out = torch.zeros(n * 1042, dtype=torch.uint8, device="cuda")
+            d_len = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
+            d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+            store._check(store.lib.gvs_process_wire_batch_device(
+                store.h, dev(s).data_ptr(), 1104, dev(lens).data_ptr(), n, dev(times).data_ptr(),
+                d_out.data_ptr(), 1042, d_len.data_ptr(), d_sig.data_ptr()))
+            out = host(d_out, np.uint8, (n, 1042))
+            ol = host(d_len, np.uint32, (n,))
+            got = [out[k, :ol[k]].tobytes() for k in range(n)]
+            assert host(d_sig, np.uint8, (n, 64)).tobytes() == sig.tobytes()
+        bad = [k for k in range(len(want)) if got[k] != want[k]]
+        assert not bad, f"batch {b}: {len(bad)} responses differ (first {bad[:5]})"
+        assert sum(1 for w in want if len(w) == 1042) > 900
+        st_ = store.stats()
+        assert (st_["messages"], st_["mailboxes"]) == (model.messages, model.mailboxes)
+    store.close()

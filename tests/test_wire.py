@@ -121,3 +121,71 @@ def test_enum_values():
             abi.STATUS_CODE_INVALID_RECIPIENT, abi.STATUS_CODE_TOO_MANY_MESSAGES_FOR_RECIPIENT,
             abi.STATUS_CODE_TOO_MANY_RECIPIENTS, abi.STATUS_CODE_TOO_MANY_MESSAGES,
             abi.STATUS_CODE_INTERNAL_ERROR] == list(range(1, 9))
+
+
+# ---- prost decoding rules (the device codec's rule, gvs_process_wire_batch) ----
+
+from wire_cases import all_variants  # noqa: E402
+
+
+def test_prost_rules_match_google_protobuf_on_valid_variants():
+    """Reordered, repeated (last wins), merged-record, unknown-field and
+    non-minimal-varint encodings decode to the same fields under the host
+    codec's prost rules and under google.protobuf."""
+    cases = all_variants(7, 6)
+    good = [(n, m) for n, m in cases if not n.startswith("bad_")]
+    q, sig, st = wire.decode_requests([m for _, m in good], timestamps=5, strict=False)
+    for k, (name, m) in enumerate(good):
+        ref = QueryRequest.FromString(m)
+        assert st[k] == wire.WIRE_OK, name
+        assert q[k]["request_type"] == ref.request_type, name
+        assert bytes(q[k]["auth_identity"]) == ref.auth_identity, name
+        assert bytes(sig[k]) == ref.auth_signature, name
+        assert bytes(q[k]["msg_id"]) == ref.record.msg_id, name
+        assert bytes(q[k]["recipient"]) == ref.record.recipient, name
+        assert bytes(q[k]["payload"]) == ref.record.payload, name
+        assert q[k]["timestamp"] == 5
+
+
+def test_malformed_variants_are_rejected():
+    cases = all_variants(8, 4)
+    bad = [(n, m) for n, m in cases if n.startswith("bad_")]
+    q, sig, st = wire.decode_requests([m for _, m in bad], timestamps=5, strict=False)
+    for k, (name, m) in enumerate(bad):
+        assert st[k] in (wire.WIRE_DECODE_ERROR, wire.WIRE_BAD_FIELD), name
+        assert q[k].tobytes() == bytes(abi.REQUEST_DTYPE.itemsize), name  # type 0: a hard error
+        assert not sig[k].any()
+    # structural errors google.protobuf also refuses
+    for name, m in bad:
+        if name in ("bad_varint_11_bytes", "bad_length_past_end", "bad_record_past_end",
+                    "bad_field_zero", "bad_wire_type_6", "bad_fixed_past_end"):
+            with pytest.raises(Exception):
+                QueryRequest.FromString(m)
+        if name.startswith("bad_") and name[4:] in ("auth_short", "sig_long", "payload_short"):
+            assert wire.decode_requests([m], strict=False)[2][0] == wire.WIRE_BAD_FIELD
+    with pytest.raises(ValueError):
+        wire.decode_requests([bad[0][1]], strict=True)
+
+
+def test_encode_response_matches_google_protobuf():
+    rng = random.Random(11)
+    r = np.zeros(24, abi.RESPONSE_DTYPE)
+    for k in range(24):
+        r[k]["record"]["msg_id"] = np.frombuffer(rb(rng, 16), np.uint8)
+        r[k]["record"]["sender"] = np.frombuffer(rb(rng, 32), np.uint8)
+        r[k]["record"]["recipient"] = np.frombuffer(rb(rng, 32), np.uint8)
+        r[k]["record"]["payload"] = np.frombuffer(rb(rng, 936), np.uint8)
+        r[k]["record"]["timestamp"] = 0 if k % 5 == 0 else rng.getrandbits(64)
+        r[k]["status_code"] = 0 if k % 7 == 3 else rng.randrange(1, 9)
+    for k in range(24):
+        enc = wire.encode_response(r[k])
+        if r[k]["status_code"] == 0:
+            assert enc == b""
+            continue
+        rec = r[k]["record"]
+        ref = QueryResponse(record=dict(msg_id=bytes(rec["msg_id"]), sender=bytes(rec["sender"]),
+                                        recipient=bytes(rec["recipient"]), timestamp=int(rec["timestamp"]),
+                                        payload=bytes(rec["payload"])),
+                            status_code=int(r[k]["status_code"])).SerializeToString()
+        assert enc == ref
+        assert len(enc) == (1042 if rec["timestamp"] else 1033)
