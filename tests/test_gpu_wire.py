@@ -57,6 +57,7 @@ def test_decode_matches_prost_rules(stride):
     d_req = torch.zeros(n * 1040, dtype=torch.uint8, device="cuda")
     d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
     d_st = torch.full((n * 4,), 0xEE, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # torch's fills/copies done before the engine stream runs
     rc = store.lib.gvs_wire_decode_device(store.h, d_in.data_ptr(), stride, d_lens.data_ptr(), n,
                                           d_t.data_ptr(), d_req.data_ptr(), d_sig.data_ptr(),
                                           d_st.data_ptr())
@@ -80,9 +81,11 @@ def test_length_beyond_stride_is_a_decode_error():
     lens[0] = 1101
     d_req = torch.zeros(1040, dtype=torch.uint8, device="cuda")
     d_st = torch.zeros(4, dtype=torch.uint8, device="cuda")
-    assert store.lib.gvs_wire_decode_device(store.h, dev(s).data_ptr(), 1100, dev(lens).data_ptr(), 1,
-                                            dev(np.array([7], np.uint64)).data_ptr(), d_req.data_ptr(),
-                                            None, d_st.data_ptr()) == 0
+    keep = [dev(s), dev(lens), dev(np.array([7], np.uint64))]  # alive across the call
+    torch.cuda.synchronize()
+    assert store.lib.gvs_wire_decode_device(store.h, keep[0].data_ptr(), 1100, keep[1].data_ptr(), 1,
+                                            keep[2].data_ptr(), d_req.data_ptr(), None,
+                                            d_st.data_ptr()) == 0
     assert host(d_st, np.uint32, (1,))[0] == abi.WIRE_DECODE_ERROR
     assert not d_req.any().item()
     store.close()
@@ -101,7 +104,9 @@ def test_encode_matches_prost(stride):
     r["status_code"][3::7] = 0
     d_out = torch.full((n * stride,), 0xAB, dtype=torch.uint8, device="cuda")
     d_len = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
-    assert store.lib.gvs_wire_encode_device(store.h, dev(r).data_ptr(), n, d_out.data_ptr(), stride,
+    d_r = dev(r)
+    torch.cuda.synchronize()
+    assert store.lib.gvs_wire_encode_device(store.h, d_r.data_ptr(), n, d_out.data_ptr(), stride,
                                             d_len.data_ptr()) == 0
     out = host(d_out, np.uint8, (n, stride))
     lens = host(d_len, np.uint32, (n,))
@@ -153,8 +158,10 @@ def test_wire_batches_end_to_end(host_api):
             d_out = torch.zeros(n * 1042, dtype=torch.uint8, device="cuda")
             d_len = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
             d_sig = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+            d_in, d_lens, d_t = dev(s), dev(lens), dev(times)  # alive across the call
+            torch.cuda.synchronize()
             store._check(store.lib.gvs_process_wire_batch_device(
-                store.h, dev(s).data_ptr(), 1104, dev(lens).data_ptr(), n, dev(times).data_ptr(),
+                store.h, d_in.data_ptr(), 1104, d_lens.data_ptr(), n, d_t.data_ptr(),
                 d_out.data_ptr(), 1042, d_len.data_ptr(), d_sig.data_ptr()))
             out = host(d_out, np.uint8, (n, 1042))
             ol = host(d_len, np.uint32, (n,))
