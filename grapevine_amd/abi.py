@@ -93,7 +93,7 @@ class GvsStats(ctypes.Structure):
 
 # wire codec (gvs_process_wire_batch, include/gvstore.h)
 WIRE_REQUEST_BYTES, WIRE_RESPONSE_BYTES, WIRE_SLOT_MAX = 1099, 1042, 2048
-WIRE_OK, WIRE_DECODE_ERROR, WIRE_BAD_FIELD = 0, 1, 2
+WIRE_OK, WIRE_DECODE_ERROR, WIRE_BAD_FIELD, WIRE_BAD_SIGNATURE = 0, 1, 2, 3
 
 COMM_ID_BYTES = 128
 FLAG_AUTH_STORAGE = 1  # GVS_FLAG_AUTH_STORAGE: AES-CTR + BLAKE2b sealed tables

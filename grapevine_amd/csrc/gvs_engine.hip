@@ -29,6 +29,7 @@
 #include "gvs_kv.h"
 #include "gvs_omap.h"
 #include "gvs_wire.h"
+#include "gvs_sr25519.h"
 
 using namespace gvs;
 
@@ -186,6 +187,7 @@ struct WireStage {
   uint64_t* times = nullptr;
   uint4* sigs = nullptr;
   uint32_t* status = nullptr;
+  uint4* chal = nullptr;     // n x 32-B challenges
 };
 
 struct gvs_handle {
@@ -1044,12 +1046,18 @@ static int agree_errors(gvs_handle* h) {
 // Enqueue one batch: n requests in the caller layout at d_in, responses in the
 // caller layout to d_out (kLocal: n <= S*Bsub, source k = requests
 // [k*Bsub, (k+1)*Bsub)).
+static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out);
+
 static int run_batch(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out,
                      bool reset = true) {
   h->n_marks = 0;
   mark(h, "start");
   if (reset)
     if (int r = reset_errors(h)) return r;
+  return run_batch_body(h, d_in, n, d_out);
+}
+
+static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d_out) {
   if (h->mode == kSingle) {
     Engine& e = h->eng[0];
     if (int r = phase_a2(h, e, d_in, kAbiU4, n)) return r;
@@ -1632,22 +1640,83 @@ int gvs_wire_encode_device(gvs_handle* h, const void* d_resps, uint32_t n, void*
   return GVS_OK;
 }
 
-// decode -> the batch -> encode, all on the engine stream; the request and
-// response slabs live in the handle's host-API staging.
+// grapevine's challenge signing context (types/src/lib.rs:13)
+static const char kChallengeContext[] = "grapevine-challenge";
+
+static int sr_args(const uint8_t* context, uint32_t context_len, sr::SrArgs& a) {
+  if (context_len > sizeof a.ctx || (context_len && !context)) return GVS_ERR_INVALID_ARG;
+  std::memset(&a, 0, sizeof a);
+  if (context_len) std::memcpy(a.ctx, context, context_len);
+  a.ctx_len = context_len;
+  return GVS_OK;
+}
+
+static void enqueue_sr_verify(gvs_handle* h, const sr::SrArgs& a) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(sr::k_sr_verify, dim3((a.n + sr::kSrThreads - 1) / sr::kSrThreads),
+                     dim3(sr::kSrThreads), 0, h->stream, a);
+}
+
+// Handle-owned wire staging: signatures and statuses always (the device path
+// may not pass them), the host-side slabs only for gvs_process_wire_batch.
+static int wire_stage_init(gvs_handle* h, bool io) {
+  WireStage& w = h->wire;
+  const uint64_t cap = max_submit(h);
+  if (!w.sigs) {
+    if (int rc = dalloc_t(h, &w.sigs, cap * 4)) return rc;
+    if (int rc = dalloc_t(h, &w.status, cap)) return rc;
+  }
+  if (io && !w.in) {
+    if (int rc = dalloc_t(h, &w.in, cap * kWireSlotMax)) return rc;
+    if (int rc = dalloc_t(h, &w.out, cap * kWireSlotMax)) return rc;
+    if (int rc = dalloc_t(h, &w.in_lens, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.out_lens, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.times, cap)) return rc;
+    if (int rc = dalloc_t(h, &w.chal, cap * 2)) return rc;
+  }
+  return GVS_OK;
+}
+
+// decode -> (challenge check) -> the batch -> encode, all on the engine
+// stream; the request and response slabs live in the handle's host-API
+// staging.  d_chal: n x 32-B challenges, or null (signatures not checked).
 static int wire_batch(gvs_handle* h, const void* d_in, uint32_t in_stride, const uint32_t* d_in_lens,
-                      uint32_t n, const uint64_t* d_times, void* d_out, uint32_t out_stride,
-                      uint32_t* d_out_lens, void* d_sigs, uint32_t* d_status) {
-  enqueue_wire_decode(h, d_in, in_stride, d_in_lens, n, d_times, h->in_stage, d_sigs, d_status);
-  if (int r = run_batch(h, h->in_stage, n, h->out_stage)) return r;
+                      uint32_t n, const uint64_t* d_times, const void* d_chal, void* d_out,
+                      uint32_t out_stride, uint32_t* d_out_lens, void* d_sigs, uint32_t* d_status) {
+  if (int rc = wire_stage_init(h, false)) return rc;
+  h->n_marks = 0;
+  mark(h, "start");
+  uint4* sigs = d_sigs ? (uint4*)d_sigs : h->wire.sigs;
+  uint32_t* status = d_status ? d_status : h->wire.status;
+  enqueue_wire_decode(h, d_in, in_stride, d_in_lens, n, d_times, h->in_stage, sigs, status);
+  mark(h, "wire_decode");
+  if (d_chal) {
+    sr::SrArgs a;
+    (void)sr_args((const uint8_t*)kChallengeContext, sizeof kChallengeContext - 1, a);
+    a.pk = (const uint8_t*)h->in_stage + 16;  // gvs_request.auth_identity
+    a.pk_stride = sizeof(gvs_request);
+    a.msg = (const uint8_t*)d_chal;
+    a.msg_stride = 32;
+    a.msg_len = 32;
+    a.sig = (const uint8_t*)sigs;
+    a.sig_stride = 64;
+    a.n = n;
+    a.reqs = h->in_stage;
+    a.status = status;
+    enqueue_sr_verify(h, a);
+    mark(h, "sr_verify");
+  }
+  if (int r = run_batch_body(h, h->in_stage, n, h->out_stage)) return r;
   enqueue_wire_encode(h, h->out_stage, n, d_out, out_stride, d_out_lens);
+  mark(h, "wire_encode");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
 }
 
 int gvs_process_wire_batch_device(gvs_handle* h, const void* d_in, uint32_t in_stride,
                                   const uint32_t* d_in_lens, uint32_t n, const uint64_t* d_times,
-                                  void* d_out, uint32_t out_stride, uint32_t* d_out_lens,
-                                  void* d_sigs) {
+                                  const void* d_challenges, void* d_out, uint32_t out_stride,
+                                  uint32_t* d_out_lens, void* d_sigs, uint32_t* d_status) {
   if (!h || h->kind != 0 || !wire_strides_ok(in_stride, out_stride) || n > max_submit(h) ||
       (n && (!d_in || !d_in_lens || !d_times || !d_out || !d_out_lens)))
     return GVS_ERR_INVALID_ARG;
@@ -1655,42 +1724,35 @@ int gvs_process_wire_batch_device(gvs_handle* h, const void* d_in, uint32_t in_s
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   if (int r = reset_errors(h)) return r;
-  if (int r = wire_batch(h, d_in, in_stride, d_in_lens, n, d_times, d_out, out_stride,
-                         d_out_lens, d_sigs, nullptr))
+  if (int r = wire_batch(h, d_in, in_stride, d_in_lens, n, d_times, d_challenges, d_out,
+                         out_stride, d_out_lens, d_sigs, d_status))
     return r;
   return finish(h);
 }
 
 int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
                            const uint32_t* in_lens, uint32_t n, const uint64_t* times,
-                           uint8_t* out, uint32_t out_stride, uint32_t* out_lens, uint8_t* sigs,
-                           uint32_t* decode_status) {
+                           const uint8_t* challenges, uint8_t* out, uint32_t out_stride,
+                           uint32_t* out_lens, uint8_t* sigs, uint32_t* decode_status) {
   if (!h || h->kind != 0 || !wire_strides_ok(in_stride, out_stride) || n > max_submit(h) ||
       (n && (!in || !in_lens || !times || !out || !out_lens)))
     return GVS_ERR_INVALID_ARG;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
+  if (int rc = wire_stage_init(h, true)) return rc;
   WireStage& w = h->wire;
-  if (!w.in) {
-    const uint64_t cap = max_submit(h);
-    if (int rc = dalloc_t(h, &w.in, cap * kWireSlotMax)) return rc;
-    if (int rc = dalloc_t(h, &w.out, cap * kWireSlotMax)) return rc;
-    if (int rc = dalloc_t(h, &w.in_lens, cap)) return rc;
-    if (int rc = dalloc_t(h, &w.out_lens, cap)) return rc;
-    if (int rc = dalloc_t(h, &w.times, cap)) return rc;
-    if (int rc = dalloc_t(h, &w.sigs, cap * 4)) return rc;
-    if (int rc = dalloc_t(h, &w.status, cap)) return rc;
-  }
   hipStream_t s = h->stream;
   if (n) {
     GVS_HIP(h, hipMemcpyAsync(w.in, in, (size_t)n * in_stride, hipMemcpyHostToDevice, s));
     GVS_HIP(h, hipMemcpyAsync(w.in_lens, in_lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
     GVS_HIP(h, hipMemcpyAsync(w.times, times, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (challenges)
+      GVS_HIP(h, hipMemcpyAsync(w.chal, challenges, (size_t)n * 32, hipMemcpyHostToDevice, s));
   }
   if (int r = reset_errors(h)) return r;
-  if (int r = wire_batch(h, w.in, in_stride, w.in_lens, n, w.times, w.out, out_stride,
-                         w.out_lens, w.sigs, w.status))
+  if (int r = wire_batch(h, w.in, in_stride, w.in_lens, n, w.times, challenges ? w.chal : nullptr,
+                         w.out, out_stride, w.out_lens, w.sigs, w.status))
     return r;
   if (n) {
     GVS_HIP(h, hipMemcpyAsync(out, w.out, (size_t)n * out_stride, hipMemcpyDeviceToHost, s));
@@ -1700,6 +1762,67 @@ int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
       GVS_HIP(h, hipMemcpyAsync(decode_status, w.status, (size_t)n * 4, hipMemcpyDeviceToHost, s));
   }
   return finish(h);
+}
+
+int gvs_sr25519_verify_device(gvs_handle* h, const void* d_pks, uint32_t pk_stride,
+                              const void* d_msgs, uint32_t msg_stride, uint32_t msg_len,
+                              const void* d_sigs, uint32_t sig_stride, uint32_t n,
+                              const uint8_t* context, uint32_t context_len, uint32_t* d_ok) {
+  sr::SrArgs a;
+  if (!h || sr_args(context, context_len, a) || pk_stride < 32 || sig_stride < 64 ||
+      msg_stride < msg_len || msg_len > 4096 || (n && (!d_pks || (msg_len && !d_msgs) || !d_sigs || !d_ok)))
+    return GVS_ERR_INVALID_ARG;
+  GVS_HIP(h, hipSetDevice(h->device));
+  a.pk = (const uint8_t*)d_pks;
+  a.pk_stride = pk_stride;
+  a.msg = (const uint8_t*)d_msgs;
+  a.msg_stride = msg_stride;
+  a.msg_len = msg_len;
+  a.sig = (const uint8_t*)d_sigs;
+  a.sig_stride = sig_stride;
+  a.n = n;
+  a.ok = d_ok;
+  h->n_marks = 0;
+  mark(h, "start");
+  enqueue_sr_verify(h, a);
+  mark(h, "sr_verify");
+  GVS_HIP(h, hipGetLastError());
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return GVS_OK;
+}
+
+int gvs_sr25519_verify(gvs_handle* h, const uint8_t* pks, const uint8_t* msgs, uint32_t msg_len,
+                       const uint8_t* sigs, uint32_t n, const uint8_t* context,
+                       uint32_t context_len, uint32_t* ok) {
+  if (!h || (n && (!pks || (msg_len && !msgs) || !sigs || !ok)) || msg_len > 4096)
+    return GVS_ERR_INVALID_ARG;
+  if (!n) return GVS_OK;
+  GVS_HIP(h, hipSetDevice(h->device));
+  const size_t b_pk = (size_t)n * 32, b_msg = (size_t)n * msg_len, b_sig = (size_t)n * 64,
+               b_ok = (size_t)n * 4;
+  uint8_t* d = nullptr;
+  GVS_HIP(h, hipMalloc((void**)&d, b_pk + b_msg + b_sig + b_ok + 64));
+  hipStream_t s = h->stream;
+  int rc = GVS_OK;
+  auto step = [&](hipError_t e) {
+    if (rc == GVS_OK && e != hipSuccess) {
+      h->err = hipGetErrorString(e);
+      rc = GVS_ERR_DEVICE;
+    }
+  };
+  step(hipMemcpyAsync(d, pks, b_pk, hipMemcpyHostToDevice, s));
+  if (b_msg) step(hipMemcpyAsync(d + b_pk, msgs, b_msg, hipMemcpyHostToDevice, s));
+  step(hipMemcpyAsync(d + b_pk + b_msg, sigs, b_sig, hipMemcpyHostToDevice, s));
+  uint32_t* d_ok = (uint32_t*)(d + ((b_pk + b_msg + b_sig + 3) & ~(size_t)3));
+  if (rc == GVS_OK)
+    rc = gvs_sr25519_verify_device(h, d, 32, d + b_pk, msg_len ? msg_len : 1, msg_len,
+                                   d + b_pk + b_msg, 64, n, context, context_len, d_ok);
+  if (rc == GVS_OK) {
+    step(hipMemcpyAsync(ok, d_ok, b_ok, hipMemcpyDeviceToHost, s));
+    step(hipStreamSynchronize(s));
+  }
+  (void)hipFree(d);
+  return rc;
 }
 
 int gvs_set_expiry_cutoff(gvs_handle* h, uint64_t cutoff) {

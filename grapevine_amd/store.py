@@ -32,7 +32,7 @@ EXPORTED = (
     "gvs_omap_create", "gvs_omap_destroy", "gvs_omap_access_batch", "gvs_omap_access_batch_device",
     "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
     "gvs_process_wire_batch", "gvs_process_wire_batch_device", "gvs_wire_decode_device",
-    "gvs_wire_encode_device",
+    "gvs_wire_encode_device", "gvs_sr25519_verify", "gvs_sr25519_verify_device",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
                  "gvs_route_plan")
@@ -67,8 +67,10 @@ def load_library(path=None):
     lib.gvs_destroy.argtypes = [vp]
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
-    lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, u32, vp, vp, vp]
-    lib.gvs_process_wire_batch_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, u32, vp, vp]
+    lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
+    lib.gvs_process_wire_batch_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
+    lib.gvs_sr25519_verify.argtypes = [vp, vp, vp, u32, vp, u32, vp, u32, vp]
+    lib.gvs_sr25519_verify_device.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, u32, vp, u32, vp]
     lib.gvs_wire_decode_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, vp]
     lib.gvs_wire_encode_device.argtypes = [vp, vp, u32, vp, u32, vp]
     lib.gvs_process_batches.argtypes = [vp, vp, vp, u32, vp, ctypes.POINTER(u32)]
@@ -209,12 +211,15 @@ class ObliviousStore:
     def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
         self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))
 
-    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=abi.WIRE_RESPONSE_BYTES):
+    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=abi.WIRE_RESPONSE_BYTES,
+                           challenges=None):
         """Wire QueryRequests (list of bytes, or an (n, L) uint8 array of
         canonical messages) through the device codec and the store
-        (gvs_process_wire_batch).  -> (list of response bytes, (n, 64)
-        signatures, per-request GVS_WIRE_* decode status).  A hard error's
-        response is b"" (the handler answers it with a gRPC error)."""
+        (gvs_process_wire_batch).  `challenges` ((n, 32) uint8, optional): the
+        challenge each auth_signature must sign; failing requests become hard
+        errors.  -> (list of response bytes, (n, 64) signatures, per-request
+        GVS_WIRE_* status).  A hard error's response is b"" (the handler
+        answers it with a gRPC error)."""
         if isinstance(msgs, np.ndarray):
             n, width = msgs.shape
             lens = np.full(n, width, np.uint32)
@@ -233,10 +238,28 @@ class ObliviousStore:
         out_lens = np.zeros(n, np.uint32)
         sigs = np.zeros((n, 64), np.uint8)
         status = np.zeros(n, np.uint32)
+        chal = None
+        if challenges is not None:
+            chal = np.ascontiguousarray(challenges, np.uint8).reshape(n, 32)
         self._check(self.lib.gvs_process_wire_batch(
             self.h, slab.ctypes.data, stride, lens.ctypes.data, n, times.ctypes.data,
-            out.ctypes.data, out_stride, out_lens.ctypes.data, sigs.ctypes.data, status.ctypes.data))
+            chal.ctypes.data if chal is not None else None, out.ctypes.data, out_stride,
+            out_lens.ctypes.data, sigs.ctypes.data, status.ctypes.data))
         return [out[k, :out_lens[k]].tobytes() for k in range(n)], sigs, status
+
+    def sr25519_verify(self, pks, msgs, sigs, context=b"grapevine-challenge"):
+        """Batched schnorrkel verification on the device (gvs_sr25519_verify):
+        pks (n, 32), msgs (n, L), sigs (n, 64) uint8 -> (n,) bool."""
+        pks = np.ascontiguousarray(pks, np.uint8)
+        msgs = np.ascontiguousarray(msgs, np.uint8)
+        sigs = np.ascontiguousarray(sigs, np.uint8)
+        n = len(pks)
+        ok = np.zeros(n, np.uint32)
+        self._check(self.lib.gvs_sr25519_verify(self.h, pks.ctypes.data, msgs.ctypes.data,
+                                                msgs.shape[1] if msgs.ndim == 2 else 0,
+                                                sigs.ctypes.data, n, context, len(context),
+                                                ok.ctypes.data))
+        return ok.astype(bool)
 
     def access(self, req):
         out = self.process_batch(np.asarray([req], dtype=abi.REQUEST_DTYPE) if not isinstance(req, np.ndarray) else req.reshape(1))

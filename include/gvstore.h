@@ -243,22 +243,29 @@ int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
 #define GVS_WIRE_OK 0u            /* decode_status values */
 #define GVS_WIRE_DECODE_ERROR 1u  /* prost would fail to decode the message */
 #define GVS_WIRE_BAD_FIELD 2u     /* decoded, but a field has the wrong size */
+#define GVS_WIRE_BAD_SIGNATURE 3u /* decoded, but the challenge signature does not verify */
 
-/* n wire requests (host buffers) through decode -> gvs_process_batch ->
- * encode on the device.  times[k] is the server time of request k
- * (README.md:143-144).  sigs (optional) receives the 64-B auth_signature of
- * each request (zero when it failed to decode) for the caller's challenge
- * check; decode_status (optional) one GVS_WIRE_* per request. */
+/* n wire requests (host buffers) through decode -> [challenge check] ->
+ * gvs_process_batch -> encode on the device.  times[k] is the server time of
+ * request k (README.md:143-144).  challenges (optional, n x 32 B): the
+ * challenge each request's auth_signature must sign (README.md:187-200); a
+ * request whose signature does not verify as a schnorrkel signature by its
+ * auth_identity under the context "grapevine-challenge" (types/src/lib.rs:13)
+ * becomes a hard error (decode_status GVS_WIRE_BAD_SIGNATURE).  NULL: no
+ * check (the caller verified).  sigs (optional) receives each request's 64-B
+ * auth_signature (zero when it failed to decode); decode_status (optional)
+ * one GVS_WIRE_* per request. */
 int gvs_process_wire_batch(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
                            const uint32_t *in_lens, uint32_t n, const uint64_t *times,
-                           uint8_t *out, uint32_t out_stride, uint32_t *out_lens,
-                           uint8_t *sigs, uint32_t *decode_status);
+                           const uint8_t *challenges, uint8_t *out, uint32_t out_stride,
+                           uint32_t *out_lens, uint8_t *sigs, uint32_t *decode_status);
 /* The same with device buffers (in: n*in_stride B, in_lens: n u32, times: n
- * u64, out: n*out_stride B, out_lens: n u32, sigs: optional n*64 B). */
+ * u64, challenges: optional n*32 B, out: n*out_stride B, out_lens: n u32,
+ * sigs: optional n*64 B, decode_status: optional n u32). */
 int gvs_process_wire_batch_device(gvs_handle *h, const void *d_in, uint32_t in_stride,
                                   const uint32_t *d_in_lens, uint32_t n, const uint64_t *d_times,
-                                  void *d_out, uint32_t out_stride, uint32_t *d_out_lens,
-                                  void *d_sigs);
+                                  const void *d_challenges, void *d_out, uint32_t out_stride,
+                                  uint32_t *d_out_lens, void *d_sigs, uint32_t *d_decode_status);
 /* The codec alone, device buffers: wire requests -> gvs_request[n] (+ sigs,
  * + per-request GVS_WIRE_* status, both optional); gvs_response[n] -> wire
  * responses.  Synchronous on the handle's stream. */
@@ -267,6 +274,22 @@ int gvs_wire_decode_device(gvs_handle *h, const void *d_wire, uint32_t stride,
                            void *d_reqs, void *d_sigs, uint32_t *d_status);
 int gvs_wire_encode_device(gvs_handle *h, const void *d_resps, uint32_t n, void *d_wire,
                            uint32_t stride, uint32_t *d_lens);
+
+/* Schnorrkel signature check (README.md:187-200,
+ * mc-crypto-keys' RistrettoPublic::verify_schnorrkel): ok[k] = 1 iff sigs[k]
+ * (R || s, 64 B, schnorrkel's marker bit set) is a valid signature by the
+ * ristretto255 public key pks[k] on msgs[k] under the signing context
+ * `context` (<= 64 B; grapevine uses "grapevine-challenge"), else 0.  Batched
+ * on the handle's device, one thread per signature, the same instruction
+ * stream whatever the inputs.  Device form: pk k at d_pks + k*pk_stride, msg k
+ * (msg_len bytes) at d_msgs + k*msg_stride, sig k at d_sigs + k*sig_stride. */
+int gvs_sr25519_verify(gvs_handle *h, const uint8_t *pks, const uint8_t *msgs, uint32_t msg_len,
+                       const uint8_t *sigs, uint32_t n, const uint8_t *context,
+                       uint32_t context_len, uint32_t *ok);
+int gvs_sr25519_verify_device(gvs_handle *h, const void *d_pks, uint32_t pk_stride,
+                              const void *d_msgs, uint32_t msg_stride, uint32_t msg_len,
+                              const void *d_sigs, uint32_t sig_stride, uint32_t n,
+                              const uint8_t *context, uint32_t context_len, uint32_t *d_ok);
 
 /* Message expiry (README.md:86-99: the untrusted host supplies the time and
  * the expiry period).  From the next batch on, messages whose timestamp is

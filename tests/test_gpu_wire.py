@@ -161,8 +161,8 @@ def test_wire_batches_end_to_end(host_api):
             d_in, d_lens, d_t = dev(s), dev(lens), dev(times)  # alive across the call
             torch.cuda.synchronize()
             store._check(store.lib.gvs_process_wire_batch_device(
-                store.h, d_in.data_ptr(), 1104, d_lens.data_ptr(), n, d_t.data_ptr(),
-                d_out.data_ptr(), 1042, d_len.data_ptr(), d_sig.data_ptr()))
+                store.h, d_in.data_ptr(), 1104, d_lens.data_ptr(), n, d_t.data_ptr(), None,
+                d_out.data_ptr(), 1042, d_len.data_ptr(), d_sig.data_ptr(), None))
             out = host(d_out, np.uint8, (n, 1042))
             ol = host(d_len, np.uint32, (n,))
             got = [out[k, :ol[k]].tobytes() for k in range(n)]
