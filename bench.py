@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--host-steps", type=int, default=8,
                    help="batches timed through the host API (gvs_process_batches) after the device run")
+    p.add_argument("--wire-steps", type=int, default=3,
+                   help="batches through the device wire path (decode, store, encode); 0 = skip")
     p.add_argument("--routed", action="store_true",
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
@@ -255,6 +257,66 @@ def cpu_baseline(budget_s, threads):
                       f"thread: {c1:.0f} req/s"}
 
 
+def front_end(torch, store, dev, batches, nreq, B):
+    """The steps either side of the store on the device:
+    wire QueryRequests -> decode -> store -> encode -> wire QueryResponses
+    (gvs_process_wire_batch_device, no challenge check, so the store sees the
+    same requests), and the batched schnorrkel check alone over B signatures
+    (gvs_sr25519_verify_device).  The verifier runs the same instruction
+    stream whatever its inputs, so random keys and signatures time it."""
+    import numpy as np
+    from grapevine_amd import abi, wire
+    W_IN = 1104
+    d_wires, d_lens, d_times = [], [], []
+    for b in batches:
+        q = b[:nreq].cpu().numpy().view(abi.REQUEST_DTYPE).reshape(-1).copy()
+        q["request_type"][q["request_type"] == 0] = 0xFFFFFFFF  # still a hard error
+        w = np.zeros((nreq, W_IN), np.uint8)
+        w[:, :wire.REQUEST_WIRE_BYTES] = wire.encode_requests(q)
+        d_wires.append(torch.from_numpy(w).to(dev))
+        d_lens.append(torch.full((nreq,), wire.REQUEST_WIRE_BYTES, dtype=torch.int32, device=dev))
+        d_times.append(torch.from_numpy(q["timestamp"].view(np.int64)).to(dev))
+    d_out = torch.empty((nreq, wire.RESPONSE_WIRE_BYTES), dtype=torch.uint8, device=dev)
+    d_olen = torch.empty((nreq,), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    stage, lens = {}, None
+    t0 = time.perf_counter()
+    for i in range(len(batches)):
+        store._check(store.lib.gvs_process_wire_batch_device(
+            store.h, d_wires[i].data_ptr(), W_IN, d_lens[i].data_ptr(), nreq, d_times[i].data_ptr(),
+            None, d_out.data_ptr(), wire.RESPONSE_WIRE_BYTES, d_olen.data_ptr(), None, None))
+        for k, v in store.last_timings().items():
+            stage[k] = stage.get(k, 0.0) + v
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter() - t0
+    lens = torch.bincount(d_olen.to(torch.int64), minlength=1043)
+    # batched signature check over B random (pk, 32-B challenge, signature)
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    pks = torch.randint(0, 256, (B, 32), dtype=torch.uint8, device=dev, generator=g)
+    msgs = torch.randint(0, 256, (B, 32), dtype=torch.uint8, device=dev, generator=g)
+    sigs = torch.randint(0, 256, (B, 64), dtype=torch.uint8, device=dev, generator=g)
+    ok = torch.empty((B,), dtype=torch.int32, device=dev)
+    ctx = b"grapevine-challenge"
+    torch.cuda.synchronize(dev)
+    ms = []
+    for _ in range(3):
+        store._check(store.lib.gvs_sr25519_verify_device(
+            store.h, pks.data_ptr(), 32, msgs.data_ptr(), 32, 32, sigs.data_ptr(), 64, B, ctx, len(ctx),
+            ok.data_ptr()))
+        ms.append(store.last_timings().get("sr_verify", float("nan")))
+    v_ms = min(ms)
+    return {"wire_batch": {"value": nreq * len(batches) / t, "unit": "req/s",
+                           "ms_per_batch": t / len(batches) * 1e3, "batches": len(batches),
+                           "api": "gvs_process_wire_batch_device (1099-B QueryRequests in 1104-B slots, "
+                                  "1042-B QueryResponses; no challenge check)",
+                           "responses_1042B": int(lens[1042].item()), "responses_empty": int(lens[0].item()),
+                           "stage_ms": {k: v / len(batches) for k, v in stage.items()}},
+            "sr25519_verify": {"value": B / (v_ms * 1e-3), "unit": "signatures/s", "batch": B,
+                               "ms": v_ms, "api": "gvs_sr25519_verify_device (context grapevine-challenge, "
+                                                  "32-B messages; random inputs)"}}
+
+
 def main():
     a = parse()
     # RCCL prints a version banner on stdout at communicator creation; keep
@@ -356,6 +418,11 @@ def main():
                      "one_by_one_ms_per_batch": t_seq / 2 * 1e3,
                      "note": "requests and responses in pageable host memory, PCIe and host copies included"}
 
+    front = None
+    if a.wire_steps and world == 1 and not a.routed:
+        front = front_end(torch, store, dev,
+                          gen_batches(torch, dev, B, a.wire_steps, known, pool, g, 1_900_000_000), nreq, B)
+
     if rank == 0:
         total = world * nreq * a.steps
         rpass_ms = stage_ms.get("rpass", float("nan"))
@@ -432,6 +499,7 @@ def main():
                                "formula": "2*N*1024 + 4*R*1024 + B*(1088 + 1088), per ms_per_step"},
             "cpu_baseline": cpu,
             "host_path": host_path,
+            "front_end": front,
             "checks": checks,
             "stage_ms": stage_ms,
             "store": {"messages": st["messages"], "mailboxes": st["mailboxes"],
