@@ -30,11 +30,14 @@
 namespace gvs {
 namespace sr {
 
+#define GVS_SR_FN __host__ __device__ __forceinline__
+#define GVS_SR_FN_NI __host__ __device__
+
 struct Fe {
   uint32_t v[8];
 };
 
-__device__ __forceinline__ Fe fe_k(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
+GVS_SR_FN Fe fe_k(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
                                    uint32_t a5, uint32_t a6, uint32_t a7) {
   Fe r;
   r.v[0] = a0, r.v[1] = a1, r.v[2] = a2, r.v[3] = a3;
@@ -42,31 +45,31 @@ __device__ __forceinline__ Fe fe_k(uint32_t a0, uint32_t a1, uint32_t a2, uint32
   return r;
 }
 
-__device__ __forceinline__ Fe fe_zero() { return fe_k(0, 0, 0, 0, 0, 0, 0, 0); }
-__device__ __forceinline__ Fe fe_one() { return fe_k(1, 0, 0, 0, 0, 0, 0, 0); }
-__device__ __forceinline__ Fe fe_p() {
+GVS_SR_FN Fe fe_zero() { return fe_k(0, 0, 0, 0, 0, 0, 0, 0); }
+GVS_SR_FN Fe fe_one() { return fe_k(1, 0, 0, 0, 0, 0, 0, 0); }
+GVS_SR_FN Fe fe_p() {
   return fe_k(0xFFFFFFEDu, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, 0x7FFFFFFFu);
 }
 // edwards25519 / ristretto255 constants (oracle/sr25519.py)
-__device__ __forceinline__ Fe fe_d2() {
+GVS_SR_FN Fe fe_d2() {
   return fe_k(0x26b2f159u, 0xebd69b94u, 0x8283b156u, 0x00e0149au, 0xeef3d130u, 0x198e80f2u,
               0x56dffce7u, 0x2406d9dcu);
 }
-__device__ __forceinline__ Fe fe_d() {
+GVS_SR_FN Fe fe_d() {
   return fe_k(0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du, 0x7779e898u, 0x8cc74079u,
               0x2b6ffe73u, 0x52036ceeu);
 }
-__device__ __forceinline__ Fe fe_sqrt_m1() {
+GVS_SR_FN Fe fe_sqrt_m1() {
   return fe_k(0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u, 0x3dfbd7a7u, 0x2b4d0099u,
               0x4fc1df0bu, 0x2b832480u);
 }
-__device__ __forceinline__ Fe fe_invsqrt_a_minus_d() {
+GVS_SR_FN Fe fe_invsqrt_a_minus_d() {
   return fe_k(0x805d40eau, 0x99c8fdaau, 0x5a4172beu, 0x9d2f1617u, 0xfe01d840u, 0x16c27b91u,
               0xcfaffca2u, 0x786c8905u);
 }
 
 // r += 38 * c (c small), carried through; returns the carry out
-__device__ __forceinline__ uint32_t fe_add_small(Fe& r, uint32_t c) {
+GVS_SR_FN uint32_t fe_add_small(Fe& r, uint32_t c) {
   uint64_t x = (uint64_t)r.v[0] + c;
   r.v[0] = (uint32_t)x;
 #pragma unroll
@@ -78,7 +81,7 @@ __device__ __forceinline__ uint32_t fe_add_small(Fe& r, uint32_t c) {
 }
 
 // r -= c (c small), borrowed through; returns the borrow out
-__device__ __forceinline__ uint32_t fe_sub_small(Fe& r, uint32_t c) {
+GVS_SR_FN uint32_t fe_sub_small(Fe& r, uint32_t c) {
   uint64_t x = (uint64_t)r.v[0] - c;
   r.v[0] = (uint32_t)x;
 #pragma unroll
@@ -89,7 +92,7 @@ __device__ __forceinline__ uint32_t fe_sub_small(Fe& r, uint32_t c) {
   return (uint32_t)(x >> 32) & 1u;
 }
 
-__device__ __forceinline__ Fe fe_add(const Fe& a, const Fe& b) {
+GVS_SR_FN Fe fe_add(const Fe& a, const Fe& b) {
   Fe r;
   uint64_t x = 0;
 #pragma unroll
@@ -102,7 +105,7 @@ __device__ __forceinline__ Fe fe_add(const Fe& a, const Fe& b) {
   return r;
 }
 
-__device__ __forceinline__ Fe fe_sub(const Fe& a, const Fe& b) {
+GVS_SR_FN Fe fe_sub(const Fe& a, const Fe& b) {
   Fe r;
   uint64_t x = 0;
 #pragma unroll
@@ -115,9 +118,9 @@ __device__ __forceinline__ Fe fe_sub(const Fe& a, const Fe& b) {
   return r;
 }
 
-__device__ __forceinline__ Fe fe_neg(const Fe& a) { return fe_sub(fe_zero(), a); }
+GVS_SR_FN Fe fe_neg(const Fe& a) { return fe_sub(fe_zero(), a); }
 
-__device__ __forceinline__ Fe fe_mul(const Fe& a, const Fe& b) {
+GVS_SR_FN Fe fe_mul(const Fe& a, const Fe& b) {
   uint32_t t[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = 0;
@@ -145,14 +148,58 @@ __device__ __forceinline__ Fe fe_mul(const Fe& a, const Fe& b) {
   return r;
 }
 
-__device__ __forceinline__ Fe fe_sq(const Fe& a) { return fe_mul(a, a); }
+// a^2: the 28 cross products once, doubled, plus the 8 squares (36 multiply-
+// adds against fe_mul's 64)
+GVS_SR_FN Fe fe_sq(const Fe& a) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      const uint64_t x = (uint64_t)a.v[i] * a.v[j] + t[i + j] + c;
+      t[i + j] = (uint32_t)x;
+      c = x >> 32;
+    }
+    t[i + 8] = (uint32_t)c;
+  }
+  uint32_t top = 0;  // cross terms < 2^511: doubling fits
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t nt = t[k] >> 31;
+    t[k] = (t[k] << 1) | top;
+    top = nt;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t x = (uint64_t)a.v[i] * a.v[i] + t[2 * i] + c;
+    t[2 * i] = (uint32_t)x;
+    const uint64_t y = (uint64_t)t[2 * i + 1] + (x >> 32);
+    t[2 * i + 1] = (uint32_t)y;
+    c = y >> 32;
+  }
+  Fe r;
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t x = (uint64_t)t[8 + i] * 38u + t[i] + c;
+    r.v[i] = (uint32_t)x;
+    c = x >> 32;
+  }
+  const uint32_t c2 = fe_add_small(r, (uint32_t)c * 38u);
+  (void)fe_add_small(r, c2 * 38u);
+  return r;
+}
 
-__device__ __forceinline__ Fe fe_sqn(Fe a, int n) {
+GVS_SR_FN Fe fe_sqn(Fe a, int n) {
   for (int i = 0; i < n; ++i) a = fe_sq(a);
   return a;
 }
 
-__device__ __forceinline__ Fe fe_select(uint32_t m, const Fe& a, const Fe& b) {  // m ? a : b
+GVS_SR_FN Fe fe_select(uint32_t m, const Fe& a, const Fe& b) {  // m ? a : b
   Fe r;
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = (a.v[i] & m) | (b.v[i] & ~m);
@@ -160,7 +207,7 @@ __device__ __forceinline__ Fe fe_select(uint32_t m, const Fe& a, const Fe& b) { 
 }
 
 // the representative in [0, p): x < 2^256 = 2p + 38, so p goes at most twice
-__device__ __forceinline__ Fe fe_canon(Fe x) {
+GVS_SR_FN Fe fe_canon(Fe x) {
   const Fe p = fe_p();
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -177,7 +224,7 @@ __device__ __forceinline__ Fe fe_canon(Fe x) {
   return x;
 }
 
-__device__ __forceinline__ uint32_t fe_mask_eq(const Fe& a, const Fe& b) {  // all ones if a == b (mod p)
+GVS_SR_FN uint32_t fe_mask_eq(const Fe& a, const Fe& b) {  // all ones if a == b (mod p)
   const Fe x = fe_canon(a), y = fe_canon(b);
   uint32_t d = 0;
 #pragma unroll
@@ -185,14 +232,14 @@ __device__ __forceinline__ uint32_t fe_mask_eq(const Fe& a, const Fe& b) {  // a
   return 0u - (uint32_t)(d == 0);
 }
 
-__device__ __forceinline__ uint32_t fe_mask_neg(const Fe& a) {  // IS_NEGATIVE: canonical value odd
+GVS_SR_FN uint32_t fe_mask_neg(const Fe& a) {  // IS_NEGATIVE: canonical value odd
   return 0u - (fe_canon(a).v[0] & 1u);
 }
 
-__device__ __forceinline__ Fe fe_abs(const Fe& a) { return fe_select(fe_mask_neg(a), fe_neg(a), a); }
+GVS_SR_FN Fe fe_abs(const Fe& a) { return fe_select(fe_mask_neg(a), fe_neg(a), a); }
 
 // z^((p-5)/8) = z^(2^252 - 3)
-__device__ Fe fe_pow22523(const Fe& z) {
+GVS_SR_FN_NI Fe fe_pow22523(const Fe& z) {
   Fe t0 = fe_sq(z);                       // 2
   Fe t1 = fe_sqn(t0, 2);                  // 8
   t1 = fe_mul(z, t1);                     // 9
@@ -218,7 +265,7 @@ __device__ Fe fe_pow22523(const Fe& z) {
 }
 
 // RFC 9496 §4.2 SQRT_RATIO_M1(u, v) -> r; *was_square all ones or zero
-__device__ Fe fe_sqrt_ratio_m1(const Fe& u, const Fe& v, uint32_t* was_square) {
+GVS_SR_FN_NI Fe fe_sqrt_ratio_m1(const Fe& u, const Fe& v, uint32_t* was_square) {
   const Fe v3 = fe_mul(fe_sq(v), v);
   const Fe v7 = fe_mul(fe_sq(v3), v);
   Fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
@@ -236,9 +283,9 @@ struct Pt {
   Fe X, Y, Z, T;
 };
 
-__device__ __forceinline__ Pt pt_identity() { return Pt{fe_zero(), fe_one(), fe_one(), fe_zero()}; }
+GVS_SR_FN Pt pt_identity() { return Pt{fe_zero(), fe_one(), fe_one(), fe_zero()}; }
 
-__device__ __forceinline__ Pt pt_base() {
+GVS_SR_FN Pt pt_base() {
   return Pt{fe_k(0x8f25d51au, 0xc9562d60u, 0x9525a7b2u, 0x692cc760u, 0xfdd6dc5cu, 0xc0a4e231u,
                  0xcd6e53feu, 0x216936d3u),
             fe_k(0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u,
@@ -249,7 +296,7 @@ __device__ __forceinline__ Pt pt_base() {
 }
 
 // extended coordinates, a = -1: add-2008-hwcd-3 (complete on edwards25519)
-__device__ __forceinline__ Pt pt_add(const Pt& p, const Pt& q) {
+GVS_SR_FN Pt pt_add(const Pt& p, const Pt& q) {
   const Fe a = fe_mul(fe_sub(p.Y, p.X), fe_sub(q.Y, q.X));
   const Fe b = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));
   const Fe c = fe_mul(fe_mul(p.T, fe_d2()), q.T);
@@ -260,7 +307,7 @@ __device__ __forceinline__ Pt pt_add(const Pt& p, const Pt& q) {
 }
 
 // dbl-2008-hwcd, a = -1
-__device__ __forceinline__ Pt pt_dbl(const Pt& p) {
+GVS_SR_FN Pt pt_dbl(const Pt& p) {
   const Fe a = fe_sq(p.X), b = fe_sq(p.Y);
   const Fe zz = fe_sq(p.Z);
   const Fe c = fe_add(zz, zz);
@@ -270,15 +317,15 @@ __device__ __forceinline__ Pt pt_dbl(const Pt& p) {
   return Pt{fe_mul(e, f), fe_mul(g, h), fe_mul(f, g), fe_mul(e, h)};
 }
 
-__device__ __forceinline__ Pt pt_neg(const Pt& p) { return Pt{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
+GVS_SR_FN Pt pt_neg(const Pt& p) { return Pt{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
 
-__device__ __forceinline__ Pt pt_select(uint32_t m, const Pt& a, const Pt& b) {
+GVS_SR_FN Pt pt_select(uint32_t m, const Pt& a, const Pt& b) {
   return Pt{fe_select(m, a.X, b.X), fe_select(m, a.Y, b.Y), fe_select(m, a.Z, b.Z),
             fe_select(m, a.T, b.T)};
 }
 
 // RFC 9496 §4.3.1; *ok all ones when s is a canonical encoding of a point
-__device__ Pt ristretto_decode(const Fe& s, uint32_t* ok) {
+GVS_SR_FN_NI Pt ristretto_decode(const Fe& s, uint32_t* ok) {
   const Fe p = fe_p();
   uint64_t t = 0;  // s < p
 #pragma unroll
@@ -303,7 +350,7 @@ __device__ Pt ristretto_decode(const Fe& s, uint32_t* ok) {
 }
 
 // RFC 9496 §4.3.2 -> canonical s
-__device__ Fe ristretto_encode(const Pt& q) {
+GVS_SR_FN_NI Fe ristretto_encode(const Pt& q) {
   const Fe u1 = fe_mul(fe_add(q.Z, q.Y), fe_sub(q.Z, q.Y));
   const Fe u2 = fe_mul(q.X, q.Y);
   uint32_t ws;
@@ -322,12 +369,12 @@ __device__ Fe ristretto_encode(const Pt& q) {
 
 // ---------------------------------------------------------------- scalars
 
-__device__ __forceinline__ Fe sc_l() {
+GVS_SR_FN Fe sc_l() {
   return fe_k(0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0, 0, 0, 0x10000000u);
 }
 
 // all ones if s < l
-__device__ __forceinline__ uint32_t sc_mask_lt_l(const Fe& s) {
+GVS_SR_FN uint32_t sc_mask_lt_l(const Fe& s) {
   const Fe l = sc_l();
   uint64_t t = 0;
 #pragma unroll
@@ -336,7 +383,7 @@ __device__ __forceinline__ uint32_t sc_mask_lt_l(const Fe& s) {
 }
 
 // a 512-bit little-endian integer mod l, one bit at a time (fixed 512 steps)
-__device__ Fe sc_reduce_wide(const uint32_t w[16]) {
+GVS_SR_FN_NI Fe sc_reduce_wide(const uint32_t w[16]) {
   const Fe l = sc_l();
   Fe r = fe_zero();
 #pragma unroll
@@ -363,7 +410,7 @@ __device__ Fe sc_reduce_wide(const uint32_t w[16]) {
   return r;
 }
 
-__device__ __forceinline__ void shl1(Fe& x) {
+GVS_SR_FN void shl1(Fe& x) {
 #pragma unroll
   for (int i = 7; i > 0; --i) x.v[i] = (x.v[i] << 1) | (x.v[i - 1] >> 31);
   x.v[0] <<= 1;
@@ -491,7 +538,7 @@ struct SrArgs {
 
 constexpr uint32_t kWireBadSignature = 3;
 
-__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+GVS_SR_FN uint32_t ld_le32(const uint8_t* p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
