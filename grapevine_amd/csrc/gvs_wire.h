@@ -21,7 +21,8 @@
 //   * a length or fixed field running past its message (or past the
 //     embedded record's end) is an error.
 //   [D] Groups (wire types 3/4) are rejected; prost would skip an unknown
-//   group.  No grapevine client emits them.
+//   group.  No grapevine client emits them.  [D] So is a message that needs
+//   more than kWireSteps field steps (fixed-work decoding, below).
 // A message that fails to decode, or whose fields do not have the sizes the
 // handler requires (auth_identity 32, auth_signature 64, msg_id 16,
 // recipient 32, payload 936), becomes a request of type 0: the store answers
@@ -57,27 +58,36 @@ struct WireDecArgs {
 };
 
 // A field walk over the wave's LDS copy.  All lanes run it on the same bytes,
-// so every value below is wave-uniform.
-struct WireWalk {
-  const uint8_t* m;
-  int err;
+// so every value below is wave-uniform.  The walk takes exactly kWireSteps
+// steps whatever the message holds (a step parses one field, leaves an
+// embedded record, or idles once the message is done), and each step reads a
+// fixed number of bytes with selects, so a batch's decode time does not depend
+// on its messages.  [D] A message that needs more steps (fields + embedded
+// records + 1) is a decode error; prost has no such bound (a canonical
+// request needs 9).
+constexpr int kWireSteps = 32;
 
-  // prost decode_varint: at most 10 bytes, the 10th at most 1
-  __device__ uint64_t varint(uint32_t& p, uint32_t lim) {
-    uint64_t v = 0;
-    for (int c = 0; c < 10; ++c) {
-      if (p >= lim) break;
-      const uint32_t b = m[p++];
-      v |= (uint64_t)(b & 0x7Fu) << (7 * c);
-      if (b < 0x80u) {
-        if (c == 9 && b > 1u) err = 1;
-        return v;
-      }
-    }
-    err = 1;
-    return 0;
-  }
+struct Varint {
+  uint64_t v;
+  uint32_t next;  // position after the varint
+  bool ok;        // prost decode_varint accepts it (at most 10 bytes, the 10th <= 1, inside lim)
 };
+
+__device__ inline Varint varint_at(const uint8_t* m, uint32_t p, uint32_t lim) {
+  Varint r{0, p, false};
+  bool done = false;
+#pragma unroll
+  for (uint32_t c = 0; c < 10; ++c) {
+    const uint32_t b = m[min(p + c, kWireSlotMax - 1u)];
+    const bool take = !done && p + c < lim;
+    r.v |= take ? (uint64_t)(b & 0x7Fu) << (7 * c) : 0ull;
+    const bool last = take && b < 0x80u;
+    r.ok = last ? !(c == 9 && b > 1u) : r.ok;
+    r.next = last ? p + c + 1 : r.next;
+    done = done || last || !take;
+  }
+  return r;
+}
 
 __global__ void __launch_bounds__(256) k_wire_decode(WireDecArgs a) {
   __shared__ uint8_t stage[4][kWireSlotMax];
@@ -92,76 +102,61 @@ __global__ void __launch_bounds__(256) k_wire_decode(WireDecArgs a) {
   if (!live) return;
 
   uint32_t len = a.lens[k];
-  WireWalk w{m, 0};
-  if (len > a.stride) {
-    w.err = 1;
-    len = 0;
-  }
+  bool err = len > a.stride;
+  len = err ? 0u : len;
   // last offset and length of each field (length kNone: absent)
   uint32_t rt = 0;
   uint32_t o_auth = 0, l_auth = kNone, o_sig = 0, l_sig = kNone;
   uint32_t o_id = 0, l_id = kNone, o_rc = 0, l_rc = kNone, o_pl = 0, l_pl = kNone;
   uint32_t p = 0, depth = 0, nend = 0;
-  while (!w.err) {
+  bool done = false;
+  for (int step = 0; step < kWireSteps; ++step) {
+    const bool idle = done || err;
     const uint32_t lim = depth ? nend : len;
-    if (p == lim) {
-      if (!depth) break;
-      depth = 0;  // end of an embedded record: back to the request
-      continue;
-    }
-    const uint64_t key = w.varint(p, lim);
-    const uint32_t wt = (uint32_t)(key & 7u);
-    const uint64_t tag = key >> 3;
-    if (w.err || key > 0xFFFFFFFFull || tag == 0 || wt == 3 || wt == 4 || wt > 5) {
-      w.err = 1;
-      break;
-    }
+    const bool at_end = p == lim;
+    const bool pop = !idle && at_end && depth;
+    done = done || (!idle && at_end && !depth);
+    const bool field = !idle && !at_end;
+    // the key, then the varint / fixed / length that follows it (all read)
+    const Varint kv = varint_at(m, p, lim);
+    const uint32_t wt = (uint32_t)(kv.v & 7u);
+    const uint64_t tag = kv.v >> 3;
+    const Varint vv = varint_at(m, kv.next, lim);
+    const uint32_t q = min(kv.next, kWireSlotMax - 4u);
+    const uint32_t fx = (uint32_t)m[q] | (uint32_t)m[q + 1] << 8 | (uint32_t)m[q + 2] << 16 |
+                        (uint32_t)m[q + 3] << 24;
     const bool known = depth ? (tag >= 1 && tag <= 3) : (tag >= 1 && tag <= 4);
     const uint32_t want = (!depth && tag == 1) ? 5u : 2u;
-    if (known && wt != want) {
-      w.err = 1;
-      break;
-    }
-    if (wt == 0) {
-      (void)w.varint(p, lim);
-    } else if (wt == 1 || wt == 5) {
-      const uint32_t sz = wt == 1 ? 8u : 4u;
-      if (lim - p < sz) {
-        w.err = 1;
-        break;
-      }
-      if (known)  // request_type (the only known fixed field)
-        rt = (uint32_t)m[p] | (uint32_t)m[p + 1] << 8 | (uint32_t)m[p + 2] << 16 |
-             (uint32_t)m[p + 3] << 24;
-      p += sz;
-    } else {  // length-delimited
-      const uint64_t l = w.varint(p, lim);
-      if (w.err || l > lim - p) {
-        w.err = 1;
-        break;
-      }
-      const uint32_t L = (uint32_t)l;
-      if (known && !depth && tag == 4) {  // RequestRecord: merge its fields
-        depth = 1;
-        nend = p + L;
-        continue;
-      }
-      if (known) {
-        if (!depth) {
-          if (tag == 2) o_auth = p, l_auth = L;
-          else o_sig = p, l_sig = L;
-        } else {
-          if (tag == 1) o_id = p, l_id = L;
-          else if (tag == 2) o_rc = p, l_rc = L;
-          else o_pl = p, l_pl = L;
-        }
-      }
-      p += L;
-    }
+    const uint32_t sz = wt == 1 ? 8u : 4u;
+    bool bad = !kv.ok || kv.v > 0xFFFFFFFFull || tag == 0 || wt == 3 || wt == 4 || wt > 5 ||
+               (known && wt != want);
+    bad = bad || (wt == 0 && !vv.ok) || ((wt == 1 || wt == 5) && lim - kv.next < sz) ||
+          (wt == 2 && (!vv.ok || vv.v > lim - vv.next));
+    err = err || (field && bad);
+    const bool apply = field && !bad;
+    const uint32_t L = (uint32_t)vv.v, body = vv.next;
+    const bool rec = apply && known && !depth && tag == 4;  // RequestRecord: merge its fields
+    const bool ldk = apply && known && wt == 2 && !rec;
+    rt = (apply && known && wt == 5) ? fx : rt;
+    o_auth = (ldk && !depth && tag == 2) ? body : o_auth;
+    l_auth = (ldk && !depth && tag == 2) ? L : l_auth;
+    o_sig = (ldk && !depth && tag == 3) ? body : o_sig;
+    l_sig = (ldk && !depth && tag == 3) ? L : l_sig;
+    o_id = (ldk && depth && tag == 1) ? body : o_id;
+    l_id = (ldk && depth && tag == 1) ? L : l_id;
+    o_rc = (ldk && depth && tag == 2) ? body : o_rc;
+    l_rc = (ldk && depth && tag == 2) ? L : l_rc;
+    o_pl = (ldk && depth && tag == 3) ? body : o_pl;
+    l_pl = (ldk && depth && tag == 3) ? L : l_pl;
+    const uint32_t np = wt == 0 ? vv.next : (wt == 2 ? body + L : kv.next + sz);
+    p = apply ? (rec ? body : np) : p;
+    nend = rec ? body + L : nend;
+    depth = rec ? 1u : (pop ? 0u : depth);
   }
+  err = err || !done;
   const bool sizes = l_auth == 32u && l_sig == 64u && l_id == 16u && l_rc == 32u &&
                      l_pl == kWirePayload;
-  const uint32_t st = w.err ? kWireDecodeError : (sizes ? kWireOk : kWireBadField);
+  const uint32_t st = err ? kWireDecodeError : (sizes ? kWireOk : kWireBadField);
   const bool ok = st == kWireOk;
   if (!ok) o_id = o_auth = o_rc = o_pl = o_sig = 0;  // keep the reads inside the stage
   const uint64_t ts = a.times[k];

@@ -114,13 +114,18 @@ def _varint(b, i, end):
     raise DecodeError("invalid varint")
 
 
-def _walk(b, i, end, spec, out, nested=None):
+WIRE_STEPS = 32  # gvs_wire.h kWireSteps: fields + embedded records + 1 per request
+
+
+def _walk(b, i, end, spec, out, nested=None, steps=None):
     """Decode fields in b[i:end) the way prost's generated merge does: a known
     field must carry its wire type, unknown fields are skipped, the last
     occurrence of a scalar / bytes field wins, and an embedded message named in
     `nested` ({field: (spec, dict)}) is merged over all its occurrences.
     [D] Groups (wire types 3/4) are rejected (prost would skip unknown ones)."""
     while i < end:
+        if steps is not None:
+            steps[0] += 1
         key, i = _varint(b, i, end)
         if key > 0xFFFFFFFF:
             raise DecodeError("invalid key value")
@@ -144,7 +149,9 @@ def _walk(b, i, end, spec, out, nested=None):
                 raise DecodeError("buffer underflow")
             if f in spec:
                 if nested and f in nested:
-                    _walk(b, i, i + ln, nested[f][0], nested[f][1])
+                    _walk(b, i, i + ln, nested[f][0], nested[f][1], steps=steps)
+                    if steps is not None:
+                        steps[0] += 1  # leaving the embedded message
                 else:
                     out[f] = bytes(b[i:i + ln])
             i += ln
@@ -160,9 +167,13 @@ def _fixed(v, size, name):
 
 def decode_request(m):
     """One wire QueryRequest -> (fields, record fields) with prost semantics;
-    raises DecodeError."""
+    raises DecodeError.  [D] Like the device decoder, a request needing more
+    than WIRE_STEPS steps (fields + embedded records + 1) is refused."""
     f, rec = {}, {}
-    _walk(bytes(m), 0, len(m), _REQ_SPEC, f, {4: (_REQREC_SPEC, rec)})
+    steps = [1]
+    _walk(bytes(m), 0, len(m), _REQ_SPEC, f, {4: (_REQREC_SPEC, rec)}, steps=steps)
+    if steps[0] > WIRE_STEPS:
+        raise DecodeError(f"{steps[0]} decode steps, more than {WIRE_STEPS}")
     return f, rec
 
 

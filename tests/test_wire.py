@@ -134,6 +134,7 @@ def test_prost_rules_match_google_protobuf_on_valid_variants():
     codec's prost rules and under google.protobuf."""
     cases = all_variants(7, 6)
     good = [(n, m) for n, m in cases if not n.startswith("bad_")]
+    assert any(n == "step_cap_exact" for n, _ in good)
     q, sig, st = wire.decode_requests([m for _, m in good], timestamps=5, strict=False)
     for k, (name, m) in enumerate(good):
         ref = QueryRequest.FromString(m)

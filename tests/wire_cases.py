@@ -90,6 +90,8 @@ def variants(rng):
         ("type_zero_explicit", canonical(dict(f, rt=0))),
         ("type_out_of_range", canonical(dict(f, rt=rng.choice((5, 9, 0xFFFFFFFF))))),
         ("type_absent", ld(2, f["auth"]) + ld(3, f["sig"]) + ld(4, rec)),
+        # 9 steps for the canonical fields + 23 one-step unknown fields: exactly the step cap
+        ("step_cap_exact", canonical(f) + (key(9, 0) + varint(1)) * 23),
         ("empty_record_then_full", fx32(1, f["rt"]) + ld(2, f["auth"]) + ld(3, f["sig"]) + ld(4, b"") +
          ld(4, rec) + ld(4, b"")),
         # malformed: prost returns DecodeError
@@ -110,6 +112,7 @@ def variants(rng):
         ("bad_varint_11_bytes", canonical(f) + key(9, 0) + b"\xff" * 10 + b"\x01"),
         ("bad_varint_10th_byte", canonical(f) + key(9, 0) + b"\xff" * 9 + b"\x02"),
         ("bad_key_above_u32", canonical(f) + varint((1 << 32) | 0) + varint(1)),
+        ("bad_over_step_cap", canonical(f) + (key(9, 0) + varint(1)) * 24),  # [D] prost has no cap
         ("bad_fixed_past_end", canonical(f) + key(10, 1) + b"\x01\x02\x03"),
         # decodes, but a field has the wrong size: a hard error for the handler
         ("bad_auth_short", canonical(dict(f, auth=f["auth"][:31]))),
