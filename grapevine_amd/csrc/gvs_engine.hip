@@ -324,6 +324,28 @@ static uint32_t txn_slots(uint32_t B, uint32_t W, uint32_t S) {
   return (uint32_t)c;
 }
 
+// The X expiry deletes of one batch are by-id deletes of X recorded messages;
+// each distinct recipient among them takes one group slot of its mailbox
+// partition.  Their load per partition must fit the partition's group slots
+// on its own, by the same binomial bound the slots are sized with (recipients
+// are spread by the keyed PRF): otherwise a batch could overflow on its expiry
+// deletes alone, and since a failed batch keeps its records for the next one,
+// every later batch (even an empty one) would fail the same way.  This rules
+// out configurations whose group slots are capped (kGroupMax) below the
+// deletes' own bound, e.g. few mailbox partitions and a large X.
+static bool expiry_fits(const gvs_config* c, bool sharded) {
+  if (!c->expiry_per_batch) return true;
+  uint32_t Be = c->max_batch;
+  if (sharded) {
+    const uint32_t S = c->shard_count ? c->shard_count : 1;
+    const uint32_t C = c->route_capacity ? c->route_capacity : auto_capacity(c->max_batch, S);
+    Be = shard_batch((uint64_t)S * C + c->expiry_per_batch);
+    if (!Be) return false;
+  }
+  const uint32_t need = txn_slots(c->expiry_per_batch, c->mailbox_partitions, ~0u);
+  return need <= txn_slots(Be, c->mailbox_partitions, kGroupMax);
+}
+
 // ------------------------------------------------- authenticated storage (host)
 
 static uint8_t gf_mul(uint8_t a, uint8_t b) {
@@ -586,6 +608,7 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
   if (!out) return GVS_ERR_INVALID_ARG;
   *out = nullptr;
   if (int rc = validate(cfg)) return rc;
+  if (!expiry_fits(cfg, mode != kSingle)) return GVS_ERR_INVALID_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GVS_ERR_NO_DEVICE;
   if ((int)cfg->device >= ndev) return GVS_ERR_INVALID_ARG;

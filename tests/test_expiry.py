@@ -123,6 +123,14 @@ def test_update_after_sweep_keeps_message():
     assert updated <= alive                 # every refreshed message survived
     assert gone and not (gone & updated)    # only unrefreshed ones were deleted
     assert len(gone) <= 128
+    # exactly the swept ones: the first 8 live rows of each of the 16
+    # partitions (slot s lives in partition s mod 16 at offset s div 16; the
+    # dump is in slot order), minus the refreshed ones
+    swept = set()
+    for w in range(16):
+        part = recs[w::16]
+        swept |= {bytes(r["msg_id"]) for r in part[part["msg_id"].any(axis=1)][:8]}
+    assert len(swept) == 128 and gone == swept - updated
 
 
 def test_rotating_workgroups_when_X_below_W():
@@ -245,3 +253,26 @@ def test_gpu_sharded_expiry_parity(S, B, X):
     dt = diff_tables(store.dump_messages(), cl.dump_messages())
     assert not dt, "\n".join(dt)
     assert expired > 0
+
+
+def test_expiry_deletes_must_fit_group_slots():
+    """with few mailbox partitions the group slots are capped
+    (kGroupMax), and X expiry deletes could overflow a partition on their own;
+    every later batch would then fail with its records.  gvs_create refuses
+    such a configuration before touching the device."""
+    import ctypes
+    from grapevine_amd.store import load_library
+    lib = load_library()
+    ok_codes = (abi.GVS_OK, abi.GVS_ERR_NO_DEVICE)
+
+    def create(**kw):
+        cfg = abi.make_config(8192, mailbox_partition_slots=256, max_batch=4096, **kw)
+        h = ctypes.c_void_p()
+        rc = lib.gvs_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc == 0:
+            lib.gvs_destroy(h)
+        return rc
+
+    assert create(mailbox_partitions=2, expiry_per_batch=1024) == abi.GVS_ERR_INVALID_ARG
+    assert create(mailbox_partitions=2, expiry_per_batch=256) in ok_codes
+    assert create(mailbox_partitions=2, expiry_per_batch=0) in ok_codes
