@@ -9,18 +9,23 @@
 //   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
 //                       (standard CTR, counter in the last two bytes)
 //   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
-//   L_i  = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table),
-//                      ct[256i, 256i+256))                       i = 0..3
+//   L_i  = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table & 1),
+//                      leaf i of ct)
+//          message tables (table & 1 = 0: tables 0, 2 and 0x100): 8 leaves
+//          of 128 B; mailbox table (1): 4 leaves of 256 B
 //   H    = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
 //                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
-//   tag  = H ^ L_0 ^ L_1 ^ L_2 ^ L_3
+//   tag  = H ^ L_0 ^ .. ^ L_(n-1)
 // An XOR-MAC with a counter term (Bellare-Guerin-Rogaway's XMACC): H is the
 // PRF of a value that is never sealed twice, (row, e, table), and the L_i are
 // PRFs of index-separated blocks.  The tag binds row, table and epoch, so a
 // replayed, moved or spliced row fails.  The key block of each keyed hash
 // depends only on (key, person): its state is computed once (SealCtx), so a
-// leaf costs two compressions and the header one; the header depends on no
-// row data, so the message pass computes it for 64 rows at a time.
+// 128-B leaf costs one compression, a 256-B leaf two and the header one; the
+// header depends on no row data, so the message pass computes it for 64 rows
+// at a time.  Message rows use 128-B leaves so that a wave of 8 rows hashes
+// its 64 leaves in 64 lanes (the message pass runs 8 rows per wave, 2 waves
+// per SIMD, gvs_txn.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -245,8 +250,19 @@ __host__ __device__ inline B2State b2_keyed_state(const uint8_t key[32], uint64_
   return s;
 }
 
+// L_i over one 128-byte leaf (m = its 16 little-endian words), from the
+// keyed state of leaf i (message tables)
+__host__ __device__ __attribute__((always_inline)) inline void leaf_prf128(const B2State& k,
+                                                                          const uint64_t m[16],
+                                                                          uint64_t out[2]) {
+  B2State s = k;
+  b2_compress(s, m, 128 + 128, true);
+  out[0] = s.h[0];
+  out[1] = s.h[1];
+}
+
 // L_i over one 256-byte leaf (m = its 32 little-endian words), from the
-// keyed state of leaf i
+// keyed state of leaf i (mailbox table)
 __host__ __device__ __attribute__((always_inline)) inline void leaf_prf(const B2State& k,
                                                                        const uint64_t m[32],
                                                                        uint64_t out[2]) {
@@ -283,7 +299,8 @@ __host__ __device__ __attribute__((always_inline)) inline void header_prf(
 // Everything a sealing kernel needs, passed by value.
 struct SealCtx {
   AesRk rk;
-  B2State leafk[2][4];  // keyed states after the key block: [table][leaf]
+  B2State leafk0[8];    // keyed states after the key block: message-table leaves (128 B)
+  B2State leafk1[4];    // mailbox-table leaves (256 B)
   B2State headk;        // keyed state of the header PRF
   uint32_t epoch;       // rows are read at `epoch`, written at `epoch + 1`
   uint32_t on;          // authenticated-storage mode enabled

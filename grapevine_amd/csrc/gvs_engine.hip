@@ -214,6 +214,7 @@ struct gvs_handle {
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
+  int sealed_nw = 8;         // waves per workgroup of the sealed message pass (4 or 8; option)
   HostPipe pipe;
   WireStage wire;
   std::vector<void*> allocs;
@@ -428,9 +429,10 @@ static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256]
   b2_keyed_short(secret, "gvs storage aes", 16, ak);
   b2_keyed_short(secret, "gvs storage mac", 32, mk);
   aes_expand(sb, ak, sc.rk);
-  for (uint32_t t = 0; t < 2; ++t)
-    for (uint32_t i = 0; i < 4; ++i)
-      sc.leafk[t][i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i | ((uint64_t)t << 32));
+  for (uint32_t i = 0; i < 8; ++i)  // message tables: 8 leaves of 128 B
+    sc.leafk0[i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i);
+  for (uint32_t i = 0; i < 4; ++i)  // mailbox table: 4 leaves of 256 B
+    sc.leafk1[i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i | (1ull << 32));
   sc.headk = b2_keyed_state(mk, kHeadPerson0, 0);
   sc.epoch = 0;
   sc.on = 1;
@@ -910,7 +912,10 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     if (e.stamp_prev != kNone)
       hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
     mark(h, "punseal");
-    hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
+    if (h->sealed_nw == 8 && e.S % 512 == 0)  // two waves per SIMD (gvs_txn.h)
+      hipLaunchKernelGGL((k_rpass2<8, true, true, 1, true, 8>), dim3(e.W), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
   }
@@ -1904,6 +1909,10 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
+  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 4 || value == 8)) {
+    h->sealed_nw = (int)value;
+    return GVS_OK;
+  }
   return GVS_ERR_INVALID_ARG;
 }
 
@@ -1946,10 +1955,14 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
   }
   uint64_t t[2];
   header_prf(sc.headk, row, epoch, table, sd, t);
-  for (uint32_t i = 0; i < 4; ++i) {
+  const uint32_t nl = (table & 1) ? 4 : 8, lb = 1024 / nl;  // leaves, bytes per leaf
+  for (uint32_t i = 0; i < nl; ++i) {
     uint64_t m[32], l[2];
-    for (int k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
-    leaf_prf(sc.leafk[table & 1][i], m, l);
+    for (uint32_t k = 0; k < lb / 8; ++k) m[k] = ld64(ct + lb * i + 8 * k);
+    if (table & 1)
+      leaf_prf(sc.leafk1[i], m, l);
+    else
+      leaf_prf128(sc.leafk0[i], m, l);
     t[0] ^= l[0];
     t[1] ^= l[1];
   }

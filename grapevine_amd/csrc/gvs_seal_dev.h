@@ -189,69 +189,117 @@ __device__ inline B2State b2_sel(bool c, const B2State& a, const B2State& b) {
   return r;
 }
 
-// Tag of row row0 + ur, ur = (lane >> 2) % U, over the ciphertext rows
-// already in the stage: tag = H ^ L_0 ^ .. ^ L_3 (gvs_crypto.h).  Lane L
-// computes leaf L & 3 of row ur; the quad XORs its four leaves by shuffles.
-//  * U <= 8 (mailbox passes, side entries staged at st[U*4*kSegU4 + u]):
-//    lanes 32 + u compute H of row u in the same instructions (their first
-//    compression takes the header block instead of leaf data), so the header
-//    costs no extra time.  Valid in lanes < 4U.
-//  * U = 16 (message pass): every lane hashes a leaf; `hdr` is H of the
-//    lane's row, computed by the caller (for 64 rows at once).
-template <int U>
+// Tag of row row0 + (lane >> 2) % U, over the ciphertext rows already in the
+// stage: tag = H ^ L_0 ^ .. ^ L_(NL-1) (gvs_crypto.h).
+//  * NL = 4 (mailbox rows, 256-B leaves): lane L computes leaf L & 3 of row
+//    (L >> 2) % U; the quad XORs its four leaves by shuffles.
+//    - U <= 8 (side entries staged at st[U*4*kSegU4 + u]): lanes 32 + u
+//      compute H of row u in the same instructions (their first compression
+//      takes the header block instead of leaf data), so the header costs no
+//      extra time.  htab: the header's table field in this lane's header row.
+//    - U = 16: every lane hashes a leaf; `hdr` is H of the lane's row.
+//  * NL = 8 (message tables, 128-B leaves, one compression each): lane L
+//    computes leaf L & 7 of row L >> 3 (U = 8), or of rows L >> 3 and
+//    (L >> 3) + 8 (U = 16); the 8 lanes of a row XOR their leaves, and every
+//    lane then takes its row's sum.  `hdr` is H of the lane's row (the
+//    message pass computes it for 64 rows at once).
+// Valid in lanes < 4U.
+template <int U, int NL = 4>
 __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0, uint32_t epoch,
                                  bool with_side, const uint4* st, const uint64_t* hdr,
-                                 uint64_t out[2]) {
-  constexpr bool kInlineHdr = U <= 8;
+                                 uint64_t out[2], uint32_t htab) {
   const uint32_t lane = lane_id();
-  const uint32_t ur = (lane >> 2) % (uint32_t)U, leaf = lane & 3;
-  uint64_t m[32];
-  const uint4* seg = st + (ur * 4 + leaf) * kSegU4;
+  if constexpr (NL == 8) {
+    static_assert(U == 8 || U == 16, "8 or 16 rows of 8 leaves");
+    const uint32_t leaf = lane & 7;
+    B2State k = c.leafk0[0];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint4 x = seg[k];
-    m[2 * k] = u4lo(x);
-    m[2 * k + 1] = u4hi(x);
-  }
-  uint64_t res[2];
-  if (kInlineHdr) {
-    const bool hl = lane >= 32;
-    const uint32_t hrow = (lane - 32) % (uint32_t)U;
-    uint64_t sd[2] = {0, 0};
-    if (with_side) {
-      const uint4 x = st[U * 4 * kSegU4 + hrow];
-      sd[0] = u4lo(x);
-      sd[1] = u4hi(x);
+    for (uint32_t i = 1; i < 8; ++i) k = b2_sel(leaf == i, c.leafk0[i], k);
+    uint64_t acc[U / 8][2];
+#pragma unroll
+    for (int set = 0; set < U / 8; ++set) {
+      const uint32_t ur = (lane >> 3) + 8u * (uint32_t)set;
+      const uint4* seg = st + (ur * 4 + (leaf >> 1)) * kSegU4 + (leaf & 1) * 8;
+      uint64_t m[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 x = seg[q];
+        m[2 * q] = u4lo(x);
+        m[2 * q + 1] = u4hi(x);
+      }
+      uint64_t r[2];
+      leaf_prf128(k, m, r);
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        r[w] ^= shfl_u64(r[w], (int)(lane ^ 1u));
+        r[w] ^= shfl_u64(r[w], (int)(lane ^ 2u));
+        r[w] ^= shfl_u64(r[w], (int)(lane ^ 4u));
+        acc[set][w] = r[w];
+      }
     }
-    uint64_t hb[16];
-    header_block(row0 + hrow, epoch, table, sd, hb);
+    const uint32_t row = (lane >> 2) % (uint32_t)U;
+    const int src = (int)(8u * (row & 7u));
 #pragma unroll
-    for (int k = 0; k < 16; ++k) hb[k] = hl ? hb[k] : m[k];
-    B2State s = b2_sel(hl, c.headk, c.leafk[table & 1][0]);
-#pragma unroll
-    for (uint32_t i = 1; i < 4; ++i) s = b2_sel(!hl && leaf == i, c.leafk[table & 1][i], s);
-    b2_compress(s, hb, hl ? 128 + 32 : 128 + 128, hl);
-    const uint64_t h0 = s.h[0], h1 = s.h[1];
-    b2_compress(s, m + 16, 128 + 256, true);
-    res[0] = hl ? h0 : s.h[0];
-    res[1] = hl ? h1 : s.h[1];
+    for (int w = 0; w < 2; ++w) {
+      // both shuffles in every lane (a shuffle under a divergent branch would
+      // read lanes that are switched off), then a per-lane select
+      const uint64_t lo = shfl_u64(acc[0][w], src);
+      const uint64_t hi = shfl_u64(acc[U / 8 - 1][w], src);
+      out[w] = (U == 16 && row >= 8 ? hi : lo) ^ hdr[w];
+    }
+    (void)table, (void)row0, (void)epoch, (void)with_side, (void)htab;
+    return;
   } else {
-    B2State s = c.leafk[table & 1][0];
+    constexpr bool kInlineHdr = U <= 8;
+    const uint32_t ur = (lane >> 2) % (uint32_t)U, leaf = lane & 3;
+    uint64_t m[32];
+    const uint4* seg = st + (ur * 4 + leaf) * kSegU4;
 #pragma unroll
-    for (uint32_t i = 1; i < 4; ++i) s = b2_sel(leaf == i, c.leafk[table & 1][i], s);
-    leaf_prf(s, m, res);
-  }
-  // H of the lane's row: taken before the quad reduction below, which would
-  // fold four rows' headers together in the header lanes
-  uint64_t h[2];
+    for (int k = 0; k < 16; ++k) {
+      const uint4 x = seg[k];
+      m[2 * k] = u4lo(x);
+      m[2 * k + 1] = u4hi(x);
+    }
+    uint64_t res[2];
+    if (kInlineHdr) {
+      const bool hl = lane >= 32;
+      const uint32_t hrow = (lane - 32) % (uint32_t)U;
+      uint64_t sd[2] = {0, 0};
+      if (with_side) {
+        const uint4 x = st[U * 4 * kSegU4 + hrow];
+        sd[0] = u4lo(x);
+        sd[1] = u4hi(x);
+      }
+      uint64_t hb[16];
+      header_block(row0 + hrow, epoch, htab, sd, hb);
 #pragma unroll
-  for (int w = 0; w < 2; ++w) h[w] = kInlineHdr ? shfl_u64(res[w], (int)(32 + ur)) : hdr[w];
-  // XOR of the row's four leaves (lanes 4ur .. 4ur + 3), then H
+      for (int k = 0; k < 16; ++k) hb[k] = hl ? hb[k] : m[k];
+      B2State s = b2_sel(hl, c.headk, c.leafk1[0]);
 #pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    res[w] ^= shfl_u64(res[w], (int)(lane ^ 1u));
-    res[w] ^= shfl_u64(res[w], (int)(lane ^ 2u));
-    out[w] = res[w] ^ h[w];
+      for (uint32_t i = 1; i < 4; ++i) s = b2_sel(!hl && leaf == i, c.leafk1[i], s);
+      b2_compress(s, hb, hl ? 128 + 32 : 128 + 128, hl);
+      const uint64_t h0 = s.h[0], h1 = s.h[1];
+      b2_compress(s, m + 16, 128 + 256, true);
+      res[0] = hl ? h0 : s.h[0];
+      res[1] = hl ? h1 : s.h[1];
+    } else {
+      B2State s = c.leafk1[0];
+#pragma unroll
+      for (uint32_t i = 1; i < 4; ++i) s = b2_sel(leaf == i, c.leafk1[i], s);
+      leaf_prf(s, m, res);
+    }
+    // H of the lane's row: taken before the quad reduction below, which would
+    // fold four rows' headers together in the header lanes
+    uint64_t h[2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) h[w] = kInlineHdr ? shfl_u64(res[w], (int)(32 + ur)) : hdr[w];
+    // XOR of the row's four leaves (lanes 4ur .. 4ur + 3), then H
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      res[w] ^= shfl_u64(res[w], (int)(lane ^ 1u));
+      res[w] ^= shfl_u64(res[w], (int)(lane ^ 2u));
+      out[w] = res[w] ^ h[w];
+    }
   }
 }
 
@@ -281,13 +329,13 @@ __device__ inline void stage_ctr(const SealCtx& c, const uint32_t* s_te, uint32_
 // Verify and decrypt U rows read at c.epoch.  `tags` is the table's tag
 // array (indexed by row); side ciphertexts (mailbox rows) must already be in
 // the stage's side slots.  Returns false (wave-uniform) on any mismatch.
-template <int U>
+template <int U, int NL = 4>
 __device__ inline bool wave_unseal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                    uint64_t row0, uint4 (&v)[U], const uint4* tags, bool with_side,
-                                   uint4* st, const uint64_t* hdr = nullptr) {
+                                   uint4* st, const uint64_t* hdr = nullptr, uint32_t htab = ~0u) {
   stage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, c.epoch, with_side, st, hdr, t);
+  wave_tags<U, NL>(c, table, row0, c.epoch, with_side, st, hdr, t, htab == ~0u ? table : htab);
   const uint32_t lane = lane_id(), ur = (lane >> 2) % (uint32_t)U;
   const uint4 want = tags[row0 + ur];
   const bool bad = lane < 4u * U && (u4lo(want) != t[0] || u4hi(want) != t[1]);
@@ -298,15 +346,16 @@ __device__ inline bool wave_unseal(const SealCtx& c, const uint32_t* s_te, uint3
 
 // Encrypt U plaintext rows at epoch `ep` (c.epoch + 1 for a pass's writes)
 // and store their tags (side ciphertexts, if any, already staged).
-template <int U>
+template <int U, int NL = 4>
 __device__ inline void wave_seal(const SealCtx& c, const uint32_t* s_te, uint32_t table,
                                  uint64_t row0, uint32_t ep, uint4 (&v)[U], uint4* tags,
-                                 bool with_side, uint4* st, const uint64_t* hdr = nullptr) {
+                                 bool with_side, uint4* st, const uint64_t* hdr = nullptr,
+                                 uint32_t htab = ~0u) {
   stage_rows<U>(v, st);
   stage_ctr<U>(c, s_te, table, row0, ep, st);
   unstage_rows<U>(v, st);
   uint64_t t[2];
-  wave_tags<U>(c, table, row0, ep, with_side, st, hdr, t);
+  wave_tags<U, NL>(c, table, row0, ep, with_side, st, hdr, t, htab == ~0u ? table : htab);
   wave_lds_sync();  // the stage is reused by the caller
   const uint32_t lane = lane_id();
   if ((lane & 3u) == 0 && (lane >> 2) < (uint32_t)U)
@@ -353,7 +402,10 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
       sd[1] = u4hi(x);
     }
     header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);  // one-time: no amortising
-    wave_seal<U>(c, s_te, table, r0, 0u, v, tags, side != nullptr, st, hdr);
+    if (side)
+      wave_seal<U, 4>(c, s_te, table, r0, 0u, v, tags, true, st, hdr);
+    else  // message tables: 8 leaves of 128 B
+      wave_seal<U, 8>(c, s_te, table, r0, 0u, v, tags, false, st, hdr);
 #pragma unroll
     for (int u = 0; u < U; ++u) rows[(r0 + u) * 64 + lane] = v[u];
   }

@@ -289,6 +289,7 @@ __device__ inline uint32_t x_detect2(const R2Args& a, const uint4 (&v)[U], uint4
   return xc;
 }
 
+template <int NW>
 __device__ inline uint32_t x_merge2(uint32_t xep, const uint4* s_xw, const uint32_t* s_xc,
                                     uint4* s_xp, uint32_t tot) {
   const uint32_t tid = threadIdx.x, cap = xep;
@@ -297,7 +298,7 @@ __device__ inline uint32_t x_merge2(uint32_t xep, const uint4* s_xw, const uint3
     const uint32_t k = tid / 3, c = tid % 3;
     uint32_t off = k - tot, src = kNone;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const uint32_t cw = min(s_xc[w], cap);
       const bool take = k >= tot && src == kNone && off < cw;
       src = selu32(take, ((uint32_t)w * (kXepMax + 1) + off) * 3 + c, src);
@@ -306,7 +307,7 @@ __device__ inline uint32_t x_merge2(uint32_t xep, const uint4* s_xw, const uint3
     if (src != kNone) s_xp[k * 3 + c] = s_xw[src];
   }
 #pragma unroll
-  for (int w = 0; w < 4; ++w) add += min(s_xc[w], cap);
+  for (int w = 0; w < NW; ++w) add += min(s_xc[w], cap);
   return min(tot + add, cap);
 }
 
@@ -320,23 +321,29 @@ constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose fi
 // flag in its header, so the next pass must find its final state in P (a
 // hidden P slot fails that row's tag); P rows are sealed as table 2, bound to
 // their position and, through their side entry, to the row they replace.
-template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false>
-__global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
+//
+// NW waves per workgroup, 64 rows per wave per tile (tiles of 64 * NW rows;
+// S must be a multiple).  The sealed pass runs 8 waves of U = 8 rows: they
+// share one AES table, so two waves per SIMD fit the CU's LDS (its VALU work
+// needs both to issue at full rate); the plain pass runs 4 waves of 16 rows.
+template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
+  constexpr uint32_t kT = 64u * NW;  // rows per tile
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
   __shared__ uint32_t s_pp[kSlotMax];  // slot -> position of its final state in P
   __shared__ uint32_t s_np, s_ns;
-  __shared__ uint4 s_xw[4 * (kXepMax + 1) * 3];
+  __shared__ uint4 s_xw[NW * (kXepMax + 1) * 3];
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
-  __shared__ uint32_t s_xc[4], s_xt;
+  __shared__ uint32_t s_xc[NW], s_xt;
   GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
-  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(U) : 1];
+  __shared__ uint4 s_st[AUTH ? NW * stage_u4(U) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
   if (AUTH) load_te(s_te, a.te);
   uint4* st = s_st + (AUTH ? wave * stage_u4(U) : 0u);
-  for (uint32_t o = tid; o < a.S; o += 256) {
+  for (uint32_t o = tid; o < a.S; o += kT) {
     s_pk[o] = -1;
     s_sk[o] = -1;
   }
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
   __syncthreads();
   // every slot descriptor of this partition, both batches (fixed reads)
   const uint64_t sbase = (uint64_t)w * a.c;
-  for (uint32_t k = tid; k < a.c; k += 256) {
+  for (uint32_t k = tid; k < a.c; k += kT) {
     const uint4 dp = a.tprev[(sbase + k) * 8];
     const uint4 ds = a.tcur[(sbase + k) * 8];
     if (dp.y == a.stamp_prev && dp.x < a.S) {
@@ -377,10 +384,10 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
   uint4* part = a.table + rowbase * 64;
   uint4* sslot = a.snap + sbase * 64;
   uint4* dry = a.dry + (uint64_t)w * 64;
-  const uint32_t tiles = a.S / kTile;
+  const uint32_t tiles = a.S / kT;
   for (uint32_t t = 0; t < tiles; ++t) {
     uint32_t xc = 0;
-    const uint32_t rb = t * kTile + wave * 64;
+    const uint32_t rb = t * kT + wave * 64;
     // AUTH: the header PRF of the wave's 64 rows at both epochs, one row per
     // lane; the pending flag comes from the slots of each batch
     uint64_t hv[2] = {0, 0}, hs[2] = {0, 0};
@@ -399,7 +406,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
       if (AUTH) {
         const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
-        if (!wave_unseal<U>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
+        if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
           atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
       }
       uint32_t mp = 0, ms = 0;
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
       if (AUTH) {
         const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
-        wave_seal<U>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
+        wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
@@ -462,18 +469,18 @@ __global__ __launch_bounds__(256, MINW) void k_rpass2(R2Args a) {
     if (lane == 0) s_xc[wave] = xc;
     __syncthreads();
     if (a.xon) {
-      const uint32_t tot = x_merge2(a.xep, s_xw, s_xc, s_xp, s_xt);
+      const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
       __syncthreads();
       if (tid == 0) s_xt = tot;
     }
   }
   // unused slots: c reads of final states and c snapshot writes per partition
-  for (uint32_t k = np + wave; k < a.c; k += 4) {
+  for (uint32_t k = np + wave; k < a.c; k += NW) {
     uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
     if (AUTH) x = xor4(x, uni4(a.psdum[(sbase + k) * 8]));  // as the side entry a P slot reads
     keep4(x);
   }
-  for (uint32_t k = ns + wave; k < a.c; k += 4) {
+  for (uint32_t k = ns + wave; k < a.c; k += NW) {
     st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
     if (lane < 8) st_drop(a.snapid, (sbase + k) * 8 + lane, make_uint4(0, 0, 0, 0));
   }
@@ -531,8 +538,8 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
   uint64_t hdr[2];
   header_prf(a.sc.headk, p0 + ur, a.ep, 2u, sdv, hdr);
   if (SEAL) {
-    wave_seal<U>(a.sc, s_te, 2u, p0, a.ep, v, a.ptag, true, st, hdr);
-  } else if (!wave_unseal<U>(a.sc, s_te, 2u, p0, v, a.ptag, true, st, hdr) && lane == 0) {
+    wave_seal<U, 8>(a.sc, s_te, 2u, p0, a.ep, v, a.ptag, true, st, hdr);
+  } else if (!wave_unseal<U, 8>(a.sc, s_te, 2u, p0, v, a.ptag, true, st, hdr) && lane == 0) {
     atomicOr(&a.scal->error, 8u);
   }
 #pragma unroll

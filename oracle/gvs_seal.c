@@ -225,8 +225,9 @@ static void put_le(uint8_t *p, uint64_t v, int n) {
   for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
 }
 
-/* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ L_0 ^ .. ^ L_3 with
+/* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ L_0 ^ .. ^ L_(n-1) with
  *   L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table & 1), leaf i)
+ *   (message tables, table & 1 = 0: n = 8 leaves of 128 B; mailbox table: n = 4 of 256 B)
  *   H   = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
  *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
  * table: 0 message rows, 1 mailbox rows, 2 pending final states (P, by
@@ -262,11 +263,13 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   put_le(hdr + 12, table, 4);
   if (side_pt) memcpy(hdr + 16, side_ct, 16);
   gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
-  for (uint32_t i = 0; i < 4; ++i) {
+  /* message tables (table & 1 = 0): 8 leaves of 128 B; mailbox table: 4 of 256 B */
+  const uint32_t nl = (table & 1) ? 4 : 8, lb = 1024 / nl;
+  for (uint32_t i = 0; i < nl; ++i) {
     uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'}, l[16];
     put_le(person + 8, i, 4);
     put_le(person + 12, table & 1, 4);
-    gvo_blake2b(mk, 32, person, ct + 256 * i, 256, l, 16);
+    gvo_blake2b(mk, 32, person, ct + lb * i, lb, l, 16);
     for (int k = 0; k < 16; ++k) tag[k] ^= l[k];
   }
 }

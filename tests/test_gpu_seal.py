@@ -24,9 +24,12 @@ pytestmark = pytest.mark.gpu
 SECRET = bytes((0x67 + 31 * i) & 0xFF for i in range(32))
 
 
-def make_pair(n_msgs=4096, Q=16, Sr=32, B=1024):
+def make_pair(n_msgs=4096, Q=16, Sr=32, B=1024, rpp=0):
+    """rpp = 512 (rows per partition) runs the 8-wave sealed message pass
+    (gvs_txn.h k_rpass2 NW = 8, U = 8); the default small-table partitions of
+    256 rows run the 4-wave one."""
     cfg = abi.make_config(n_msgs, mailbox_partitions=Q, mailbox_partition_slots=Sr,
-                          max_batch=B, secret_key=SECRET, auth_storage=True)
+                          max_batch=B, secret_key=SECRET, auth_storage=True, rows_per_partition=rpp)
     return ObliviousStore(cfg), ffi.Model(cfg)
 
 
@@ -43,8 +46,10 @@ def unseal(table, row, epoch, ct, side_ct=None):
     return pt, spt
 
 
-def test_auth_mode_parity_stream():
-    store, model = make_pair()
+@pytest.mark.parametrize("rpp,waves", [(0, 8), (512, 8), (512, 4)])
+def test_auth_mode_parity_stream(rpp, waves):
+    store, model = make_pair(rpp=rpp)
+    store.set_option("sealed_pass_waves", waves)
     model.seed(31)
     seen = run_stream(store, model, ffi.gen_params(n_identities=300), batches=8, n=1024)
     assert {0, 1, 2} <= set(seen), seen
@@ -79,8 +84,9 @@ def pending_states(store, ep):
     return out
 
 
-def test_stored_bytes_are_the_oracle_format():
-    store, model = make_pair()
+@pytest.mark.parametrize("rpp", [0, 512])
+def test_stored_bytes_are_the_oracle_format(rpp):
+    store, model = make_pair(rpp=rpp)
     model.seed(33)
     run_stream(store, model, ffi.gen_params(n_identities=200), batches=3, n=1024)
     st = store.stats()

@@ -53,9 +53,11 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
         hdr += sct if sct is not None else bytes(16)
         tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
                                              person=b"gvs-head" + bytes(8)).digest(), "little")
-        for i in range(4):
+        nl = 4 if table & 1 else 8  # mailbox rows: 4 leaves of 256 B; message tables: 8 of 128 B
+        lb = 1024 // nl
+        for i in range(nl):
             person = b"gvs-leaf" + i.to_bytes(4, "little") + (table & 1).to_bytes(4, "little")
-            tag ^= int.from_bytes(hashlib.blake2b(ct[256 * i:256 * i + 256], key=mk, digest_size=16,
+            tag ^= int.from_bytes(hashlib.blake2b(ct[lb * i:lb * i + lb], key=mk, digest_size=16,
                                                   person=person).digest(), "little")
         out.append((ct, sct, tag.to_bytes(16, "little")))
     return out
