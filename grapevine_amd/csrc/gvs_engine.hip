@@ -1518,6 +1518,31 @@ static void par_memcpy(void* dst, const void* src, size_t bytes) {
   for (auto& t : th) t.join();
 }
 
+// host memory the device can copy from directly (hipHostMalloc'd, e.g. by
+// gvs_host_alloc, or registered)
+static bool is_pinned(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error for the caller
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+int gvs_host_alloc(gvs_handle* h, size_t bytes, void** out) {
+  if (!h || !out || !bytes) return GVS_ERR_INVALID_ARG;
+  *out = nullptr;
+  GVS_HIP(h, hipSetDevice(h->device));
+  GVS_HIP(h, hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return GVS_OK;
+}
+
+int gvs_host_free(gvs_handle* h, void* p) {
+  if (!h) return GVS_ERR_INVALID_ARG;
+  if (p) GVS_HIP(h, hipHostFree(p));
+  return GVS_OK;
+}
+
 static int pipe_init(gvs_handle* h) {
   HostPipe& p = h->pipe;
   if (p.ready) return GVS_OK;
@@ -1555,6 +1580,9 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
   HostPipe& p = h->pipe;
   hipStream_t s = h->stream;
   if (int r = reset_errors(h)) return r;
+  // Caller buffers in pinned memory (gvs_host_alloc) are copied to and from
+  // directly; pageable ones go through the pinned staging pair.
+  const bool pin_in = is_pinned(reqs), pin_out = is_pinned(out);
   HostState snap[2];
   uint64_t off[2] = {0, 0};
   uint64_t next_off = 0;
@@ -1569,11 +1597,15 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       }
     if (more) {  // enqueue batch t in slot b
       const uint32_t b = t & 1u, n = counts[t];
-      if (t >= 2) GVS_HIP(h, hipEventSynchronize(p.h2d[b]));  // hin[b] free again
-      par_memcpy(p.hin[b], reqs + next_off, (size_t)n * sizeof(gvs_request));
+      const void* src = reqs + next_off;
+      if (!pin_in) {
+        if (t >= 2) GVS_HIP(h, hipEventSynchronize(p.h2d[b]));  // hin[b] free again
+        par_memcpy(p.hin[b], reqs + next_off, (size_t)n * sizeof(gvs_request));
+        src = p.hin[b];
+      }
       if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(p.copy, p.done[b], 0));  // din[b] consumed
       if (n)
-        GVS_HIP(h, hipMemcpyAsync(p.din[b], p.hin[b], (size_t)n * sizeof(gvs_request),
+        GVS_HIP(h, hipMemcpyAsync(p.din[b], src, (size_t)n * sizeof(gvs_request),
                                   hipMemcpyHostToDevice, p.copy));
       GVS_HIP(h, hipEventRecord(p.h2d[b], p.copy));
       GVS_HIP(h, hipStreamWaitEvent(s, p.h2d[b], 0));
@@ -1587,8 +1619,8 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       GVS_HIP(h, hipEventRecord(p.done[b], s));
       GVS_HIP(h, hipStreamWaitEvent(p.copy, p.done[b], 0));
       if (n)
-        GVS_HIP(h, hipMemcpyAsync(p.hout[b], p.dout[b], (size_t)n * sizeof(gvs_response),
-                                  hipMemcpyDeviceToHost, p.copy));
+        GVS_HIP(h, hipMemcpyAsync(pin_out ? (void*)(out + next_off) : (void*)p.hout[b], p.dout[b],
+                                  (size_t)n * sizeof(gvs_response), hipMemcpyDeviceToHost, p.copy));
       GVS_HIP(h, hipEventRecord(p.d2h[b], p.copy));
       advance(h);  // as if applied; rolled back below if it was not
       off[b] = next_off;
@@ -1604,7 +1636,8 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
         GVS_HIP(h, hipStreamSynchronize(p.copy));
         return decode_error(h, e);
       }
-      par_memcpy(out + off[pb], p.hout[pb], (size_t)counts[t - 1] * sizeof(gvs_response));
+      if (!pin_out)
+        par_memcpy(out + off[pb], p.hout[pb], (size_t)counts[t - 1] * sizeof(gvs_response));
       if (applied) *applied = t;
     }
     if (!more && t >= enq) break;

@@ -33,6 +33,7 @@ EXPORTED = (
     "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
     "gvs_process_wire_batch", "gvs_process_wire_batch_device", "gvs_wire_decode_device",
     "gvs_wire_encode_device", "gvs_sr25519_verify", "gvs_sr25519_verify_device",
+    "gvs_host_alloc", "gvs_host_free",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
                  "gvs_route_plan")
@@ -70,6 +71,8 @@ def load_library(path=None):
     lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
     lib.gvs_process_wire_batch_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
     lib.gvs_sr25519_verify.argtypes = [vp, vp, vp, u32, vp, u32, vp, u32, vp]
+    lib.gvs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    lib.gvs_host_free.argtypes = [vp, vp]
     lib.gvs_sr25519_verify_device.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, u32, vp, u32, vp]
     lib.gvs_wire_decode_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, vp]
     lib.gvs_wire_encode_device.argtypes = [vp, vp, u32, vp, u32, vp]
@@ -159,6 +162,7 @@ class ObliviousStore:
     def __init__(self, config, comm_id=None):
         self.lib = load_library()
         self.config = config
+        self._pinned = []
         h = ctypes.c_void_p()
         if comm_id is None:
             rc = self.lib.gvs_create(ctypes.byref(config), ctypes.byref(h))
@@ -171,6 +175,9 @@ class ObliviousStore:
 
     def close(self):
         if getattr(self, "h", None):
+            for p in getattr(self, "_pinned", []):
+                self.lib.gvs_host_free(self.h, p)
+            self._pinned = []
             self.lib.gvs_destroy(self.h)
             self.h = None
 
@@ -246,6 +253,17 @@ class ObliviousStore:
             chal.ctypes.data if chal is not None else None, out.ctypes.data, out_stride,
             out_lens.ctypes.data, sigs.ctypes.data, status.ctypes.data))
         return [out[k, :out_lens[k]].tobytes() for k in range(n)], sigs, status
+
+    def host_array(self, count, dtype):
+        """A numpy array of `count` items in pinned host memory (gvs_host_alloc),
+        which gvs_process_batches copies without staging.  Freed when the
+        store closes."""
+        dtype = np.dtype(dtype)
+        p = ctypes.c_void_p()
+        self._check(self.lib.gvs_host_alloc(self.h, max(1, count * dtype.itemsize), ctypes.byref(p)))
+        self._pinned.append(p)
+        buf = (ctypes.c_uint8 * (count * dtype.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dtype, count=count)
 
     def sr25519_verify(self, pks, msgs, sigs, context=b"grapevine-challenge"):
         """Batched schnorrkel verification on the device (gvs_sr25519_verify):

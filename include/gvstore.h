@@ -212,6 +212,13 @@ int gvs_process_batch(gvs_handle *h, const gvs_request *reqs, uint32_t n,
 int gvs_process_batches(gvs_handle *h, const gvs_request *reqs, const uint32_t *counts,
                         uint32_t k, gvs_response *out, uint32_t *applied);
 
+/* Pinned host memory for request / response arrays (hipHostMalloc on the
+ * handle's device).  gvs_process_batches copies such buffers to and from the
+ * device directly, without its pinned staging copies; any other host memory
+ * works too, staged. */
+int gvs_host_alloc(gvs_handle *h, size_t bytes, void **out);
+int gvs_host_free(gvs_handle *h, void *p);
+
 /* Same, with device-resident buffers (n * sizeof(gvs_request) and
  * n * sizeof(gvs_response) bytes on the handle's device).  Used by the
  * benchmark so that the timed region excludes PCIe. */

@@ -130,6 +130,35 @@ def test_host_pipeline_matches_oracle():
     assert not diff_tables(store.dump_messages(), model.dump_messages())
 
 
+@pytest.mark.parametrize("pin", ["in", "out", "both"])
+def test_host_pipeline_pinned_buffers(pin):
+    """Caller buffers in pinned memory (gvs_host_alloc) skip the staging
+    copies: same responses as the oracle, pageable and pinned mixed."""
+    import ctypes
+    store, model = make_pair(4096, 16, 32, 1024)
+    model.seed(15)
+    p = ffi.gen_params(n_identities=300)
+    sizes = [1024, 600, 1024, 1]
+    batches = [model.gen_batch(n, p) for n in sizes]
+    want = np.concatenate([model.process_batch(b) for b in batches])
+    total = sum(sizes)
+    reqs = store.host_array(total, abi.REQUEST_DTYPE) if pin in ("in", "both") else \
+        np.zeros(total, abi.REQUEST_DTYPE)
+    out = store.host_array(total, abi.RESPONSE_DTYPE) if pin in ("out", "both") else \
+        np.zeros(total, abi.RESPONSE_DTYPE)
+    reqs[:] = np.concatenate(batches)
+    counts = np.array(sizes, np.uint32)
+    applied = ctypes.c_uint32(0)
+    store._check(store.lib.gvs_process_batches(store.h, reqs.ctypes.data, counts.ctypes.data,
+                                               len(sizes), out.ctypes.data, ctypes.byref(applied)))
+    assert applied.value == len(sizes)
+    d = diff_responses(np.array(out), want, reqs)
+    assert not d, "\n".join(d)
+    st = store.stats()
+    assert (st["messages"], st["mailboxes"]) == (model.messages, model.mailboxes)
+    store.close()
+
+
 def test_host_pipeline_stops_at_failing_batch():
     """A batch that overflows a router bucket stops the pipeline there: the
     batches before it are applied, it and the later ones are not, and the
