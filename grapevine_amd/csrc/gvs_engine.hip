@@ -173,7 +173,9 @@ struct HostPipe {
   uint8_t* hin[2] = {};
   uint8_t* hout[2] = {};
   uint32_t* herr = nullptr;  // pinned: the agreed error word of the batch in each slot
-  hipStream_t copy = nullptr;
+  hipStream_t copy = nullptr;      // host -> device
+  hipStream_t copy_out = nullptr;  // device -> host (its own queue: an H2D of batch t+1
+                                   // must not wait behind the D2H of batch t)
   hipEvent_t h2d[2] = {}, done[2] = {}, d2h[2] = {};
 };
 
@@ -1447,6 +1449,7 @@ int gvs_destroy(gvs_handle* h) {
   if (h->comm) (void)ncclCommDestroy(h->comm);
   HostPipe& hp = h->pipe;
   if (hp.copy) (void)hipStreamSynchronize(hp.copy);
+  if (hp.copy_out) (void)hipStreamSynchronize(hp.copy_out);
   for (int b = 0; b < 2; ++b) {
     if (hp.hin[b]) (void)hipHostFree(hp.hin[b]);
     if (hp.hout[b]) (void)hipHostFree(hp.hout[b]);
@@ -1455,6 +1458,7 @@ int gvs_destroy(gvs_handle* h) {
   }
   if (hp.herr) (void)hipHostFree(hp.herr);
   if (hp.copy) (void)hipStreamDestroy(hp.copy);
+  if (hp.copy_out) (void)hipStreamDestroy(hp.copy_out);
   for (void* p : h->allocs) (void)hipFree(p);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1558,6 +1562,7 @@ static int pipe_init(gvs_handle* h) {
   }
   GVS_HIP(h, hipHostMalloc((void**)&p.herr, 2 * sizeof(uint32_t), hipHostMallocDefault));
   GVS_HIP(h, hipStreamCreateWithFlags(&p.copy, hipStreamNonBlocking));
+  GVS_HIP(h, hipStreamCreateWithFlags(&p.copy_out, hipStreamNonBlocking));
   p.ready = true;
   return GVS_OK;
 }
@@ -1617,11 +1622,11 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       GVS_HIP(h, hipMemcpyAsync(&p.herr[b], &h->eng[0].scal->error, sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, s));
       GVS_HIP(h, hipEventRecord(p.done[b], s));
-      GVS_HIP(h, hipStreamWaitEvent(p.copy, p.done[b], 0));
+      GVS_HIP(h, hipStreamWaitEvent(p.copy_out, p.done[b], 0));
       if (n)
         GVS_HIP(h, hipMemcpyAsync(pin_out ? (void*)(out + next_off) : (void*)p.hout[b], p.dout[b],
-                                  (size_t)n * sizeof(gvs_response), hipMemcpyDeviceToHost, p.copy));
-      GVS_HIP(h, hipEventRecord(p.d2h[b], p.copy));
+                                  (size_t)n * sizeof(gvs_response), hipMemcpyDeviceToHost, p.copy_out));
+      GVS_HIP(h, hipEventRecord(p.d2h[b], p.copy_out));
       advance(h);  // as if applied; rolled back below if it was not
       off[b] = next_off;
       next_off += n;
@@ -1634,6 +1639,7 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
         restore_state(h, snap[pb]);
         GVS_HIP(h, hipStreamSynchronize(s));  // batch t, if enqueued, did nothing
         GVS_HIP(h, hipStreamSynchronize(p.copy));
+        GVS_HIP(h, hipStreamSynchronize(p.copy_out));
         return decode_error(h, e);
       }
       if (!pin_out)
