@@ -35,6 +35,18 @@ SHAPES = {
     "plain": dict(args=["--log2n", "20", "--batch", "65536"], mixes=ALL_MIXES),
     "auth": dict(args=["--log2n", "20", "--batch", "65536", "--auth"], mixes=ALL_MIXES),
     "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2"], mixes=ROUTED_MIXES),
+    # the wire path (decode, schnorrkel check, store, encode), every batch through it.
+    # Launches and grids must not depend on forged signatures or malformed
+    # messages either; the byte counters are compared over requests that
+    # verify and decode (canonical or not): a forged or malformed request
+    # fails at the gRPC level in the reference (grapevine.proto:57-64), which
+    # the host sees, and an all-failing batch is a batch of hard errors, which
+    # take padding keys in the store's sorts.
+    "wire": dict(args=["--log2n", "20", "--batch", "16384", "--wire"],
+                 mixes=["main", "rud", "wire_forged", "wire_malformed", "wire_noncanonical"],
+                 pmc_mixes=["main", "rud", "wire_noncanonical"],
+                 # the store's own kernels are covered by the shapes above
+                 pmc_kernels=("k_wire_decode", "sr::k_sr_verify", "k_wire_encode")),
 }
 FILL_BATCHES = 4
 
@@ -73,7 +85,8 @@ def split_batches(vals):
     (k_seal_init at store creation) are dropped.  Routed stores start each
     batch with the router, one k_route_dest..k_route_fill run per source: a
     batch starts at the k_route_dest that follows a non-router kernel."""
-    first = "k_route_dest" if any(k == "k_route_dest" for k, _ in vals) else "k_copy"
+    first = ("k_wire_decode" if any(k == "k_wire_decode" for k, _ in vals) else
+             "k_route_dest" if any(k == "k_route_dest" for k, _ in vals) else "k_copy")
     out, cur, prev = [], None, ""
     for k, v in vals:
         starts = k == first and not (first == "k_route_dest" and prev.startswith("k_route_")
@@ -113,6 +126,8 @@ def test_launch_sequence_and_grids_identical(traces):
     if shape == "routed":
         assert {"k_route_dest", "k_route_pos", "k_route_copy", "k_route_fill",
                 "k_route_gather"} <= names, sorted(names)
+    if shape == "wire":
+        assert {"k_wire_decode", "sr::k_sr_verify", "k_wire_encode"} <= names, sorted(names)
     for mix, seq in tr.items():
         assert seq == ref, f"{shape}: mix {mix} launches differ from main"
 
@@ -139,7 +154,7 @@ def test_hbm_bytes_identical(counter, shape, tmp_path):
     """Per kernel, the byte counter of every measured batch of every mix must
     equal main's within the counter's own run-to-run noise."""
     per_mix = {}
-    for mix in SHAPES[shape]["mixes"]:
+    for mix in SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"]):
         d = rocprof(["--pmc", counter], mix, str(tmp_path / f"{counter}_{mix}"), shape)
         rows = gvs_rows(os.path.join(d, "**", "*counter_collection.csv"))
         vals = [(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
@@ -154,7 +169,10 @@ def test_hbm_bytes_identical(counter, shape, tmp_path):
     ref_b = per_mix["main"]
     kernels = [k for k, _ in ref_b[-1]]
     lines, bad = [], []
+    only = SHAPES[shape].get("pmc_kernels")
     for idx, k in enumerate(kernels):
+        if only and k not in only:
+            continue
         noise, tol = noise_tolerance(per_mix, repeat, idx, n_meas)
         ref = sorted(b[idx][1] for b in ref_b[-n_meas:])[1]
         row = [f"{k[:28]:28s} ref={ref:12.1f} noise={noise:8.2f} tol={tol:8.2f}"]

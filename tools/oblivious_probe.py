@@ -11,6 +11,12 @@ state and checks the responses.
 --shards S > 1 runs the sharded store in its single-process form (S shards on
 one device, the router kernels k_route_* and the padded all-to-all), against
 the oracle's cluster model.
+
+--wire runs every batch (prefill included) through gvs_process_wire_batch:
+protobuf requests in 1200-B slots, decoded, their schnorrkel signatures
+checked against per-request challenges, the store, responses encoded.  The
+wire_* mixes are the main mix with every signature forged, every message
+malformed, or every message in a non-canonical encoding.
 """
 import argparse
 import os
@@ -31,7 +37,85 @@ MIXES = {
     "hot_next": dict(create=30, read=35, update=0, delete=35, nxt=100, hot=100),
     "hot_next_rud": dict(create=0, read=50, update=0, delete=50, nxt=100, hot=100),
     "deletes": dict(create=0, read=0, update=0, delete=100, nxt=30),
+    # --wire only: the main mix, mutated on the wire
+    "wire_forged": dict(create=25, read=25, update=25, delete=25, nxt=50),
+    "wire_malformed": dict(create=25, read=25, update=25, delete=25, nxt=50),
+    "wire_noncanonical": dict(create=25, read=25, update=25, delete=25, nxt=50),
 }
+WIRE_STRIDE = 1200
+
+
+class WirePath:
+    """Requests as signed wire messages (test infrastructure: 64 ristretto keys,
+    each with one pre-signed challenge; identities map to keys in order of
+    first appearance, so every process maps them the same way)."""
+
+    def __init__(self, store, model, n_keys):
+        import random
+        import numpy as np
+        from oracle import sr25519 as sr
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import wire_cases
+        self.store, self.model, self.wc = store, model, wire_cases
+        # one key per identity; generated once per box (seeded), then cached
+        cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gvs_probe_keys_{n_keys}.npy")
+        if os.path.exists(cache):
+            raw = np.load(cache)
+        else:
+            rng = random.Random(5)
+            rows = []
+            for _ in range(n_keys):
+                x = rng.randrange(1, sr.L)
+                chal = rng.randbytes(32)
+                rows.append(sr.public_key(x) + chal + sr.sign(x, chal, rng.randrange(1, sr.L)))
+            raw = np.frombuffer(b"".join(rows), np.uint8).reshape(n_keys, 128)
+            np.save(cache + ".tmp.npy", raw)
+            os.replace(cache + ".tmp.npy", cache)
+        self.keys = [(bytes(r[:32]), bytes(r[32:64]), bytes(r[64:])) for r in raw]
+        self.idmap = {}
+        self.rng = random.Random(9)
+
+    def key_of(self, v):
+        if v not in self.idmap:
+            self.idmap[v] = len(self.idmap) % len(self.keys)
+        return self.idmap[v]
+
+    def run(self, reqs, mix):
+        import numpy as np
+        from grapevine_amd import wire
+        msgs, chal, valid = [], [], []
+        for q in reqs:
+            a0 = bytes(q["auth_identity"])
+            k = self.key_of(a0) if any(a0) else None
+            for f in ("recipient", "auth_identity"):
+                v = bytes(q[f])
+                if any(v):
+                    q[f] = np.frombuffer(self.keys[self.key_of(v)][0], np.uint8)
+            pk, c, sig = self.keys[k] if k is not None else (bytes(32), bytes(32), bytes(64))
+            if mix == "wire_forged":
+                sig = bytes([sig[0] ^ 1]) + sig[1:]
+            f = dict(rt=int(q["request_type"]), auth=bytes(q["auth_identity"]), sig=sig,
+                     id=bytes(q["msg_id"]), rc=bytes(q["recipient"]), pl=bytes(q["payload"]))
+            m = self.wc.canonical(f)
+            if mix == "wire_malformed":
+                m = m[:self.rng.randrange(1, len(m))]
+            elif mix == "wire_noncanonical":
+                m = self.wc.ld(4, self.wc.record(f, (3, 1, 2))) + self.wc.fx64(10, 7) + m[:105]
+            msgs.append(m)
+            chal.append(c)
+            valid.append(k is not None and mix != "wire_forged")
+        times = reqs["timestamp"].copy()
+        q, _, st = wire.decode_requests(msgs, timestamps=times, strict=False)
+        for i in range(len(q)):
+            if st[i] == 0 and not valid[i]:
+                q[i]["request_type"] = 0
+        want = [wire.encode_response(r) for r in self.model.process_batch(q)]
+        got, _, _ = self.store.process_wire_batch(
+            msgs, times, in_stride=WIRE_STRIDE,
+            challenges=np.frombuffer(b"".join(chal), np.uint8).reshape(-1, 32))
+        assert got == want, "parity failure inside the probe (wire path)"
+        if mix == "main":
+            assert sum(1 for r in got if r) > len(got) // 2, "wire prefill: most requests must verify"
 
 
 def main():
@@ -44,7 +128,9 @@ def main():
     p.add_argument("--shards", type=int, default=0)
     p.add_argument("--identities", type=int, default=5000)
     p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
+    p.add_argument("--wire", action="store_true", help="wire path with challenge check")
     a = p.parse_args()
+    assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
     S = a.shards if a.shards > 1 else 0
     cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth, shard_count=S)
     store = ObliviousStore(cfg)
@@ -52,8 +138,12 @@ def main():
     n = a.batch * (S or 1)
     model.seed(77)
     fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=a.identities)
+    wp = WirePath(store, model, a.identities) if a.wire else None
     for _ in range(a.fill_batches):
         reqs = model.gen_batch(n, fill)
+        if wp:
+            wp.run(reqs, "main")
+            continue
         want = model.process_batch(reqs)
         got = store.process_batch(reqs)
         assert got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
@@ -62,6 +152,9 @@ def main():
                             zero_recipient=0, **{"miss": 0, **MIXES[a.mix]})
     for _ in range(a.batches):
         reqs = model.gen_batch(n, params)
+        if wp:
+            wp.run(reqs, a.mix)
+            continue
         want = model.process_batch(reqs)
         got = store.process_batch(reqs)
         assert got.tobytes() == want.tobytes(), "parity failure inside the probe"
