@@ -42,6 +42,7 @@ case "$2" in
   tob) tests && step oblivious_all 1000 $PT tests/test_oblivious.py && step hbm_probe 300 tools/hbm_probe 16 && bench ;;
   oblall) step oblivious_all 1150 $PT tests/test_oblivious.py ;;
   all) tests && bench && timing ;;
+  full) tests && timing && step oblivious_all 1150 $PT tests/test_oblivious.py ;;
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines
     step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
