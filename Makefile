@@ -9,7 +9,9 @@ TESTLIB := grapevine_amd/libgvstore_test.so
 SRCS := grapevine_amd/csrc/gvs_engine.hip
 HDRS := $(wildcard grapevine_amd/csrc/*.h) include/gvstore.h include/gvstore_test.h
 
-all: $(LIB) $(TESTLIB) oracle
+SRHOST := tests/libsrhost.so
+
+all: $(LIB) $(TESTLIB) $(SRHOST) oracle
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
@@ -17,11 +19,15 @@ $(LIB): $(SRCS) $(HDRS)
 $(TESTLIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DGVS_TEST_HOOKS -shared -o $@ $(SRCS) -lrccl
 
+# the device signature-check arithmetic built for the CPU (tests/test_sr_host.py)
+$(SRHOST): tests/sr_host.cpp grapevine_amd/csrc/gvs_sr25519.h grapevine_amd/csrc/gvs_device.h
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -o $@ tests/sr_host.cpp
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB) $(TESTLIB)
+	rm -f $(LIB) $(TESTLIB) $(SRHOST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -416,6 +416,31 @@ GVS_SR_FN void shl1(Fe& x) {
   x.v[0] <<= 1;
 }
 
+// s*B - k*A for scalars below 2^253: one joint double-and-add from bit 252,
+// fixed 253 steps, the addend selected by masks from {0, B, -A, B - A}
+GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A) {
+  const Pt B = pt_base();
+  const Pt nA = pt_neg(A);
+  const Pt BnA = pt_add(B, nA);
+  Pt acc = pt_identity();
+  Fe sw = s, kw = k;  // bit 252 moved to the top, then shifted out one per step
+  for (int i = 0; i < 3; ++i) {
+    shl1(sw);
+    shl1(kw);
+  }
+  for (int b = 252; b >= 0; --b) {
+    acc = pt_dbl(acc);
+    const uint32_t sb = 0u - (sw.v[7] >> 31);
+    const uint32_t kb = 0u - (kw.v[7] >> 31);
+    shl1(sw);
+    shl1(kw);
+    Pt q = pt_select(kb, nA, pt_identity());
+    q = pt_select(sb, pt_select(kb, BnA, B), q);
+    acc = pt_add(acc, q);
+  }
+  return acc;
+}
+
 // ------------------------------------------------------------ STROBE / merlin
 
 constexpr int kStrobeR = 166;
@@ -616,26 +641,7 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   const Pt A = ristretto_decode(A_s, &pk_ok);
   ok &= pk_ok;
 
-  // s*B - k*A, both scalars < 2^253: joint double-and-add from bit 252
-  const Pt B = pt_base();
-  const Pt nA = pt_neg(A);
-  const Pt BnA = pt_add(B, nA);
-  Pt acc = pt_identity();
-  Fe sw = sc, kw = kc;  // bit 252 moved to the top, then shifted out one per step
-  for (int i = 0; i < 3; ++i) {
-    shl1(sw);
-    shl1(kw);
-  }
-  for (int b = 252; b >= 0; --b) {
-    acc = pt_dbl(acc);
-    const uint32_t sb = 0u - (sw.v[7] >> 31);
-    const uint32_t kb = 0u - (kw.v[7] >> 31);
-    shl1(sw);
-    shl1(kw);
-    Pt q = pt_select(kb, nA, pt_identity());
-    q = pt_select(sb, pt_select(kb, BnA, B), q);
-    acc = pt_add(acc, q);
-  }
+  const Pt acc = double_scalar_mul(sc, kc, A);
   const Fe enc = ristretto_encode(acc);
   uint32_t diff = 0;
 #pragma unroll
