@@ -690,7 +690,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       if (lane < (uint32_t)kMU) {
         const uint4 ct = xor4(mine, side_keystream(a.sc, s_te, r0 + lane, ep));
         st[kMU * 4 * kSegU4 + lane] = ct;
-        st_drop(side + j0, lane, ct);  // whole 128-B line of side entries, written through
+        side[j0 + lane] = ct;
       }
       wave_seal<kMU>(a.sc, s_te, 1u, r0, ep, v, a.btag, true, st);
     }

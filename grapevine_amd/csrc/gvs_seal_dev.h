@@ -358,12 +358,9 @@ __device__ inline void wave_seal(const SealCtx& c, const uint32_t* s_te, uint32_
   wave_tags<U, NL>(c, table, row0, ep, with_side, st, hdr, t, htab == ~0u ? table : htab);
   wave_lds_sync();  // the stage is reused by the caller
   const uint32_t lane = lane_id();
-  // the chunk's tags (whole lines: U x 16 B, one store instruction) are
-  // written through and dropped from L2, so they reach HBM inside this kernel
-  // whatever else the L2 holds (DESIGN.md §3 rules 2-3)
   if ((lane & 3u) == 0 && (lane >> 2) < (uint32_t)U)
-    st_drop(tags + row0, lane >> 2,
-            make_uint4((uint32_t)t[0], (uint32_t)(t[0] >> 32), (uint32_t)t[1], (uint32_t)(t[1] >> 32)));
+    tags[row0 + (lane >> 2)] = make_uint4((uint32_t)t[0], (uint32_t)(t[0] >> 32), (uint32_t)t[1],
+                                          (uint32_t)(t[1] >> 32));
 }
 
 // Keystream block 64 (the mailbox side entry) of `row` at `ep`.
