@@ -383,6 +383,10 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     }
     vscan_carry_tail<M1rOp>(a, s_v, s_f, f, v, cf, cv);
   }
+  // Pass 1, op by op (the carry is sequential): everything but the id decode.
+  // Lane j keeps op j's result words and the id it must decode.
+  uint4 my_idv = make_uint4(0, 0, 0, 0), my_w = make_uint4(0, 0, 0, 0), my_oid = my_idv;
+  uint32_t my_need = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
@@ -399,7 +403,6 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     // next-message op: the one with d delete-nexts before it reads id d
     const uint32_t d = pf.y;
     const uint4 idv = shfl4(pv, 2 + (int)min(d, 61u));
-    const uint32_t dec = id_decode(a.kc, u4lo(idv), u4hi(idv), a.N);  // every op: fixed work
     const bool found = !null && d < len;
     // create: rank r among the group's creates (grapevine.proto:73-75)
     const uint32_t r = pf.z;
@@ -413,16 +416,29 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     const bool c0 = !null && cls == 0u, c1 = !null && cls == 1u, c2 = !null && cls > 1u;
     const uint32_t st1 = selu32(cok, kPending, selu32(exists1 || admitted, 5u, 6u));
     const uint32_t status = selu32(c0, selu32(found, kPending, 2u), selu32(c1, st1, kPending));
-    const uint32_t slot = selu32(c0 && found, dec, kNone);
     const uint32_t flags = selu32(c0 && found && mpos_sub(mp.x), CF_POP, selu32(c1 && cok, CF_MBOX_OK, 0u));
     const uint32_t opos = selu32(c2, pos, 63u);
-    const uint4 oid = sel4(c0 && found, idv, make_uint4(0, 0, 0, 0));
-    if (lane < 8)
-      st_drop(a.m1out, (uint64_t)seq * 8 + lane,
-              sel4(lane == 0, make_uint4(status, slot, flags, opos), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0))));
+    const bool mine = lane == j;
+    my_idv = sel4(mine, idv, my_idv);
+    my_oid = sel4(mine, sel4(c0 && found, idv, make_uint4(0, 0, 0, 0)), my_oid);
+    my_w = sel4(mine, make_uint4(status, seq, flags, opos), my_w);
+    my_need = selu32(mine, (c0 && found) ? 1u : 0u, my_need);
     const uint4 e = M1rOp::f_of_pos(mp.x);
     cv = M1rOp::v_combine(cf, cv, e, A);
     cf = M1rOp::f_combine(cf, e);
+  }
+  // Pass 2: the 16 id decodes at once, one per lane (every lane decodes:
+  // fixed work), then the records in op order.
+  const uint32_t my_dec = id_decode(a.kc, u4lo(my_idv), u4hi(my_idv), a.N);
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint4 w = uni4(shfl4(my_w, (int)j));
+    const uint4 oid = shfl4(my_oid, (int)j);
+    const uint32_t dec = __shfl(my_dec, (int)j), need = __shfl(my_need, (int)j);
+    const uint32_t slot = selu32(need != 0u, dec, kNone);
+    if (lane < 8)
+      st_drop(a.m1out, (uint64_t)w.y * 8 + lane,
+              sel4(lane == 0, make_uint4(w.x, slot, w.z, w.w), sel4(lane == 1, oid, make_uint4(0, 0, 0, 0))));
   }
 }
 
