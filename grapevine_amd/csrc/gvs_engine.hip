@@ -192,6 +192,21 @@ struct WireStage {
   uint4* chal = nullptr;     // n x 32-B challenges
 };
 
+// Double-buffered wire path (gvs_process_wire_batches): per slot, the device
+// and pinned host buffers of one batch's wire messages and results, allocated
+// on first use for max_submit messages of kWireSlotMax bytes each way.
+struct WirePipe {
+  bool ready = false;
+  uint8_t *din[2] = {}, *dout[2] = {};
+  uint32_t *dlens[2] = {}, *dolens[2] = {}, *dstat[2] = {};
+  uint64_t* dtimes[2] = {};
+  uint4* dchal[2] = {};
+  uint8_t *hin[2] = {}, *hout[2] = {}, *hchal[2] = {};
+  uint32_t *hlens[2] = {}, *holens[2] = {}, *hstat[2] = {};
+  uint64_t* htimes[2] = {};
+  hipEvent_t h2d[2] = {}, done[2] = {}, d2h[2] = {};
+};
+
 struct gvs_handle {
   gvs_config cfg{};
   Mode mode = kSingle;
@@ -219,6 +234,7 @@ struct gvs_handle {
   int sealed_nw = 8;         // waves per workgroup of the sealed message pass (4 or 8; option)
   HostPipe pipe;
   WireStage wire;
+  WirePipe wpipe;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -1457,6 +1473,14 @@ int gvs_destroy(gvs_handle* h) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (hp.herr) (void)hipHostFree(hp.herr);
+  WirePipe& wp = h->wpipe;
+  for (int b = 0; b < 2; ++b) {
+    for (void* q : {(void*)wp.hin[b], (void*)wp.hout[b], (void*)wp.hchal[b], (void*)wp.hlens[b],
+                    (void*)wp.holens[b], (void*)wp.hstat[b], (void*)wp.htimes[b]})
+      if (q) (void)hipHostFree(q);
+    for (hipEvent_t ev : {wp.h2d[b], wp.done[b], wp.d2h[b]})
+      if (ev) (void)hipEventDestroy(ev);
+  }
   if (hp.copy) (void)hipStreamDestroy(hp.copy);
   if (hp.copy_out) (void)hipStreamDestroy(hp.copy_out);
   for (void* p : h->allocs) (void)hipFree(p);
@@ -1829,6 +1853,130 @@ int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
       GVS_HIP(h, hipMemcpyAsync(decode_status, w.status, (size_t)n * 4, hipMemcpyDeviceToHost, s));
   }
   return finish(h);
+}
+
+static int wire_pipe_init(gvs_handle* h) {
+  WirePipe& p = h->wpipe;
+  if (p.ready) return GVS_OK;
+  if (int r = pipe_init(h)) return r;  // the copy streams and the host pipeline's pinned words
+  const uint64_t cap = max_submit(h), big = cap * kWireSlotMax;
+  for (int b = 0; b < 2; ++b) {
+    if (int rc = dalloc_t(h, &p.din[b], big)) return rc;
+    if (int rc = dalloc_t(h, &p.dout[b], big)) return rc;
+    if (int rc = dalloc_t(h, &p.dlens[b], cap)) return rc;
+    if (int rc = dalloc_t(h, &p.dolens[b], cap)) return rc;
+    if (int rc = dalloc_t(h, &p.dstat[b], cap)) return rc;
+    if (int rc = dalloc_t(h, &p.dtimes[b], cap)) return rc;
+    if (int rc = dalloc_t(h, &p.dchal[b], cap * 2)) return rc;
+    GVS_HIP(h, hipHostMalloc((void**)&p.hin[b], big, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.hout[b], big, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.hchal[b], cap * 32, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.hlens[b], cap * 4, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.holens[b], cap * 4, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.hstat[b], cap * 4, hipHostMallocDefault));
+    GVS_HIP(h, hipHostMalloc((void**)&p.htimes[b], cap * 8, hipHostMallocDefault));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.h2d[b], hipEventDisableTiming));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.done[b], hipEventDisableTiming));
+    GVS_HIP(h, hipEventCreateWithFlags(&p.d2h[b], hipEventDisableTiming));
+  }
+  p.ready = true;
+  return GVS_OK;
+}
+
+// k wire batches from host memory, double-buffered like gvs_process_batches:
+// batch t+1's messages go up on the copy stream and batch t-1's results come
+// down on the other while batch t runs (decode, challenge check, the store,
+// encode).  At the first batch that fails, its error is returned and it and
+// the later batches are not applied.
+int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
+                             const uint32_t* in_lens, const uint32_t* counts, uint32_t k,
+                             const uint64_t* times, const uint8_t* challenges, uint8_t* out,
+                             uint32_t out_stride, uint32_t* out_lens, uint32_t* decode_status,
+                             uint32_t* applied) {
+  if (applied) *applied = 0;
+  if (!h || h->kind != 0 || !wire_strides_ok(in_stride, out_stride) ||
+      (k && (!counts || !in || !in_lens || !times || !out || !out_lens)))
+    return GVS_ERR_INVALID_ARG;
+  for (uint32_t t = 0; t < k; ++t)
+    if (counts[t] > max_submit(h)) return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (k == 0) return GVS_OK;
+  GVS_HIP(h, hipSetDevice(h->device));
+  if (int r = wire_pipe_init(h)) return r;
+  if (int r = wire_stage_init(h, false)) return r;
+  WirePipe& p = h->wpipe;
+  HostPipe& hp = h->pipe;
+  hipStream_t s = h->stream;
+  if (int r = reset_errors(h)) return r;
+  HostState snap[2];
+  uint64_t off[2] = {0, 0}, next_off = 0;
+  uint32_t enq = 0;
+  int stop = GVS_OK;
+  for (uint32_t t = 0;; ++t) {
+    bool more = t < k && stop == GVS_OK;
+    if (more)
+      if (int r = check_epoch(h)) {
+        stop = r;
+        more = false;
+      }
+    if (more) {  // enqueue batch t in slot b
+      const uint32_t b = t & 1u, n = counts[t];
+      if (t >= 2) GVS_HIP(h, hipEventSynchronize(p.h2d[b]));  // staging b free again
+      par_memcpy(p.hin[b], in + next_off * in_stride, (size_t)n * in_stride);
+      std::memcpy(p.hlens[b], in_lens + next_off, (size_t)n * 4);
+      std::memcpy(p.htimes[b], times + next_off, (size_t)n * 8);
+      if (challenges) std::memcpy(p.hchal[b], challenges + next_off * 32, (size_t)n * 32);
+      if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(hp.copy, p.done[b], 0));  // device slot b consumed
+      if (n) {
+        GVS_HIP(h, hipMemcpyAsync(p.din[b], p.hin[b], (size_t)n * in_stride, hipMemcpyHostToDevice, hp.copy));
+        GVS_HIP(h, hipMemcpyAsync(p.dlens[b], p.hlens[b], (size_t)n * 4, hipMemcpyHostToDevice, hp.copy));
+        GVS_HIP(h, hipMemcpyAsync(p.dtimes[b], p.htimes[b], (size_t)n * 8, hipMemcpyHostToDevice, hp.copy));
+        if (challenges)
+          GVS_HIP(h, hipMemcpyAsync(p.dchal[b], p.hchal[b], (size_t)n * 32, hipMemcpyHostToDevice, hp.copy));
+      }
+      GVS_HIP(h, hipEventRecord(p.h2d[b], hp.copy));
+      GVS_HIP(h, hipStreamWaitEvent(s, p.h2d[b], 0));
+      if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(s, p.d2h[b], 0));  // results b copied out
+      snap[b] = save_state(h);
+      if (int r = wire_batch(h, p.din[b], in_stride, p.dlens[b], n, p.dtimes[b],
+                             challenges ? p.dchal[b] : nullptr, p.dout[b], out_stride, p.dolens[b],
+                             nullptr, p.dstat[b]))
+        return r;
+      if (h->mode != kSingle)
+        if (int r = agree_errors(h)) return r;
+      GVS_HIP(h, hipMemcpyAsync(&hp.herr[b], &h->eng[0].scal->error, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, s));
+      GVS_HIP(h, hipEventRecord(p.done[b], s));
+      GVS_HIP(h, hipStreamWaitEvent(hp.copy_out, p.done[b], 0));
+      if (n) {
+        GVS_HIP(h, hipMemcpyAsync(p.hout[b], p.dout[b], (size_t)n * out_stride, hipMemcpyDeviceToHost, hp.copy_out));
+        GVS_HIP(h, hipMemcpyAsync(p.holens[b], p.dolens[b], (size_t)n * 4, hipMemcpyDeviceToHost, hp.copy_out));
+        GVS_HIP(h, hipMemcpyAsync(p.hstat[b], p.dstat[b], (size_t)n * 4, hipMemcpyDeviceToHost, hp.copy_out));
+      }
+      GVS_HIP(h, hipEventRecord(p.d2h[b], hp.copy_out));
+      advance(h);  // as if applied; rolled back below if it was not
+      off[b] = next_off;
+      next_off += n;
+      enq = t + 1;
+    }
+    if (t >= 1 && t - 1 < enq) {  // collect batch t-1
+      const uint32_t pb = (t - 1) & 1u, n = counts[t - 1];
+      GVS_HIP(h, hipEventSynchronize(p.d2h[pb]));
+      if (const uint32_t e = hp.herr[pb]) {
+        restore_state(h, snap[pb]);
+        GVS_HIP(h, hipStreamSynchronize(s));
+        GVS_HIP(h, hipStreamSynchronize(hp.copy));
+        GVS_HIP(h, hipStreamSynchronize(hp.copy_out));
+        return decode_error(h, e);
+      }
+      par_memcpy(out + off[pb] * out_stride, p.hout[pb], (size_t)n * out_stride);
+      std::memcpy(out_lens + off[pb], p.holens[pb], (size_t)n * 4);
+      if (decode_status) std::memcpy(decode_status + off[pb], p.hstat[pb], (size_t)n * 4);
+      if (applied) *applied = t;
+    }
+    if (!more && t >= enq) break;
+  }
+  return stop;
 }
 
 int gvs_sr25519_verify_device(gvs_handle* h, const void* d_pks, uint32_t pk_stride,

@@ -33,7 +33,7 @@ EXPORTED = (
     "gvs_omap_set_timing", "gvs_omap_last_timings", "gvs_omap_last_error",
     "gvs_process_wire_batch", "gvs_process_wire_batch_device", "gvs_wire_decode_device",
     "gvs_wire_encode_device", "gvs_sr25519_verify", "gvs_sr25519_verify_device",
-    "gvs_host_alloc", "gvs_host_free",
+    "gvs_host_alloc", "gvs_host_free", "gvs_process_wire_batches",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
                  "gvs_route_plan")
@@ -69,6 +69,8 @@ def load_library(path=None):
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
+    lib.gvs_process_wire_batches.argtypes = [vp, vp, u32, vp, vp, u32, vp, vp, vp, u32, vp, vp,
+                                             ctypes.POINTER(u32)]
     lib.gvs_process_wire_batch_device.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
     lib.gvs_sr25519_verify.argtypes = [vp, vp, vp, u32, vp, u32, vp, u32, vp]
     lib.gvs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
@@ -218,15 +220,8 @@ class ObliviousStore:
     def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
         self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))
 
-    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=abi.WIRE_RESPONSE_BYTES,
-                           challenges=None):
-        """Wire QueryRequests (list of bytes, or an (n, L) uint8 array of
-        canonical messages) through the device codec and the store
-        (gvs_process_wire_batch).  `challenges` ((n, 32) uint8, optional): the
-        challenge each auth_signature must sign; failing requests become hard
-        errors.  -> (list of response bytes, (n, 64) signatures, per-request
-        GVS_WIRE_* status).  A hard error's response is b"" (the handler
-        answers it with a gRPC error)."""
+    @staticmethod
+    def _wire_slab(msgs, in_stride):
         if isinstance(msgs, np.ndarray):
             n, width = msgs.shape
             lens = np.full(n, width, np.uint32)
@@ -240,6 +235,52 @@ class ObliviousStore:
             slab = np.zeros((n, stride), np.uint8)
             for k, m in enumerate(msgs):
                 slab[k, :len(m)] = np.frombuffer(bytes(m), np.uint8)
+        return slab, lens, stride
+
+    def process_wire_batches(self, batches, times, in_stride=None,
+                             out_stride=abi.WIRE_RESPONSE_BYTES, challenges=None):
+        """Several wire batches in one double-buffered call
+        (gvs_process_wire_batches).  batches: list of lists of message bytes;
+        times / challenges: per message over all batches (times may be a
+        scalar).  -> list of (response bytes list, status array) per batch.
+        On a failing batch raises GvsError with `.applied`."""
+        counts = np.array([len(b) for b in batches], dtype=np.uint32)
+        flat = [m for b in batches for m in b]
+        n = len(flat)
+        slab, lens, stride = self._wire_slab(flat, in_stride)
+        times = np.ascontiguousarray(np.broadcast_to(np.asarray(times, np.uint64), (n,)))
+        out = np.zeros((n, out_stride), np.uint8)
+        out_lens = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint32)
+        chal = None
+        if challenges is not None:
+            chal = np.ascontiguousarray(challenges, np.uint8).reshape(n, 32)
+        applied = ctypes.c_uint32(0)
+        rc = self.lib.gvs_process_wire_batches(
+            self.h, slab.ctypes.data, stride, lens.ctypes.data, counts.ctypes.data, len(counts),
+            times.ctypes.data, chal.ctypes.data if chal is not None else None, out.ctypes.data,
+            out_stride, out_lens.ctypes.data, status.ctypes.data, ctypes.byref(applied))
+        if rc != 0:
+            err = GvsError(rc, (self.lib.gvs_last_error(self.h) or b"").decode())
+            err.applied = applied.value
+            raise err
+        res, o = [], 0
+        for c in counts:
+            res.append(([out[k, :out_lens[k]].tobytes() for k in range(o, o + c)], status[o:o + c]))
+            o += int(c)
+        return res
+
+    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=abi.WIRE_RESPONSE_BYTES,
+                           challenges=None):
+        """Wire QueryRequests (list of bytes, or an (n, L) uint8 array of
+        canonical messages) through the device codec and the store
+        (gvs_process_wire_batch).  `challenges` ((n, 32) uint8, optional): the
+        challenge each auth_signature must sign; failing requests become hard
+        errors.  -> (list of response bytes, (n, 64) signatures, per-request
+        GVS_WIRE_* status).  A hard error's response is b"" (the handler
+        answers it with a gRPC error)."""
+        slab, lens, stride = self._wire_slab(msgs, in_stride)
+        n = len(lens)
         times = np.ascontiguousarray(np.broadcast_to(np.asarray(times, np.uint64), (n,)))
         out = np.zeros((n, out_stride), np.uint8)
         out_lens = np.zeros(n, np.uint32)

@@ -266,6 +266,17 @@ int gvs_process_wire_batch(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
                            const uint32_t *in_lens, uint32_t n, const uint64_t *times,
                            const uint8_t *challenges, uint8_t *out, uint32_t out_stride,
                            uint32_t *out_lens, uint8_t *sigs, uint32_t *decode_status);
+/* k wire batches from host memory in one call, double-buffered like
+ * gvs_process_batches (uploads of batch t+1 and downloads of batch t-1 run
+ * while batch t is processed).  Batch t has counts[t] messages; the messages
+ * of all batches are consecutive in `in` (and in in_lens, times, challenges),
+ * their results likewise in out / out_lens / decode_status.  Stops at the
+ * first failing batch: its error is returned, *applied = the batches before. */
+int gvs_process_wire_batches(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
+                             const uint32_t *in_lens, const uint32_t *counts, uint32_t k,
+                             const uint64_t *times, const uint8_t *challenges, uint8_t *out,
+                             uint32_t out_stride, uint32_t *out_lens, uint32_t *decode_status,
+                             uint32_t *applied);
 /* The same with device buffers (in: n*in_stride B, in_lens: n u32, times: n
  * u64, challenges: optional n*32 B, out: n*out_stride B, out_lens: n u32,
  * sigs: optional n*64 B, decode_status: optional n u32). */

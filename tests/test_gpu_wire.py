@@ -173,3 +173,60 @@ def test_wire_batches_end_to_end(host_api):
         st_ = store.stats()
         assert (st_["messages"], st_["mailboxes"]) == (model.messages, model.mailboxes)
     store.close()
+
+
+def test_wire_batches_pipelined():
+    """gvs_process_wire_batches: several wire batches (one empty, ragged
+    sizes) in one double-buffered call, equal to the oracle batch by batch;
+    then a call with one batch carrying challenges, half signed correctly."""
+    from oracle import sr25519 as sr
+    import random
+    store, model = small_store()
+    model.seed(33)
+    params = ffi.gen_params(n_identities=200, hot=10)
+    rng = np.random.default_rng(19)
+    sizes = [1024, 0, 517, 1024, 3, 40]
+    batches, times, wants = [], [], []
+    signer = random.Random(8)
+    xs = {}
+    chal = np.zeros((sum(sizes), 32), np.uint8)
+    base = sum(sizes[:-1])
+    for b, n in enumerate(sizes):
+        reqs = model.gen_batch(n, params) if n else np.zeros(0, abi.REQUEST_DTYPE)
+        msgs = to_wire(reqs, rng)
+        t = reqs["timestamp"].copy()
+        q, sig, st = wire.decode_requests(msgs, timestamps=t, strict=False)
+        if b == len(sizes) - 1:  # signed batch: identities with known keys
+            for k in range(n):
+                x = xs.setdefault(k, signer.randrange(1, sr.L))
+                pk = sr.public_key(x)
+                c = rng.bytes(32)
+                chal[base + k] = np.frombuffer(c, np.uint8)
+                f = dict(rt=int(reqs[k]["request_type"]), auth=pk,
+                         sig=sr.sign(x, c, signer.randrange(1, sr.L)) if k % 2 == 0 else rng.bytes(64),
+                         id=bytes(reqs[k]["msg_id"]), rc=bytes(reqs[k]["recipient"]),
+                         pl=bytes(reqs[k]["payload"]))
+                msgs[k] = wire_cases.canonical(f)
+            q, sig, st = wire.decode_requests(msgs, timestamps=t, strict=False)
+            for k in range(n):
+                if st[k] == 0 and not sr.verify(bytes(q[k]["auth_identity"]), bytes(chal[base + k]),
+                                                bytes(sig[k])):
+                    q[k]["request_type"] = 0
+                    st[k] = abi.WIRE_BAD_SIGNATURE
+        wants.append(([wire.encode_response(r) for r in model.process_batch(q)], st))
+        batches.append(msgs)
+        times.append(t)
+    # challenges are all-or-none per call: the unsigned batches in one call,
+    # the signed one in a second
+    got = store.process_wire_batches(batches[:-1], np.concatenate(times[:-1]), in_stride=1104)
+    got += store.process_wire_batches(batches[-1:], times[-1], in_stride=1104, challenges=chal[base:])
+    assert len(got) == len(sizes)
+    for b, ((g, gst), (w, wst)) in enumerate(zip(got, wants)):
+        assert len(g) == sizes[b]
+        assert (gst == wst).all(), b
+        bad = [k for k in range(len(w)) if g[k] != w[k]]
+        assert not bad, f"batch {b}: {len(bad)} responses differ (first {bad[:5]})"
+    assert (wants[-1][1] == abi.WIRE_BAD_SIGNATURE).sum() >= 10
+    st_ = store.stats()
+    assert (st_["messages"], st_["mailboxes"]) == (model.messages, model.mailboxes)
+    store.close()
