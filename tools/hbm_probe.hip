@@ -2,12 +2,14 @@
 // message-table pass's access shape (1 KiB rows, 16 B per lane, every row read
 // and written back once).  Not part of the product; run on the GPU box:
 //   hipcc -O3 --offload-arch=gfx950 -o tools/hbm_probe tools/hbm_probe.hip
-//   tools/hbm_probe [GiB]
+//   tools/hbm_probe [GiB]      (the pass shapes on one buffer)
+//   tools/hbm_probe sweep      (read-only and copy rates against buffer size)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -80,6 +82,35 @@ __global__ __launch_bounds__(256, MINW) void k_pipe(v4u* a, uint32_t rows) {
   }
 }
 
+// k_pipe with a per-workgroup start: workgroup b begins its waves' streams at
+// chunk (b * STAG) mod chunks and wraps, so that at any moment the grid's
+// accesses are not all at one offset of equal, power-of-two-strided partitions
+template <int U, int STAG, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_pipe_stag(v4u* a, uint32_t rows) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v4u* part = a + (size_t)blockIdx.x * rows * 64;
+  const uint32_t per_wave = rows / 4, chunks = per_wave / U;
+  v4u* w = part + (size_t)wave * per_wave * 64;
+  const uint32_t c0 = (blockIdx.x * STAG) % chunks;
+  v4u cur[U], nxt[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) cur[u] = ld<true>(&w[(size_t)(c0 * U + u) * 64 + lane]);
+  for (uint32_t i = 0; i < chunks; ++i) {
+    const uint32_t c = (c0 + i) % chunks, cn = (c + 1) % chunks;
+    if (i + 1 < chunks) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) nxt[u] = ld<true>(&w[(size_t)(cn * U + u) * 64 + lane]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cur[u].x ^= 1u;
+      st<true>(&w[(size_t)(c * U + u) * 64 + lane], cur[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+  }
+}
+
 // grid-stride with U independent 16-B accesses in flight per thread: thread t
 // of block b handles elements (b * U + u) * 256 + t, then jumps the grid
 template <int U, bool NT, bool COPY>
@@ -95,6 +126,22 @@ __global__ __launch_bounds__(256) void k_wide(const v4u* s, v4u* d, size_t n) {
       if (base + u * 256 < n) st<NT>(d + base + u * 256, v[u]);
     }
   }
+}
+
+// read only: U independent 16-B loads per thread per step, XOR-folded into one
+// word per thread (stored once, so the loads are not dead)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_read(const v4u* s, uint32_t* out, size_t n) {
+  const size_t step = (size_t)gridDim.x * U * 256;
+  uint32_t acc = 0;
+  for (size_t base = (size_t)blockIdx.x * U * 256 + threadIdx.x; base < n; base += step) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = base + u * 256 < n ? ld<NT>(s + base + u * 256) : v4u{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
 // out-of-place copy, grid-stride
@@ -136,7 +183,38 @@ static void timeit(const char* name, double bytes, F launch) {
   std::fflush(stdout);
 }
 
+// `hbm_probe sweep`: read-only and copy rates against the buffer size, to
+// place the 16-GiB figures beside the guide's (float4 copy, smaller buffers)
+static int sweep() {
+  const size_t maxb = 16ull << 30;
+  v4u* a;
+  uint32_t* o;
+  CK(hipMalloc(&a, maxb));
+  CK(hipMalloc(&o, 8192 * 256 * 4));
+  CK(hipMemset(a, 1, maxb));
+  for (double gib : {0.125, 0.5, 1.0, 4.0, 16.0}) {
+    const size_t bytes = (size_t)(gib * (1ull << 30)), n = bytes / 16, h = n / 2;
+    char nm[64];
+    for (int g : {2048, 8192}) {
+      std::snprintf(nm, sizeof nm, "%.3g GiB read U8 nt grid=%d", gib, g);
+      timeit(nm, (double)bytes, [&] { hipLaunchKernelGGL((k_read<8, true>), dim3(g), dim3(256), 0, 0, a, o, n); });
+      std::snprintf(nm, sizeof nm, "%.3g GiB read U8 plain grid=%d", gib, g);
+      timeit(nm, (double)bytes, [&] { hipLaunchKernelGGL((k_read<8, false>), dim3(g), dim3(256), 0, 0, a, o, n); });
+    }
+    std::snprintf(nm, sizeof nm, "%.3g GiB copy float4 plain grid=4096", gib);
+    timeit(nm, 2.0 * h * 16, [&] { hipLaunchKernelGGL(k_copy<false>, dim3(4096), dim3(256), 0, 0, a, a + h, h); });
+    std::snprintf(nm, sizeof nm, "%.3g GiB copy U8 nt grid=8192", gib);
+    timeit(nm, 2.0 * h * 16, [&] { hipLaunchKernelGGL((k_wide<8, true, true>), dim3(8192), dim3(256), 0, 0, a, a + h, h); });
+    std::snprintf(nm, sizeof nm, "%.3g GiB inplace U8 nt grid=8192", gib);
+    timeit(nm, 2.0 * bytes, [&] { hipLaunchKernelGGL((k_wide<8, true, false>), dim3(8192), dim3(256), 0, 0, a, a, n); });
+  }
+  CK(hipFree(a));
+  CK(hipFree(o));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
   const double gib = argc > 1 ? std::atof(argv[1]) : 16.0;
   const size_t bytes = (size_t)(gib * (1ull << 30));
   const size_t n = bytes / 16;
@@ -166,6 +244,12 @@ int main(int argc, char** argv) {
     timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe<4, true, 4>), dim3(nb), dim3(256), 0, 0, a, rows); });
     std::snprintf(nm, sizeof nm, "pipe U16 nt w1 rows=%u", rows);
     timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe<16, true, 1>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "pipe U8 nt stag1 rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe_stag<8, 1, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "pipe U8 nt stag7 rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe_stag<8, 7, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "pipe U8 nt stag0 rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe_stag<8, 0, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
   }
   // copy between two halves
   const size_t h = n / 2;
