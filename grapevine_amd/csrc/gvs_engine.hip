@@ -1697,7 +1697,11 @@ static void enqueue_wire_decode(gvs_handle* h, const void* d_wire, uint32_t stri
   if (!n) return;
   WireDecArgs a{(const uint8_t*)d_wire, stride, n, d_lens, d_times, (uint4*)d_reqs,
                 (uint4*)d_sigs, d_status};
-  hipLaunchKernelGGL(k_wire_decode, dim3((n + 3) / 4), dim3(256), 0, h->stream, a);
+  const uint32_t lds = wire_decode_lds(stride);
+  if (lds > 65536u)  // past the default dynamic-LDS limit (kWireSlotMax strides)
+    (void)hipFuncSetAttribute((const void*)k_wire_decode, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)wire_decode_lds(kWireSlotMax));
+  hipLaunchKernelGGL(k_wire_decode, dim3((n + kWireMsgs - 1) / kWireMsgs), dim3(64), lds, h->stream, a);
 }
 
 static void enqueue_wire_encode(gvs_handle* h, const void* d_resps, uint32_t n, void* d_wire,

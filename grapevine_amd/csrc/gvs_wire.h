@@ -30,9 +30,10 @@
 // (grapevine.proto:57-64).  Encoding writes the proto3 bytes prost would
 // write; a hard-error response (status 0) has length 0.
 //
-// One wave per message.  Every wave reads its whole input slot (stride
-// bytes) and writes its whole output slab, so the HBM traffic depends on n
-// and the strides only; the field walk itself runs on the wave's LDS copy.
+// Decode: one wave per kWireMsgs messages, staged whole in LDS, one lane's
+// field walk per message; encode: one wave per message.  Every message's
+// whole input slot (stride bytes) is read and its whole output slab written,
+// so the HBM traffic depends on n and the strides only.
 #pragma once
 #include "gvs_device.h"
 #include "gvs_route.h"
@@ -71,37 +72,92 @@ struct Varint {
   uint64_t v;
   uint32_t next;  // position after the varint
   bool ok;        // prost decode_varint accepts it (at most 10 bytes, the 10th <= 1, inside lim)
+  uint32_t w0;    // the 4 bytes at the varint's start (a fixed32 read at the same place)
 };
 
-__device__ inline Varint varint_at(const uint8_t* m, uint32_t p, uint32_t lim) {
-  Varint r{0, p, false};
-  bool done = false;
-#pragma unroll
-  for (uint32_t c = 0; c < 10; ++c) {
-    const uint32_t b = m[min(p + c, kWireSlotMax - 1u)];
-    const bool take = !done && p + c < lim;
-    r.v |= take ? (uint64_t)(b & 0x7Fu) << (7 * c) : 0ull;
-    const bool last = take && b < 0x80u;
-    r.ok = last ? !(c == 9 && b > 1u) : r.ok;
-    r.next = last ? p + c + 1 : r.next;
-    done = done || last || !take;
-  }
+// Encode stage: one slot plus slack for the 5-dword window reads.
+constexpr uint32_t kWireStage = kWireSlotMax + 32;
+
+// 16 bytes at byte offset p of a dword-aligned LDS stage: five aligned dword
+// reads and byte funnel shifts (no byte loads, no divergence).
+__device__ inline uint4 lds_bytes16(const uint8_t* m, uint32_t p) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(m) + (p >> 2);
+  const uint32_t sh = p & 3u, d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                    __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+}
+
+// The 7-bit groups of 8 varint bytes, packed (56 bits).
+__device__ inline uint64_t varint_pack8(uint64_t w) {
+  uint64_t y = w & 0x7f7f7f7f7f7f7f7full;
+  y = (y & 0x007f007f007f007full) | ((y >> 1) & 0x3f803f803f803f80ull);
+  y = (y & 0x00003fff00003fffull) | ((y >> 2) & 0x0fffc0000fffc000ull);
+  y = (y & 0x000000000fffffffull) | ((y >> 4) & 0x00fffffff0000000ull);
+  return y;
+}
+
+// The varint at message offset p (bytes at or past lim do not count) of the
+// message at byte `base` of the stage, from one 16-byte window: the
+// terminator is the first byte below 0x80, found with a mask over 8 bytes at
+// once; bytes 9 and 10 are handled apart.  Same results as a byte-by-byte
+// decode, in a fixed instruction count.
+__device__ inline Varint varint_at(const uint8_t* m, uint32_t base, uint32_t p, uint32_t lim) {
+  const uint4 win = lds_bytes16(m, base + p);
+  const uint64_t w = (uint64_t)win.y << 32 | win.x;
+  const uint32_t b8 = win.z & 0xFFu, b9 = (win.z >> 8) & 0xFFu;
+  const uint32_t n = lim > p ? lim - p : 0u;  // bytes inside the limit
+  const uint64_t inlim = n >= 8u ? ~0ull : ((1ull << (8u * n)) - 1ull);
+  const uint64_t term = ~w & 0x8080808080808080ull & inlim;
+  const uint32_t i = term ? (uint32_t)__builtin_ctzll(term) >> 3 : 8u;  // first terminator (8: none)
+  const uint64_t keep = i >= 7u ? ~0ull : ((1ull << (8u * (i + 1u))) - 1ull);
+  const uint64_t lo = varint_pack8(w & keep);
+  const bool t8 = i == 8u && n >= 9u && b8 < 0x80u;
+  const bool t9 = i == 8u && !t8 && n >= 10u && b8 >= 0x80u && b9 < 0x80u;
+  Varint r;
+  r.v = lo | (i == 8u ? (uint64_t)(b8 & 0x7Fu) << 56 : 0ull) | (t9 ? (uint64_t)(b9 & 1u) << 63 : 0ull);
+  r.ok = i < 8u || t8 || (t9 && b9 <= 1u);
+  r.next = i < 8u ? p + i + 1u : (t8 ? p + 9u : (t9 ? p + 10u : p));
+  r.w0 = win.x;
   return r;
 }
 
-__global__ void __launch_bounds__(256) k_wire_decode(WireDecArgs a) {
-  __shared__ uint8_t stage[4][kWireSlotMax];
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t k = blockIdx.x * 4u + wv;
-  const bool live = k < a.n;
-  uint8_t* m = stage[wv];
-  const uint8_t* src = a.in + (uint64_t)k * a.stride;
-  if (live)
-    for (uint32_t b = lane; b < a.stride; b += 64) m[b] = src[b];
-  __syncthreads();
-  if (!live) return;
+// Messages per decode workgroup (one wave): the wave stages its messages'
+// slots in LDS as one contiguous copy, each lane walks one message, then the
+// whole wave assembles each message's gvs_request in turn.
+constexpr uint32_t kWireMsgs = 32;
 
-  uint32_t len = a.lens[k];
+// LDS bytes of one decode workgroup at slot stride `stride`.
+inline uint32_t wire_decode_lds(uint32_t stride) { return (kWireMsgs * stride + 32u + 15u) & ~15u; }
+
+__global__ void __launch_bounds__(64) k_wire_decode(WireDecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t m[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t k0 = blockIdx.x * kWireMsgs;
+  const uint32_t nm = min(kWireMsgs, a.n - k0);  // messages of this wave
+  {
+    // the wave's slots are contiguous in HBM and in the stage: 16 B per lane
+    // when the slots are 16-B aligned (the usual strides), else 4 B, else
+    // bytes (a kernel-wide choice)
+    const uint8_t* src = a.in + (uint64_t)k0 * a.stride;
+    const uint32_t total = nm * a.stride;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(a.in) | a.stride;
+    if ((al & 15u) == 0) {
+      for (uint32_t b = lane * 16u; b < total; b += 1024u)
+        *reinterpret_cast<uint4*>(m + b) = *reinterpret_cast<const uint4*>(src + b);
+    } else if ((al & 3u) == 0) {
+      for (uint32_t b = lane * 4u; b < total; b += 256u)
+        *reinterpret_cast<uint32_t*>(m + b) = *reinterpret_cast<const uint32_t*>(src + b);
+    } else {
+      for (uint32_t b = lane; b < total; b += 64u) m[b] = src[b];
+    }
+  }
+  __syncthreads();
+
+  // lane i < nm walks message k0 + i; the other lanes walk an empty message
+  const bool mine = lane < nm;
+  const uint32_t k = k0 + (mine ? lane : 0u);
+  const uint32_t base = mine ? lane * a.stride : 0u;
+  uint32_t len = mine ? a.lens[k] : 0u;
   bool err = len > a.stride;
   len = err ? 0u : len;
   // last offset and length of each field (length kNone: absent)
@@ -118,13 +174,11 @@ __global__ void __launch_bounds__(256) k_wire_decode(WireDecArgs a) {
     done = done || (!idle && at_end && !depth);
     const bool field = !idle && !at_end;
     // the key, then the varint / fixed / length that follows it (all read)
-    const Varint kv = varint_at(m, p, lim);
+    const Varint kv = varint_at(m, base, p, lim);
     const uint32_t wt = (uint32_t)(kv.v & 7u);
     const uint64_t tag = kv.v >> 3;
-    const Varint vv = varint_at(m, kv.next, lim);
-    const uint32_t q = min(kv.next, kWireSlotMax - 4u);
-    const uint32_t fx = (uint32_t)m[q] | (uint32_t)m[q + 1] << 8 | (uint32_t)m[q + 2] << 16 |
-                        (uint32_t)m[q + 3] << 24;
+    const Varint vv = varint_at(m, base, kv.next, lim);
+    const uint32_t fx = vv.w0;  // a fixed32 at kv.next
     const bool known = depth ? (tag >= 1 && tag <= 3) : (tag >= 1 && tag <= 4);
     const uint32_t want = (!depth && tag == 1) ? 5u : 2u;
     const uint32_t sz = wt == 1 ? 8u : 4u;
@@ -157,49 +211,49 @@ __global__ void __launch_bounds__(256) k_wire_decode(WireDecArgs a) {
   const bool sizes = l_auth == 32u && l_sig == 64u && l_id == 16u && l_rc == 32u &&
                      l_pl == kWirePayload;
   const uint32_t st = err ? kWireDecodeError : (sizes ? kWireOk : kWireBadField);
+  // stage positions of the fields (a failed message reads its own slot start;
+  // the reads stay inside the stage, the values are not used)
   const bool ok = st == kWireOk;
-  if (!ok) o_id = o_auth = o_rc = o_pl = o_sig = 0;  // keep the reads inside the stage
-  const uint64_t ts = a.times[k];
+  o_id = base + (ok ? o_id : 0u);
+  o_auth = base + (ok ? o_auth : 0u);
+  o_rc = base + (ok ? o_rc : 0u);
+  o_pl = base + (ok ? o_pl : 0u);
+  o_sig = base + (ok ? o_sig : 0u);
+  const uint64_t ts = mine ? a.times[k] : 0ull;
 
   // gvs_request: msg_id | auth_identity | recipient | timestamp | payload |
-  // request_type | reserved.  Lane u writes 16-B unit u (lane 0 also unit 64).
-  auto unit = [&](uint32_t u) -> uint4 {
-    uint32_t wds[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t j = u * 16u + (uint32_t)q * 4u + (uint32_t)c;
-        uint32_t byte;
-        if (j < 16u) byte = m[o_id + j];
-        else if (j < 48u) byte = m[o_auth + j - 16u];
-        else if (j < 80u) byte = m[o_rc + j - 48u];
-        else if (j < 88u) byte = (uint32_t)(ts >> (8u * (j - 80u))) & 0xFFu;
-        else if (j < 1024u) byte = m[o_pl + j - 88u];
-        else if (j < 1028u) byte = (rt >> (8u * (j - 1024u))) & 0xFFu;
-        else byte = 0;
-        v |= byte << (8 * c);
-      }
-      wds[q] = ok ? v : 0u;
+  // request_type | reserved.  For each message in turn, lane u writes 16-B
+  // unit u (lane 0 also unit 64): unit 0 is msg_id, 1-2 auth_identity, 3-4
+  // recipient, 5 the timestamp and payload bytes 0-7, 6-63 payload bytes
+  // 16u-88 on; 64 request_type.
+  const uint32_t u = lane;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (uint32_t i = 0; i < nm; ++i) {
+    const uint32_t st_i = __builtin_amdgcn_readlane(st, i);
+    const bool ok_i = st_i == kWireOk;
+    const uint32_t id_i = __builtin_amdgcn_readlane(o_id, i);
+    const uint32_t au_i = __builtin_amdgcn_readlane(o_auth, i);
+    const uint32_t rc_i = __builtin_amdgcn_readlane(o_rc, i);
+    const uint32_t pl_i = __builtin_amdgcn_readlane(o_pl, i);
+    const uint32_t sg_i = __builtin_amdgcn_readlane(o_sig, i);
+    const uint32_t rt_i = __builtin_amdgcn_readlane(rt, i);
+    const uint32_t tlo = __builtin_amdgcn_readlane((uint32_t)ts, i);
+    const uint32_t thi = __builtin_amdgcn_readlane((uint32_t)(ts >> 32), i);
+    const uint32_t at = u == 0 ? id_i
+                      : u <= 2 ? au_i + 16u * (u - 1u)
+                      : u <= 4 ? rc_i + 16u * (u - 3u)
+                      : u == 5 ? pl_i : pl_i + 16u * u - 88u;
+    uint4 v = lds_bytes16(m, at);
+    v = u == 5 ? make_uint4(tlo, thi, v.x, v.y) : v;
+    uint4* dst = a.out + (uint64_t)(k0 + i) * kAbiU4;
+    dst[lane] = ok_i ? v : z;
+    if (lane == 0) dst[64] = ok_i ? make_uint4(rt_i, 0, 0, 0) : z;
+    if (a.sigs && lane < 4) {
+      const uint4 sg = lds_bytes16(m, sg_i + 16u * lane);
+      a.sigs[(uint64_t)(k0 + i) * 4u + lane] = ok_i ? sg : z;
     }
-    return make_uint4(wds[0], wds[1], wds[2], wds[3]);
-  };
-  uint4* dst = a.out + (uint64_t)k * kAbiU4;
-  dst[lane] = unit(lane);
-  if (lane == 0) dst[64] = unit(64);
-  if (a.sigs && lane < 4) {
-    uint32_t wds[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v |= (uint32_t)m[o_sig + lane * 16u + q * 4u + c] << (8 * c);
-      wds[q] = ok ? v : 0u;
-    }
-    a.sigs[(uint64_t)k * 4u + lane] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
   }
-  if (a.status && lane == 0) a.status[k] = st;
+  if (a.status && mine) a.status[k] = st;
 }
 
 struct WireEncArgs {
@@ -213,51 +267,86 @@ struct WireEncArgs {
 // 3: recipient, 4: timestamp (omitted when 0), 5: payload}, then status_code
 // (2).  Status 0 (a hard error) has no response message: length 0, zero bytes.
 __global__ void __launch_bounds__(256) k_wire_encode(WireEncArgs a) {
-  __shared__ uint8_t stage[4][kAbiU4 * 16];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4][kAbiU4 * 16 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t image[4][kWireStage];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t k = blockIdx.x * 4u + wv;
   const bool live = k < a.n;
   uint8_t* r = stage[wv];
+  uint8_t* im = image[wv];
+  const uint32_t* r32 = reinterpret_cast<const uint32_t*>(r);
   const uint4* src = a.in + (uint64_t)k * kAbiU4;
   if (live) {
     reinterpret_cast<uint4*>(r)[lane] = src[lane];
     if (lane == 0) reinterpret_cast<uint4*>(r)[64] = src[64];
   }
   __syncthreads();
-  if (!live) return;
-  const uint32_t status = *reinterpret_cast<const uint32_t*>(r + 1024);
-  uint64_t ts = 0;
-  for (int c = 0; c < 8; ++c) ts |= (uint64_t)r[80 + c] << (8 * c);
-  const uint32_t t = ts ? 9u : 0u;
-  const uint32_t reclen = 1025u + t;            // 1034 with a timestamp
-  const uint32_t base = 89u + t;                // payload field header
-  const uint32_t total = status ? base + 944u : 0u;
-  uint8_t* dst = a.out + (uint64_t)k * a.stride;
-  for (uint32_t j = lane; j < a.stride; j += 64) {
-    uint32_t b;
-    if (j == 0) b = 0x0A;
-    else if (j == 1) b = (reclen & 0x7Fu) | 0x80u;
-    else if (j == 2) b = reclen >> 7;
-    else if (j == 3) b = 0x0A;
-    else if (j == 4) b = 0x10;
-    else if (j < 21) b = r[j - 5];               // msg_id
-    else if (j == 21) b = 0x12;
-    else if (j == 22) b = 0x20;
-    else if (j < 55) b = r[16 + j - 23];         // sender
-    else if (j == 55) b = 0x1A;
-    else if (j == 56) b = 0x20;
-    else if (j < 89) b = r[48 + j - 57];         // recipient
-    else if (t && j == 89) b = 0x21;
-    else if (t && j < 98) b = r[80 + j - 90];    // timestamp
-    else if (j == base) b = 0x2A;
-    else if (j == base + 1) b = 0xA8;
-    else if (j == base + 2) b = 0x07;
-    else if (j < base + 939) b = r[88 + j - base - 3];  // payload
-    else if (j == base + 939) b = 0x15;
-    else if (j < base + 944) b = r[1024 + j - base - 940];  // status_code
-    else b = 0;
-    dst[j] = (uint8_t)(j < total ? b : 0u);
+  uint32_t total = 0;
+  if (live) {
+    // the response slab as prost writes it, built in LDS a dword per lane
+    const uint32_t status = r32[256];
+    const uint64_t ts = (uint64_t)r32[21] << 32 | r32[20];
+    const uint32_t t = ts ? 9u : 0u;
+    const uint32_t reclen = 1025u + t;            // 1034 with a timestamp
+    const uint32_t base = 89u + t;                // payload field header
+    const uint32_t e = base + 939u;               // status_code field
+    const uint32_t delta = base + 3u - 88u;       // payload: out[j] = r[j - delta]
+    total = status ? base + 944u : 0u;
+    auto hdr_byte = [&](uint32_t j) -> uint32_t {  // bytes 0-127: fields before the payload body
+      if (j == 0) return 0x0A;
+      if (j == 1) return (reclen & 0x7Fu) | 0x80u;
+      if (j == 2) return reclen >> 7;
+      if (j == 3) return 0x0A;
+      if (j == 4) return 0x10;
+      if (j < 21) return r[j - 5];                // msg_id
+      if (j == 21) return 0x12;
+      if (j == 22) return 0x20;
+      if (j < 55) return r[16 + j - 23];          // sender
+      if (j == 55) return 0x1A;
+      if (j == 56) return 0x20;
+      if (j < 89) return r[48 + j - 57];          // recipient
+      if (t && j == 89) return 0x21;
+      if (t && j < 98) return r[80 + j - 90];     // timestamp
+      if (j == base) return 0x2A;
+      if (j == base + 1) return 0xA8;
+      if (j == base + 2) return 0x07;
+      return r[j - delta];                        // payload
+    };
+    const uint32_t nd = (a.stride + 3u) >> 2;
+    for (uint32_t i = lane; i < nd; i += 64u) {
+      const uint32_t j = 4u * i;
+      uint32_t w = 0;
+      if (j < 128u) {
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) w |= (j + c < total ? hdr_byte(j + c) : 0u) << (8 * c);
+      } else {
+        // payload bytes, then the status_code field (0x15 + fixed32), then zeros
+        const uint32_t o = min(j - delta, 1024u);
+        const uint32_t pay = __builtin_amdgcn_alignbyte(r32[(o >> 2) + 1], r32[o >> 2], o & 3u);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+          const uint32_t jj = j + c, x = jj - e;
+          const uint32_t tb = x == 0 ? 0x15u : (status >> (8u * (x - 1u))) & 0xFFu;
+          const uint32_t b = jj < e ? (pay >> (8 * c)) & 0xFFu : tb;
+          w |= (jj < total ? b : 0u) << (8 * c);
+        }
+      }
+      reinterpret_cast<uint32_t*>(im)[i] = w;
+    }
   }
+  __syncthreads();
+  if (!live) return;
+  // slab -> output slot: head bytes to a 4-B boundary, dwords, tail bytes
+  uint8_t* dst = a.out + (uint64_t)k * a.stride;
+  const uint32_t h = (4u - (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u;
+  const uint32_t nb = (a.stride - h) >> 2, t0 = h + 4u * nb;
+  const uint32_t* im32 = reinterpret_cast<const uint32_t*>(im);
+  if (lane < h) dst[lane] = im[lane];
+  for (uint32_t i = lane; i < nb; i += 64u) {
+    const uint32_t o = h + 4u * i;
+    *reinterpret_cast<uint32_t*>(dst + o) = __builtin_amdgcn_alignbyte(im32[(o >> 2) + 1], im32[o >> 2], o & 3u);
+  }
+  if (t0 + lane < a.stride) dst[t0 + lane] = im[t0 + lane];
   if (lane == 0) a.lens[k] = total;
 }
 
