@@ -306,6 +306,31 @@ GVS_SR_FN Pt pt_add(const Pt& p, const Pt& q) {
   return Pt{fe_mul(e, f), fe_mul(g, h), fe_mul(f, g), fe_mul(e, h)};
 }
 
+// An addend in cached form (Y - X, Y + X, 2Z, 2dT): adding it costs 8
+// multiplies instead of 9 and no sums of its coordinates.
+struct PtC {
+  Fe ymx, ypx, z2, t2d;
+};
+
+GVS_SR_FN PtC pt_cache(const Pt& q) {
+  return PtC{fe_sub(q.Y, q.X), fe_add(q.Y, q.X), fe_add(q.Z, q.Z), fe_mul(q.T, fe_d2())};
+}
+
+// p + q, the same formula as pt_add with q's sums and products precomputed
+GVS_SR_FN Pt pt_add_c(const Pt& p, const PtC& q) {
+  const Fe a = fe_mul(fe_sub(p.Y, p.X), q.ymx);
+  const Fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
+  const Fe c = fe_mul(p.T, q.t2d);
+  const Fe d = fe_mul(p.Z, q.z2);
+  const Fe e = fe_sub(b, a), f = fe_sub(d, c), g = fe_add(d, c), h = fe_add(b, a);
+  return Pt{fe_mul(e, f), fe_mul(g, h), fe_mul(f, g), fe_mul(e, h)};
+}
+
+GVS_SR_FN PtC ptc_select(uint32_t m, const PtC& a, const PtC& b) {
+  return PtC{fe_select(m, a.ymx, b.ymx), fe_select(m, a.ypx, b.ypx), fe_select(m, a.z2, b.z2),
+             fe_select(m, a.t2d, b.t2d)};
+}
+
 // dbl-2008-hwcd, a = -1
 GVS_SR_FN Pt pt_dbl(const Pt& p) {
   const Fe a = fe_sq(p.X), b = fe_sq(p.Y);
@@ -418,10 +443,13 @@ GVS_SR_FN void shl1(Fe& x) {
 
 // s*B - k*A for scalars below 2^253: one joint double-and-add from bit 252,
 // fixed 253 steps, the addend selected by masks from {0, B, -A, B - A}
+// (cached form)
 GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A) {
-  const Pt B = pt_base();
-  const Pt nA = pt_neg(A);
-  const Pt BnA = pt_add(B, nA);
+  const Pt Bp = pt_base();
+  const PtC B = pt_cache(Bp);
+  const PtC nA = pt_cache(pt_neg(A));
+  const PtC BnA = pt_cache(pt_add(Bp, pt_neg(A)));
+  const PtC O = pt_cache(pt_identity());
   Pt acc = pt_identity();
   Fe sw = s, kw = k;  // bit 252 moved to the top, then shifted out one per step
   for (int i = 0; i < 3; ++i) {
@@ -434,9 +462,9 @@ GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A) {
     const uint32_t kb = 0u - (kw.v[7] >> 31);
     shl1(sw);
     shl1(kw);
-    Pt q = pt_select(kb, nA, pt_identity());
-    q = pt_select(sb, pt_select(kb, BnA, B), q);
-    acc = pt_add(acc, q);
+    PtC q = ptc_select(kb, nA, O);
+    q = ptc_select(sb, ptc_select(kb, BnA, B), q);
+    acc = pt_add_c(acc, q);
   }
   return acc;
 }
