@@ -442,26 +442,14 @@ GVS_SR_FN void shl1(Fe& x) {
 }
 
 // s*B - k*A for scalars below 2^253: one joint double-and-add from bit 252,
-// fixed 253 steps, the addend chosen by masks from {0, B, -A, B - A} (cached
-// form).  The two per-signature addends live in `tab` (64 words at stride
-// `ts`: LDS on the device, so that they do not hold 64 registers through the
-// loop), B's in `btab` (32 words, shared by every thread); every step reads
-// all of them and selects, so the instruction and LDS-access sequence does
-// not depend on the scalars.
-GVS_SR_FN void ptc_store(uint32_t* t, uint32_t ts, const PtC& q) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    t[(0 + i) * ts] = q.ymx.v[i];
-    t[(8 + i) * ts] = q.ypx.v[i];
-    t[(16 + i) * ts] = q.z2.v[i];
-    t[(24 + i) * ts] = q.t2d.v[i];
-  }
-}
-
-GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A, uint32_t* tab, uint32_t ts,
-                                  const uint32_t* btab) {
-  ptc_store(tab, ts, pt_cache(pt_neg(A)));
-  ptc_store(tab + 32 * ts, ts, pt_cache(pt_add(pt_base(), pt_neg(A))));
+// fixed 253 steps, the addend selected by masks from {0, B, -A, B - A}
+// (cached form)
+GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A) {
+  const Pt Bp = pt_base();
+  const PtC B = pt_cache(Bp);
+  const PtC nA = pt_cache(pt_neg(A));
+  const PtC BnA = pt_cache(pt_add(Bp, pt_neg(A)));
+  const PtC O = pt_cache(pt_identity());
   Pt acc = pt_identity();
   Fe sw = s, kw = k;  // bit 252 moved to the top, then shifted out one per step
   for (int i = 0; i < 3; ++i) {
@@ -474,24 +462,8 @@ GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A, uint32_
     const uint32_t kb = 0u - (kw.v[7] >> 31);
     shl1(sw);
     shl1(kw);
-    // kb ? (sb ? B - A : -A) : (sb ? B : 0); the cached identity is (1, 1, 2, 0)
-    uint32_t w[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const uint32_t o = (j == 0 || j == 8) ? 1u : (j == 16 ? 2u : 0u);
-      const uint32_t na = tab[j * ts], bna = tab[(32 + j) * ts];
-      const uint32_t with_a = (bna & sb) | (na & ~sb);
-      const uint32_t no_a = (btab[j] & sb) | (o & ~sb);
-      w[j] = (with_a & kb) | (no_a & ~kb);
-    }
-    PtC q;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      q.ymx.v[i] = w[i];
-      q.ypx.v[i] = w[8 + i];
-      q.z2.v[i] = w[16 + i];
-      q.t2d.v[i] = w[24 + i];
-    }
+    PtC q = ptc_select(kb, nA, O);
+    q = ptc_select(sb, ptc_select(kb, BnA, B), q);
     acc = pt_add_c(acc, q);
   }
   return acc;
@@ -623,11 +595,8 @@ GVS_SR_FN uint32_t ld_le32(const uint8_t* p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
-__global__ void __launch_bounds__(kSrThreads, 2) k_sr_verify(SrArgs a) {
-  // per thread: the Keccak state (50 words) while hashing, then the ladder's
-  // two cached addends (64 words); plus B's cached form, shared
-  __shared__ uint32_t sponge[64 * kSrThreads];
-  __shared__ uint32_t btab[32];
+__global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
+  __shared__ uint32_t sponge[50 * kSrThreads];
   const uint32_t tid = threadIdx.x;
   const uint32_t k = blockIdx.x * kSrThreads + tid;
   const uint32_t kk = k < a.n ? k : a.n - 1;  // tail threads redo the last signature
@@ -700,9 +669,7 @@ __global__ void __launch_bounds__(kSrThreads, 2) k_sr_verify(SrArgs a) {
   const Pt A = ristretto_decode(A_s, &pk_ok);
   ok &= pk_ok;
 
-  if (tid == 0) ptc_store(btab, 1, pt_cache(pt_base()));  // B cached, shared
-  __syncthreads();
-  const Pt acc = double_scalar_mul(sc, kc, A, sponge + tid, kSrThreads, btab);
+  const Pt acc = double_scalar_mul(sc, kc, A);
   const Fe enc = ristretto_encode(acc);
   uint32_t diff = 0;
 #pragma unroll
