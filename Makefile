@@ -21,7 +21,7 @@ $(TESTLIB): $(SRCS) $(HDRS)
 
 # the device signature-check arithmetic built for the CPU (tests/test_sr_host.py)
 $(SRHOST): tests/sr_host.cpp grapevine_amd/csrc/gvs_sr25519.h grapevine_amd/csrc/gvs_device.h
-	$(HIPCC) -O2 -std=c++17 -fPIC -shared --cuda-host-only -o $@ tests/sr_host.cpp
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -o $@ tests/sr_host.cpp
 
 oracle:
 	$(MAKE) -C oracle
