@@ -318,15 +318,20 @@ def front_end(torch, store, dev, batches, nreq, B):
     h_olen = np.zeros(len(h_in), np.uint32)
     applied = ctypes.c_uint32(0)
 
-    def host_call(k):
+    h_chal = np.random.default_rng(7).integers(0, 256, (len(h_in), 32), dtype=np.uint8)
+
+    def host_call(k, chal=None):
         store._check(store.lib.gvs_process_wire_batches(
             store.h, h_in.ctypes.data, W_IN, h_lens.ctypes.data, counts.ctypes.data, k,
-            h_times.ctypes.data, None, h_out.ctypes.data, wire.RESPONSE_WIRE_BYTES,
-            h_olen.ctypes.data, None, ctypes.byref(applied)))
-    host_call(1)  # first use allocates the pipeline's buffers
+            h_times.ctypes.data, None if chal is None else chal.ctypes.data, h_out.ctypes.data,
+            wire.RESPONSE_WIRE_BYTES, h_olen.ctypes.data, None, ctypes.byref(applied)))
+    host_call(1, h_chal)  # first use allocates the pipeline's buffers (and loads the verifier)
     t0 = time.perf_counter()
     host_call(len(batches))
     t_h = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    host_call(len(batches), h_chal)
+    t_hc = time.perf_counter() - t0
     # batched signature check over B random (pk, 32-B challenge, signature)
     g = torch.Generator(device=dev)
     g.manual_seed(99)
@@ -354,6 +359,12 @@ def front_end(torch, store, dev, batches, nreq, B):
                                   "api": "gvs_process_wire_batches (pageable host buffers, one call, "
                                          "double-buffered; PCIe-inclusive)",
                                   "responses_1042B": int((h_olen == 1042).sum())},
+            "wire_batches_host_checked": {"value": nreq * len(batches) / t_hc, "unit": "req/s",
+                                          "ms_per_batch": t_hc / len(batches) * 1e3,
+                                          "api": "gvs_process_wire_batches with per-request challenges "
+                                                 "(decode, schnorrkel check, store, encode per batch)",
+                                          "note": "random challenges: every signature fails (hard "
+                                                  "errors); the store's work is fixed per batch"},
             "wire_batch_checked": {"value": nreq * len(batches) / t_c, "unit": "req/s",
                                    "ms_per_batch": t_c / len(batches) * 1e3,
                                    "api": "gvs_process_wire_batch_device with per-request challenges "
