@@ -20,9 +20,10 @@
 // One thread per signature.  Field elements are 8 x 32-bit limbs kept below
 // 2^256 (lazy: reduced to [0, p) only for comparisons and encodings), products
 // schoolbook with 64-bit multiply-adds and a 2^256 = 38 fold.  The scalar
-// multiplication is a joint double-and-add over both scalars (Shamir), fixed
-// 253 steps with masked table selects; the transcript's STROBE state lives in
-// LDS (one 200-byte column per thread).  No branch depends on the signature,
+// multiplication runs fixed signed radix-8 windows over both scalars
+// (Straus: 252 doublings, 170 additions) with masked table selects; the
+// transcript's STROBE state, then the per-signature table, live in LDS (one
+// column per thread).  No branch depends on the signature,
 // key or message: every thread runs the same instruction stream.
 #pragma once
 #include "gvs_device.h"
@@ -342,6 +343,18 @@ GVS_SR_FN Pt pt_dbl(const Pt& p) {
   return Pt{fe_mul(e, f), fe_mul(g, h), fe_mul(f, g), fe_mul(e, h)};
 }
 
+// the same doubling without T, for a result that is only doubled again
+// (dbl-2008-hwcd reads X, Y, Z)
+GVS_SR_FN Pt pt_dbl_noT(const Pt& p) {
+  const Fe a = fe_sq(p.X), b = fe_sq(p.Y);
+  const Fe zz = fe_sq(p.Z);
+  const Fe c = fe_add(zz, zz);
+  const Fe d = fe_neg(a);
+  const Fe e = fe_sub(fe_sub(fe_sq(fe_add(p.X, p.Y)), a), b);
+  const Fe g = fe_add(d, b), f = fe_sub(g, c), h = fe_sub(d, b);
+  return Pt{fe_mul(e, f), fe_mul(g, h), fe_mul(f, g), fe_zero()};
+}
+
 GVS_SR_FN Pt pt_neg(const Pt& p) { return Pt{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
 
 GVS_SR_FN Pt pt_select(uint32_t m, const Pt& a, const Pt& b) {
@@ -441,32 +454,104 @@ GVS_SR_FN void shl1(Fe& x) {
   x.v[0] <<= 1;
 }
 
-// s*B - k*A for scalars below 2^253: one joint double-and-add from bit 252,
-// fixed 253 steps, the addend selected by masks from {0, B, -A, B - A}
-// (cached form)
-GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A) {
-  const Pt Bp = pt_base();
-  const PtC B = pt_cache(Bp);
-  const PtC nA = pt_cache(pt_neg(A));
-  const PtC BnA = pt_cache(pt_add(Bp, pt_neg(A)));
-  const PtC O = pt_cache(pt_identity());
-  Pt acc = pt_identity();
-  Fe sw = s, kw = k;  // bit 252 moved to the top, then shifted out one per step
-  for (int i = 0; i < 3; ++i) {
-    shl1(sw);
-    shl1(kw);
+GVS_SR_FN void ptc_store(uint32_t* t, uint32_t ts, const PtC& q) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    t[(0 + i) * ts] = q.ymx.v[i];
+    t[(8 + i) * ts] = q.ypx.v[i];
+    t[(16 + i) * ts] = q.z2.v[i];
+    t[(24 + i) * ts] = q.t2d.v[i];
   }
-  for (int b = 252; b >= 0; --b) {
-    acc = pt_dbl(acc);
-    const uint32_t sb = 0u - (sw.v[7] >> 31);
-    const uint32_t kb = 0u - (kw.v[7] >> 31);
-    shl1(sw);
-    shl1(kw);
-    PtC q = ptc_select(kb, nA, O);
-    q = ptc_select(sb, ptc_select(kb, BnA, B), q);
-    acc = pt_add_c(acc, q);
+}
+
+// {P, 2P, 3P, 4P} in cached form at t (entry j at word 32j, stride ts)
+GVS_SR_FN void ptc_table4(uint32_t* t, uint32_t ts, const Pt& P) {
+  const Pt P2 = pt_dbl(P);
+  const Pt P3 = pt_add(P2, P);
+  ptc_store(t, ts, pt_cache(P));
+  ptc_store(t + 32 * ts, ts, pt_cache(P2));
+  ptc_store(t + 64 * ts, ts, pt_cache(P3));
+  ptc_store(t + 96 * ts, ts, pt_cache(pt_dbl(P2)));
+}
+
+// Signed radix-8 digits of a scalar below 2^253: 85 digits in [-4, 4],
+// digit i in 4-bit field i of dig (magnitude bits 0-2, sign bit 3).
+GVS_SR_FN void sc_digits8(const Fe& x, uint32_t dig[11]) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 11; ++w) dig[w] = 0;
+#pragma unroll
+  for (int i = 0; i < 85; ++i) {
+    const int bit = 3 * i, wd = bit >> 5, sh = bit & 31;
+    uint32_t v = x.v[wd] >> sh;
+    if (sh > 29 && wd < 7) v |= x.v[wd + 1] << (32 - sh);
+    v = (v & 7u) + carry;
+    carry = v > 4u ? 1u : 0u;
+    const uint32_t neg = carry, mag = neg ? 8u - v : v;  // v - 8 when carrying
+    dig[i >> 3] |= (mag | (neg << 3)) << (4 * (i & 7));
+  }
+}
+
+// The cached addend for digit d of table t: |d| selects among the identity
+// and the 4 entries (all read), the sign swaps Y - X / Y + X and negates 2dT.
+GVS_SR_FN PtC ptc_digit(const uint32_t* t, uint32_t ts, uint32_t d) {
+  const uint32_t mag = d & 7u, neg = 0u - ((d >> 3) & 1u);
+  uint32_t w[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    uint32_t v = (j == 0 || j == 8) ? 1u : (j == 16 ? 2u : 0u);  // cached identity (1, 1, 2, 0)
+#pragma unroll
+    for (uint32_t e = 0; e < 4; ++e) {
+      const uint32_t m = 0u - (uint32_t)(mag == e + 1u);
+      v = (t[(32 * e + j) * ts] & m) | (v & ~m);
+    }
+    w[j] = v;
+  }
+  PtC q;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    q.ymx.v[i] = (w[8 + i] & neg) | (w[i] & ~neg);
+    q.ypx.v[i] = (w[i] & neg) | (w[8 + i] & ~neg);
+    q.z2.v[i] = w[16 + i];
+    q.t2d.v[i] = w[24 + i];
+  }
+  q.t2d = fe_select(neg, fe_neg(q.t2d), q.t2d);
+  return q;
+}
+
+// s*B - k*A for scalars below 2^253: fixed signed radix-8 windows over both
+// scalars (Straus), 85 digits each, 252 doublings and 170 additions of cached
+// addends; btab holds {B, 2B, 3B, 4B} (shared by every thread), atab gets
+// {-A, -2A, -3A, -4A} (this thread's, 128 words at stride ts).  Every digit
+// reads all table entries and selects, so the instruction and LDS-access
+// sequence does not depend on the scalars.
+GVS_SR_FN_NI Pt double_scalar_mul(const Fe& s, const Fe& k, const Pt& A, uint32_t* atab, uint32_t ts,
+                                  const uint32_t* btab) {
+  ptc_table4(atab, ts, pt_neg(A));
+  uint32_t ds[11], dk[11];
+  sc_digits8(s, ds);
+  sc_digits8(k, dk);
+  Pt acc = pt_identity();
+  for (int i = 84; i >= 0; --i) {
+    // the table reads stay inside the loop: hoisted, they would hold 256
+    // registers for its whole length
+    __asm__ volatile("" ::: "memory");
+    if (i < 84) {
+      acc = pt_dbl_noT(acc);
+      acc = pt_dbl_noT(acc);
+      acc = pt_dbl(acc);
+    }
+    acc = pt_add_c(acc, ptc_digit(atab, ts, (dk[i >> 3] >> (4 * (i & 7))) & 15u));
+    acc = pt_add_c(acc, ptc_digit(btab, 1, (ds[i >> 3] >> (4 * (i & 7))) & 15u));
   }
   return acc;
+}
+
+// Host form (tests/sr_host.cpp): the tables in local arrays.
+inline Pt double_scalar_mul_host(const Fe& s, const Fe& k, const Pt& A) {
+  uint32_t atab[128], btab[128];
+  ptc_table4(btab, 1, pt_base());
+  return double_scalar_mul(s, k, A, atab, 1, btab);
 }
 
 // ------------------------------------------------------------ STROBE / merlin
@@ -596,7 +681,11 @@ GVS_SR_FN uint32_t ld_le32(const uint8_t* p) {
 }
 
 __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
-  __shared__ uint32_t sponge[50 * kSrThreads];
+  // per thread: the Keccak state (50 words) while hashing, then this
+  // signature's -A table (128 words); plus the B table, shared
+  __shared__ uint32_t sponge[128 * kSrThreads];
+  __shared__ uint32_t btab[128];
+  if (threadIdx.x == 0) ptc_table4(btab, 1, pt_base());
   const uint32_t tid = threadIdx.x;
   const uint32_t k = blockIdx.x * kSrThreads + tid;
   const uint32_t kk = k < a.n ? k : a.n - 1;  // tail threads redo the last signature
@@ -669,7 +758,8 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   const Pt A = ristretto_decode(A_s, &pk_ok);
   ok &= pk_ok;
 
-  const Pt acc = double_scalar_mul(sc, kc, A);
+  __syncthreads();  // btab written
+  const Pt acc = double_scalar_mul(sc, kc, A, sponge + tid, kSrThreads, btab);
   const Fe enc = ristretto_encode(acc);
   uint32_t diff = 0;
 #pragma unroll

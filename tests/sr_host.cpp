@@ -26,7 +26,7 @@ extern "C" {
 int sr_host_combine(const uint8_t* s, const uint8_t* k, const uint8_t* pk, uint8_t* out) {
   uint32_t ok = 0;
   const Pt A = ristretto_decode(fe_from(pk), &ok);
-  fe_to(ristretto_encode(double_scalar_mul(fe_from(s), fe_from(k), A)), out);
+  fe_to(ristretto_encode(double_scalar_mul_host(fe_from(s), fe_from(k), A)), out);
   return ok ? 1 : 0;
 }
 
