@@ -230,3 +230,42 @@ def test_wire_batches_pipelined():
     st_ = store.stats()
     assert (st_["messages"], st_["mailboxes"]) == (model.messages, model.mailboxes)
     store.close()
+
+
+def test_wire_pipeline_stops_at_failing_batch():
+    """gvs_process_wire_batches on a 4-shard store: a batch that overflows a
+    router bucket stops the pipeline there (the batches before it applied,
+    it and the later one not), as gvs_process_batches does."""
+    from grapevine_amd.store import GvsError
+    S = 4
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024,
+                          shard_count=S, route_capacity=320)
+    store, cl = ObliviousStore(cfg), ffi.Cluster(cfg)
+    cl.seed(15)
+    p = ffi.gen_params(n_identities=300)
+    hot = ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60, n_identities=300)
+    ok = [cl.gen_batch(S * 1024, p) for _ in range(2)]
+    for b in ok:
+        cl.process_batch(b)
+    bad = cl.gen_batch(S * 1024, hot)
+    assert cl.process_batch(bad) is None
+    later = cl.gen_batch(S * 1024, p)
+
+    def msgs(b):
+        q = b.copy()
+        q["request_type"][q["request_type"] == 0] = 0xFFFFFFFF  # still a hard error
+        return [m.tobytes() for m in wire.encode_requests(q)]
+
+    batches = ok + [bad, later]
+    times = np.concatenate([b["timestamp"] for b in batches])
+    with pytest.raises(GvsError) as ei:
+        store.process_wire_batches([msgs(b) for b in batches], times, in_stride=1104)
+    assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW and ei.value.applied == 2
+    assert store.stats()["messages"] == cl.messages
+    assert store.stats()["batches"] == 2
+    # `later` was not applied: it runs now, as the oracle's next batch
+    got = store.process_wire_batches([msgs(later)], later["timestamp"], in_stride=1104)
+    w = cl.process_batch(later)
+    assert got[0][0] == [wire.encode_response(r) for r in w]
+    assert store.dump_messages().tobytes() == cl.dump_messages().tobytes()
+    store.close()
