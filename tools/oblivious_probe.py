@@ -129,6 +129,7 @@ def main():
     p.add_argument("--identities", type=int, default=5000)
     p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
     p.add_argument("--wire", action="store_true", help="wire path with challenge check")
+    p.add_argument("--seed", type=int, default=1234, help="generator seed of the measured batches")
     a = p.parse_args()
     assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
     S = a.shards if a.shards > 1 else 0
@@ -147,7 +148,7 @@ def main():
         want = model.process_batch(reqs)
         got = store.process_batch(reqs)
         assert got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
-    model.seed(1234)  # same request-generator state for every mix
+    model.seed(a.seed)  # same request-generator state for every mix
     params = ffi.gen_params(n_identities=a.identities, bad_auth=0, bad_recipient=0, hard_error=0,
                             zero_recipient=0, **{"miss": 0, **MIXES[a.mix]})
     for _ in range(a.batches):
