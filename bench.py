@@ -332,6 +332,15 @@ def front_end(torch, store, dev, batches, nreq, B):
     t0 = time.perf_counter()
     host_call(len(batches), h_chal)
     t_hc = time.perf_counter() - t0
+    # the same with the slabs in pinned memory (copied without staging)
+    p_in = store.host_array(h_in.size, np.uint8).reshape(h_in.shape)
+    p_out = store.host_array(h_out.size, np.uint8).reshape(h_out.shape)
+    p_in[:] = h_in
+    h_in, h_out = p_in, p_out
+    host_call(1)
+    t0 = time.perf_counter()
+    host_call(len(batches))
+    t_hp = time.perf_counter() - t0
     # batched signature check over B random (pk, 32-B challenge, signature)
     g = torch.Generator(device=dev)
     g.manual_seed(99)
@@ -358,7 +367,9 @@ def front_end(torch, store, dev, batches, nreq, B):
                                   "ms_per_batch": t_h / len(batches) * 1e3, "batches": len(batches),
                                   "api": "gvs_process_wire_batches (pageable host buffers, one call, "
                                          "double-buffered; PCIe-inclusive)",
-                                  "responses_1042B": int((h_olen == 1042).sum())},
+                                  "responses_1042B": int((h_olen == 1042).sum()),
+                                  "pinned_req_s": nreq * len(batches) / t_hp,
+                                  "pinned_ms_per_batch": t_hp / len(batches) * 1e3},
             "wire_batches_host_checked": {"value": nreq * len(batches) / t_hc, "unit": "req/s",
                                           "ms_per_batch": t_hc / len(batches) * 1e3,
                                           "api": "gvs_process_wire_batches with per-request challenges "

@@ -1912,6 +1912,9 @@ int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_strid
   HostPipe& hp = h->pipe;
   hipStream_t s = h->stream;
   if (int r = reset_errors(h)) return r;
+  // message and response slabs in pinned memory (gvs_host_alloc) are copied
+  // to and from directly; pageable ones go through the pinned staging pair
+  const bool pin_in = is_pinned(in), pin_out = is_pinned(out);
   HostState snap[2];
   uint64_t off[2] = {0, 0}, next_off = 0;
   uint32_t enq = 0;
@@ -1926,13 +1929,14 @@ int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_strid
     if (more) {  // enqueue batch t in slot b
       const uint32_t b = t & 1u, n = counts[t];
       if (t >= 2) GVS_HIP(h, hipEventSynchronize(p.h2d[b]));  // staging b free again
-      par_memcpy(p.hin[b], in + next_off * in_stride, (size_t)n * in_stride);
+      const uint8_t* src = pin_in ? in + next_off * in_stride : p.hin[b];
+      if (!pin_in) par_memcpy(p.hin[b], in + next_off * in_stride, (size_t)n * in_stride);
       std::memcpy(p.hlens[b], in_lens + next_off, (size_t)n * 4);
       std::memcpy(p.htimes[b], times + next_off, (size_t)n * 8);
       if (challenges) std::memcpy(p.hchal[b], challenges + next_off * 32, (size_t)n * 32);
       if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(hp.copy, p.done[b], 0));  // device slot b consumed
       if (n) {
-        GVS_HIP(h, hipMemcpyAsync(p.din[b], p.hin[b], (size_t)n * in_stride, hipMemcpyHostToDevice, hp.copy));
+        GVS_HIP(h, hipMemcpyAsync(p.din[b], src, (size_t)n * in_stride, hipMemcpyHostToDevice, hp.copy));
         GVS_HIP(h, hipMemcpyAsync(p.dlens[b], p.hlens[b], (size_t)n * 4, hipMemcpyHostToDevice, hp.copy));
         GVS_HIP(h, hipMemcpyAsync(p.dtimes[b], p.htimes[b], (size_t)n * 8, hipMemcpyHostToDevice, hp.copy));
         if (challenges)
@@ -1953,7 +1957,8 @@ int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_strid
       GVS_HIP(h, hipEventRecord(p.done[b], s));
       GVS_HIP(h, hipStreamWaitEvent(hp.copy_out, p.done[b], 0));
       if (n) {
-        GVS_HIP(h, hipMemcpyAsync(p.hout[b], p.dout[b], (size_t)n * out_stride, hipMemcpyDeviceToHost, hp.copy_out));
+        GVS_HIP(h, hipMemcpyAsync(pin_out ? out + next_off * out_stride : p.hout[b], p.dout[b],
+                                  (size_t)n * out_stride, hipMemcpyDeviceToHost, hp.copy_out));
         GVS_HIP(h, hipMemcpyAsync(p.holens[b], p.dolens[b], (size_t)n * 4, hipMemcpyDeviceToHost, hp.copy_out));
         GVS_HIP(h, hipMemcpyAsync(p.hstat[b], p.dstat[b], (size_t)n * 4, hipMemcpyDeviceToHost, hp.copy_out));
       }
@@ -1973,7 +1978,7 @@ int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_strid
         GVS_HIP(h, hipStreamSynchronize(hp.copy_out));
         return decode_error(h, e);
       }
-      par_memcpy(out + off[pb] * out_stride, p.hout[pb], (size_t)n * out_stride);
+      if (!pin_out) par_memcpy(out + off[pb] * out_stride, p.hout[pb], (size_t)n * out_stride);
       std::memcpy(out_lens + off[pb], p.holens[pb], (size_t)n * 4);
       if (decode_status) std::memcpy(decode_status + off[pb], p.hstat[pb], (size_t)n * 4);
       if (applied) *applied = t;

@@ -271,7 +271,9 @@ int gvs_process_wire_batch(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
  * while batch t is processed).  Batch t has counts[t] messages; the messages
  * of all batches are consecutive in `in` (and in in_lens, times, challenges),
  * their results likewise in out / out_lens / decode_status.  Stops at the
- * first failing batch: its error is returned, *applied = the batches before. */
+ * first failing batch: its error is returned, *applied = the batches before.
+ * `in` and `out` in pinned memory (gvs_host_alloc) are copied without
+ * staging. */
 int gvs_process_wire_batches(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
                              const uint32_t *in_lens, const uint32_t *counts, uint32_t k,
                              const uint64_t *times, const uint8_t *challenges, uint8_t *out,

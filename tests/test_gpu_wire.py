@@ -269,3 +269,43 @@ def test_wire_pipeline_stops_at_failing_batch():
     assert got[0][0] == [wire.encode_response(r) for r in w]
     assert store.dump_messages().tobytes() == cl.dump_messages().tobytes()
     store.close()
+
+
+def test_wire_batches_pinned_slabs():
+    """gvs_process_wire_batches with the message and response slabs in pinned
+    memory (gvs_host_alloc: copied without staging) gives the same bytes as
+    the oracle, batch by batch."""
+    import ctypes
+    store, model = small_store()
+    model.seed(37)
+    params = ffi.gen_params(n_identities=200, hot=10)
+    rng = np.random.default_rng(23)
+    sizes = [1024, 300, 1024]
+    msgs, times, wants = [], [], []
+    for n in sizes:
+        reqs = model.gen_batch(n, params)
+        m = to_wire(reqs, rng)
+        t = reqs["timestamp"].copy()
+        q, _, _ = wire.decode_requests(m, timestamps=t, strict=False)
+        wants += [wire.encode_response(r) for r in model.process_batch(q)]
+        msgs += m
+        times.append(t)
+    total, stride = len(msgs), 1104
+    slab = store.host_array(total * stride, np.uint8).reshape(total, stride)
+    out = store.host_array(total * 1042, np.uint8).reshape(total, 1042)
+    slab[:] = 0
+    for k, m in enumerate(msgs):
+        slab[k, :len(m)] = np.frombuffer(m, np.uint8)
+    lens = np.array([len(m) for m in msgs], np.uint32)
+    t = np.concatenate(times)
+    counts = np.array(sizes, np.uint32)
+    olens = np.zeros(total, np.uint32)
+    applied = ctypes.c_uint32(0)
+    store._check(store.lib.gvs_process_wire_batches(
+        store.h, slab.ctypes.data, stride, lens.ctypes.data, counts.ctypes.data, len(sizes),
+        t.ctypes.data, None, out.ctypes.data, 1042, olens.ctypes.data, None, ctypes.byref(applied)))
+    assert applied.value == len(sizes)
+    got = [out[k, :olens[k]].tobytes() for k in range(total)]
+    bad = [k for k in range(total) if got[k] != wants[k]]
+    assert not bad, f"{len(bad)} responses differ (first {bad[:5]})"
+    store.close()
