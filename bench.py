@@ -420,6 +420,12 @@ def main():
                               expiry_per_batch=a.expiry)
         store = ObliviousStore(cfg)
     shard_batch = store.stats()["shard_batch"]
+    # what the data path spans, from the store's own RCCL communicator
+    # (ncclCommCount / ncclCommUserRank; 0 / -1 without one), and every rank's
+    # shard pipeline size and bucket capacity
+    per_rank = gdist.gather_ints(ri, [store.get_option("rccl_ranks"), store.get_option("rccl_rank"),
+                                      shard_batch, store.stats()["route_capacity"],
+                                      store.get_option("txn_slots")], device=dev)
     if a.auth:
         store.set_option("sealed_pass_waves", a.sealed_waves)
     g = torch.Generator(device=dev)
@@ -539,8 +545,11 @@ def main():
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            if (tj.get("kernel") == "k_rpass2" and tj.get("log2n") == a.log2n and tj.get("batch") == B
-                    and world == 1 and not a.auth):
+            # the pass's bytes depend on N, W and c only: attach
+            # the file's figure when it was measured at the same N and slot
+            # count, whatever the rank count
+            if (tj.get("kernel") == "k_rpass2" and tj.get("log2n") == a.log2n and not a.auth
+                    and tj.get("txn_slots", c if tj.get("batch") == B else None) == c):
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -592,6 +601,9 @@ def main():
                        "parallelism": f"shards{world}",
                        "route_capacity": store.stats()["route_capacity"],
                        "shard_batch": shard_batch, "auth_storage": bool(a.auth),
+                       "rccl_ranks": per_rank[0][0],
+                       "per_rank": [{"rccl_rank": r[1], "rccl_ranks": r[0], "shard_batch": r[2],
+                                     "route_capacity": r[3], "txn_slots": r[4]} for r in per_rank],
                        "expiry_per_batch": a.expiry},
             "roofline": roofline,
             # SURVEY.md §8(d) whole-batch figure: message table and mailbox table

@@ -112,8 +112,8 @@ struct Engine {
   uint4* pbuf = nullptr;     // B x 1 KiB final row states, by sorted position
   uint4* psd = nullptr;      // B side entries of P (target row, valid), 128 B each
   uint4* ptag = nullptr;     // B tags of P (authenticated storage)
-  uint4* pdum = nullptr;     // W*c x 1 KiB read for unused slots
-  uint4* snapdummy = nullptr;  // B x 1 KiB
+  uint4* ps = nullptr;       // W*c x 1 KiB final states by slot (AUTH: + W*c x 128 B side entries)
+  uint4* snapp = nullptr;    // B x 1 KiB row snapshots at their first op's position
   uint4* dryb = nullptr;     // W x 1 KiB
   RtxV* rtx_agg = nullptr;
   RtxV* rtx_carry = nullptr;
@@ -123,16 +123,14 @@ struct Engine {
   uint4* m2g = nullptr;      // B x 128 B (gvs_mtx.h k_m2g)
   uint4* idn = nullptr;      // B x 128 B request identity lines (k_meta -> k_rr1)
   uint4* snapid = nullptr;   // W*c x 128 B snapshot identity lines (k_rpass2 -> k_rr1)
-  uint4* siddummy = nullptr; // B x 128 B
-  uint4* vraw = nullptr;     // B/64 x 2 KiB: raw rows of each block's defining op (k_rr2)
-  uint4* vdef = nullptr;     // B/64 x 128 B: its position in the block
+  uint4* snapidp = nullptr;  // B x 128 B their identity lines (k_rpass2 -> k_rr1)
   uint4* vagg = nullptr, *vagg2 = nullptr, *vcarry2 = nullptr, *vcarry = nullptr;
   // fixed-slot mailbox passes (gvs_mtx.h)
   uint32_t cm = 0;           // group slots per mailbox partition
   uint4* mpos = nullptr;     // B
   uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
   uint4* msnap = nullptr;    // Q*cm x 1 KiB
-  uint4* mdummy = nullptr;   // B x 1 KiB
+  uint4* msnapp = nullptr;   // B x 1 KiB (group snapshots by head position)
   uint4* mdry = nullptr;     // Q x 1 KiB
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
@@ -547,8 +545,8 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(pbuf, (uint64_t)B * 64);
     A(psd, (uint64_t)B * 8);
     if (h->auth) A(ptag, B);
-    A(pdum, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
-    A(snapdummy, (uint64_t)B * 64);
+    A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
+    A(snapp, (uint64_t)B * 64);
     A(dryb, (uint64_t)e.W * 64);
     A(rtx_agg, B / kScanT);
     A(rtx_carry, B / kScanT);
@@ -558,9 +556,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(m2g, (uint64_t)B * 8);
     A(idn, (uint64_t)B * 8);
     A(snapid, WC * 8);
-    A(siddummy, (uint64_t)B * 8);
-    A(vraw, (uint64_t)(B / kVBlk) * 128);
-    A(vdef, (uint64_t)(B / kVBlk) * 8);
+    A(snapidp, (uint64_t)B * 8);
     const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
     A(vagg, nvb * kVLineU4);
     A(vcarry, nvb * kVLineU4);
@@ -570,7 +566,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(mpos, B);
     A(gtx, (QC + B) * 8);
     A(msnap, QC * 64);
-    A(mdummy, (uint64_t)B * 64);
+    A(msnapp, (uint64_t)B * 64);
     A(mdry, (uint64_t)e.Q * 64);
     A(m2tx, (QC + B) * kVLineU4);
     A(gtx_agg, B / kScanT);
@@ -789,6 +785,20 @@ static AllocArgs aargs(const Engine& e) {
   return a;
 }
 
+// Diagnostic kernel variants (GVS_DIAG bits; honoured by the test library only,
+// results are then wrong by design: tools/gpu_pmc_mix.sh attribution runs).
+#ifdef GVS_TEST_HOOKS
+static uint32_t diag_bits() {
+  static const uint32_t d = [] {
+    const char* v = std::getenv("GVS_DIAG");
+    return v ? (uint32_t)std::strtoul(v, nullptr, 0) : 0u;
+  }();
+  return d;
+}
+#else
+static uint32_t diag_bits() { return 0u; }
+#endif
+
 // ------------------------------------------- pipeline 2: fixed-slot transactions
 
 static MArgs margs2(const gvs_handle* h, const Engine& e) {
@@ -796,6 +806,7 @@ static MArgs margs2(const gvs_handle* h, const Engine& e) {
   a.gtx = e.gtx;
   a.m2tx = e.m2tx;
   a.msnap = e.msnap;
+  a.msnapp = e.msnapp;
   a.mdry = e.mdry;
   a.stamp = e.stamp_run;
   a.cm = e.cm;
@@ -823,7 +834,8 @@ static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
 }
 
 static PsealArgs pargs(const gvs_handle* h, const Engine& e, uint32_t ep) {
-  return PsealArgs{e.pbuf, e.psd, e.ptag, seal_of(h, e), h->te, e.scal, ep};
+  return PsealArgs{e.pbuf, e.psd, e.ptag, seal_of(h, e), h->te, e.scal, ep,
+                   e.ps, e.ps + (uint64_t)e.W * e.c * 64, e.W * e.c};
 }
 
 // Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
@@ -862,11 +874,11 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     vscan_fields(a, e);
     a.mpos = e.mpos;
     a.ops = e.ops;
-    a.msnap = e.msnap;
-    a.mdummy = e.mdummy;
+    a.msnapp = e.msnapp;
     a.m1out = e.m1out;
     a.N = e.N;
     a.kc = e.kc;
+    a.diag = diag_bits();
     vscan_abc<M1rOp>(s, a);
     hipLaunchKernelGGL(k_m1r_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
@@ -903,12 +915,12 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.tprev = e.tbuf[e.par ^ 1];
   a.stamp_cur = e.stamp_run;
   a.stamp_prev = e.stamp_prev;
-  a.pbuf = e.pbuf;
-  a.psd = e.psd;
-  a.pdum = e.pdum;
-  a.psdum = h->auth ? e.pdum + (uint64_t)e.W * e.c * 64 : nullptr;
+  a.ps = e.ps;
+  a.psds = h->auth ? e.ps + (uint64_t)e.W * e.c * 64 : nullptr;
   a.snap = e.snap;
   a.snapid = e.snapid;
+  a.snapp = e.snapp;
+  a.snapidp = e.snapidp;
   a.dry = e.dryb;
   a.scal = e.scal;
   a.W = e.W;
@@ -926,7 +938,8 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     a.sc = seal_of(h, e);
     a.te = h->te;
     a.mtag = e.mtag;
-    // the previous batch's P (sealed at this epoch) is unsealed in place first
+    // the previous batch's P (sealed at this epoch, by position) is unsealed
+    // first, each row's final state to its slot's line of PS
     if (e.stamp_prev != kNone)
       hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
     mark(h, "punseal");
@@ -945,8 +958,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   launch_rpass2(h, e);
   mark(h, "rpass");
   {
-    Rr1Args a{e.rpos, e.rop, e.img, e.snap, e.snapdummy, e.rsb, e.rr1_agg, e.rr1_carry, e.scal,
-              B,      B / kScanT, B - e.X, e.S, e.rr1g, 0u, e.idn, e.snapid, e.siddummy};
+    Rr1Args a{e.rpos, e.rop, e.rsb, e.rr1_agg, e.rr1_carry, e.scal, B, B / kScanT, B - e.X, e.S,
+              e.rr1g, 0u, e.idn, e.snapidp};
     hipLaunchKernelGGL(k_scan_a<Rr1Op>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_b<Rr1Op>, dim3(1), dim3(kScanT), 0, s, a);
     a.pass = 1;
@@ -957,13 +970,11 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     Rr2Args a{};
     vscan_fields(a, e);
     a.rs = e.rsb;
-    a.vraw = e.vraw;
-    a.vdef = e.vdef;
     a.img = e.img;
-    a.snap = e.snap;
-    a.snapdummy = e.snapdummy;
+    a.snapp = e.snapp;
     a.pbuf = e.pbuf;
     a.psd = e.psd;
+    a.ps = h->auth ? nullptr : e.ps;  // AUTH: all by position, sealed, scattered by the unseal
     a.resp = e.resp;
     a.rres = e.rres;
     a.B = B;
@@ -1257,11 +1268,12 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   A(rpos, B);
   for (int k = 0; k < 2; ++k) A(tbuf[k], (WC + B) * 8);
   A(snap, WC * 64);
-  A(snapdummy, (uint64_t)B * 64);
+  A(snapp, (uint64_t)B * 64);
   A(pbuf, (uint64_t)B * 64);
   A(psd, (uint64_t)B * 8);
-  A(pdum, WC * 64);
+  A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
   A(snapid, WC * 8);
+  A(snapidp, (uint64_t)B * 8);
   A(dryb, (uint64_t)e.W * 64);
   A(rtx_agg, B / kScanT);
   A(rtx_carry, B / kScanT);
@@ -1340,10 +1352,10 @@ static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     a.rpos = e.rpos;
     a.meta = e.kvmeta;
     a.img = e.img;
-    a.snap = e.snap;
-    a.snapdummy = e.snapdummy;
+    a.snapp = e.snapp;
     a.pbuf = e.pbuf;
     a.psd = e.psd;
+    a.ps = h->auth ? nullptr : e.ps;
     a.out = d_out;
     a.outdummy = e.kvdummy;
     a.n = n;
@@ -1417,10 +1429,10 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     a.rpos = e.rpos;
     a.meta = e.kvmeta;
     a.img = e.img;
-    a.snap = e.snap;
-    a.snapdummy = e.snapdummy;
+    a.snapp = e.snapp;
     a.pbuf = e.pbuf;
     a.psd = e.psd;
+    a.ps = h->auth ? nullptr : e.ps;
     a.out = e.resp;
     a.outdummy = e.kvdummy;
     a.n = n;
@@ -1664,6 +1676,12 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
         GVS_HIP(h, hipStreamSynchronize(s));  // batch t, if enqueued, did nothing
         GVS_HIP(h, hipStreamSynchronize(p.copy));
         GVS_HIP(h, hipStreamSynchronize(p.copy_out));
+        // the batches from the failed one on were not applied: their range of
+        // `out` (which a pinned caller buffer may have received stale device
+        // responses into) is zeroed, never left holding other batches' data
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < k; ++i) total += counts[i];
+        std::memset(out + off[pb], 0, (size_t)(total - off[pb]) * sizeof(gvs_response));
         return decode_error(h, e);
       }
       if (!pin_out)
@@ -1976,6 +1994,13 @@ int gvs_process_wire_batches(gvs_handle* h, const uint8_t* in, uint32_t in_strid
         GVS_HIP(h, hipStreamSynchronize(s));
         GVS_HIP(h, hipStreamSynchronize(hp.copy));
         GVS_HIP(h, hipStreamSynchronize(hp.copy_out));
+        // unapplied batches: zero their range of `out` and their lengths (a
+        // pinned `out` may have received stale device responses)
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < k; ++i) total += counts[i];
+        std::memset(out + off[pb] * out_stride, 0, (size_t)(total - off[pb]) * out_stride);
+        std::memset(out_lens + off[pb], 0, (size_t)(total - off[pb]) * 4);
+        if (decode_status) std::memset(decode_status + off[pb], 0, (size_t)(total - off[pb]) * 4);
         return decode_error(h, e);
       }
       if (!pin_out) par_memcpy(out + off[pb] * out_stride, p.hout[pb], (size_t)n * out_stride);
@@ -2099,7 +2124,16 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
   const Engine& e = h->eng[0];
   if (std::strcmp(key, "txn_slots") == 0) *value = e.c;
   else if (std::strcmp(key, "group_slots") == 0) *value = e.cm;
-  else return GVS_ERR_INVALID_ARG;
+  else if (std::strcmp(key, "rccl_ranks") == 0) {
+    // the store's own communicator (0 without one): what the data path spans
+    int n = 0;
+    if (h->comm && ncclCommCount(h->comm, &n) != ncclSuccess) return GVS_ERR_DEVICE;
+    *value = n;
+  } else if (std::strcmp(key, "rccl_rank") == 0) {
+    int r = -1;
+    if (h->comm && ncclCommUserRank(h->comm, &r) != ncclSuccess) return GVS_ERR_DEVICE;
+    *value = r;
+  } else return GVS_ERR_INVALID_ARG;
   return GVS_OK;
 }
 
@@ -2190,16 +2224,18 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
       for (uint64_t row = 0; row < N; ++row) unseal(phys.data() + row * 1024, 0u, row);
     if (e.stamp_prev != kNone) {
       // rows the last batch changed are pending in P (applied by the next pass):
-      // slot descriptor {row in partition, stamp, P position}
+      // slot descriptor {row in partition, stamp, P position, first position};
+      // plain stores keep the final state at the slot (PS), AUTH stores by
+      // position, sealed (P)
       const uint64_t WC = (uint64_t)e.W * e.c;
       std::vector<uint4> td(WC * 8);
-      std::vector<uint8_t> pv((uint64_t)e.B * 1024);
+      std::vector<uint8_t> pv(h->auth ? (uint64_t)e.B * 1024 : WC * 1024);
       GVS_HIP(h, hipMemcpy(td.data(), e.tbuf[e.par ^ 1], WC * 128, hipMemcpyDeviceToHost));
-      GVS_HIP(h, hipMemcpy(pv.data(), e.pbuf, pv.size(), hipMemcpyDeviceToHost));
+      GVS_HIP(h, hipMemcpy(pv.data(), h->auth ? e.pbuf : e.ps, pv.size(), hipMemcpyDeviceToHost));
       for (uint64_t k = 0; k < WC; ++k) {
         const uint4 d = td[k * 8];
         if (d.y != e.stamp_prev || d.x >= e.S || d.z >= e.B) continue;
-        uint8_t* src = pv.data() + (uint64_t)d.z * 1024;
+        uint8_t* src = pv.data() + (h->auth ? (uint64_t)d.z : k) * 1024;
         if (h->auth) unseal(src, 2u, d.z);
         std::memcpy(phys.data() + ((k / e.c) * e.S + d.x) * 1024, src, 1024);
       }

@@ -392,7 +392,8 @@ struct MArgs {
   // fixed-slot mailbox passes (gvs_mtx.h)
   const uint4* gtx;    // Q*cm group descriptors (128 B) of this batch
   const uint4* m2tx;   // Q*cm group results (1152 B) for the write pass
-  uint4* msnap;        // Q*cm group snapshots (1 KiB) from the read pass
+  uint4* msnap;        // Q*cm x 1 KiB: the read pass's sink for unused group slots
+  uint4* msnapp;       // B x 1 KiB: group snapshots at their heads' sorted positions
   uint4* mdry;         // Q x 1 KiB: each workgroup's dry-run line
   uint32_t stamp, cm;
 };

@@ -76,10 +76,11 @@ struct KvArgs {
   const uint4* rpos;       // B sorted positions (RtxOp)
   const uint4* meta;       // B x 128 B, by seq: {kind, e0, overflow, 0}
   const uint4* img;        // B x 1 KiB, by seq
-  const uint4* snap;       // W*c slot snapshots
-  const uint4* snapdummy;  // B x 1 KiB (non-heads read their own line)
-  uint4* pbuf;             // B final states, by position
-  uint4* psd;              // B x 128 B side entries {row lo, row hi, valid, 0}
+  const uint4* snapp;      // B x 1 KiB: row snapshots at their first op's position
+  uint4* pbuf;             // B x 1 KiB: final states of the positions that are not a row's last
+  uint4* psd;              // B x 128 B side entries {row lo, row hi, valid, slot}
+  uint4* ps;               // plain: W*c x 1 KiB, each row's final state at its slot (the pass
+                           // reads P by slot); AUTH: null (P by position, sealed)
   uint4* out;              // ORAM: n x 1 KiB (caller); OMAP: B x kRespSlot
   uint4* outdummy;         // ORAM: B x 1 KiB for padding ops
   uint32_t n, S, omap;
@@ -149,17 +150,19 @@ struct KvOp {
     const bool head = h.flags & kPosHead;
     return (o.x == kTConst && o.y == 1u) || (o.x == kTIfAbsent && !(head && h.e0));
   }
-  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4 f) {
+  // k_vscan_a: every op's two rows (its SNAPP line and its image) are read,
+  // the defining op's value kept: addresses that do not depend on the ops
+  __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4*) {
     const KvHdr h = kv_hdr(a, p);
-    const bool img = from_img(h);
     const bool head = h.flags & kPosHead;
-    const uint4* src = (head && !img) ? a.snap + (uint64_t)h.slot * 64 : a.img + (uint64_t)h.seq * 64;
-    const uint4 x = ld_row<false>(&src[lane_id()]);
+    const uint4 sv = ld_row<false>(&a.snapp[(uint64_t)p * 64 + lane_id()]);
+    const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane_id()]);
+    const uint4 x = sel4(head && !from_img(h), sv, iv);
     const uint4 o = own_f(h);
     const bool zero = (h.flags & kPosNull) || (o.x == kTConst && o.y == 0u) || (!head && o.x == kTId);
-    (void)f;
     return sel4(zero, make_uint4(0, 0, 0, 0), x);
   }
+  __device__ static uint4 value_fin(uint4, uint4 v) { return v; }
 };
 
 // k_kv_c: each wave walks its 16 ops from its carry: the state before the op
@@ -171,13 +174,12 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
   __shared__ uint4 s_f[4];
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
-  // each op's snapshot (heads) or own dummy line, and its image, read once
+  // each op's own SNAPP line (heads: the row's snapshot) and its image, read once
   uint4 svs[16], ivs[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const KvHdr h = kv_hdr(a, p0 + j);
-    const uint4* sp = (h.flags & kPosHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
-    svs[j] = ld_row<false>(&sp[lane]);
+    svs[j] = ld_row<false>(&a.snapp[(uint64_t)(p0 + j) * 64 + lane]);
     ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
   }
   uint4 cf, cv;
@@ -236,8 +238,12 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
     } else {
       st_drop(null ? a.outdummy : a.out, (uint64_t)h.seq * 64 + lane, v);
     }
-    st_drop(a.pbuf, (uint64_t)p * 64 + lane, v2);
-    sd = sel4(lane == j, make_uint4((uint32_t)h.prow, (uint32_t)(h.prow >> 32), last ? 1u : 0u, 0u), sd);
+    // a row's final state to its slot (the next pass reads P by slot), the
+    // other positions' states to their own P line: one write per position
+    // (AUTH: all by position, sealed next; the unseal moves them to PS)
+    const bool to_slot = a.ps && last;
+    st_drop(to_slot ? a.ps : a.pbuf, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, v2);
+    sd = sel4(lane == j, make_uint4((uint32_t)h.prow, (uint32_t)(h.prow >> 32), last ? 1u : 0u, h.slot), sd);
   }
   if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);
 }

@@ -141,7 +141,8 @@ struct GroupM {  // 64 B
   uint32_t n_del, n_create, fcs, len;
   int32_t slot;
   uint32_t flags, fl, n_succ, mlo, mhi;
-  uint32_t pad[2];
+  uint32_t head;  // sorted position of the group's first op (its snapshot line in MSNAPP)
+  uint32_t pad;
 };
 
 // group of (hi, glo) among g[0, ng) (sorted), or -1: a fixed-step search
@@ -207,7 +208,8 @@ __device__ inline uint32_t load_groups(const MArgs& a, uint32_t q, GroupM* g, ui
     G.n_succ = h.y;
     G.mlo = h.z;
     G.mhi = h.w;
-    G.pad[0] = G.pad[1] = 0;
+    G.head = r1.z;
+    G.pad = 0;
     g[k] = G;
     atomicAdd(s_ng, r0.x == a.stamp ? 1u : 0u);  // unconditional: no code path skipped
   }
@@ -269,6 +271,9 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     G.flags = (exists1 ? 1u : 0u) | ((isnew && rank < freeq) ? 2u : 0u);
   }
   __syncthreads();
+  // group snapshots go to MSNAPP at the head's sorted position, so that every
+  // op of k_m1r_c reads line p (an address stream that does not depend on the
+  // batch); unused slots write their own line of the MSNAP sink
   uint4* snap = a.msnap + (uint64_t)q * a.cm * 64;
   uint4* dry = a.mdry + (uint64_t)q * 64;
   for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
@@ -299,7 +304,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
       const GroupM& G = g[k];
       const uint4 hdr = make_uint4(G.len, G.fl, G.flags, (uint32_t)G.slot);
       cur = sel4(lane == 0, hdr, sel4(lane == 1, make_uint4(0, 0, 0, 0), cur));
-      uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
+      uint4* dst = dry_run ? dry : a.msnapp + (uint64_t)G.head * 64;
       st_drop(dst, lane, cur);
     }
 #pragma unroll
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     if (has_row) continue;
     const bool real = !dry_run && k < ng;
     const uint4 hdr = sel4(real, make_uint4(0u, G.fl, G.flags, (uint32_t)G.slot), make_uint4(0, 0, 0, 0));
-    uint4* dst = dry_run ? dry : snap + (uint64_t)k * 64;
+    uint4* dst = dry_run ? dry : real ? a.msnapp + (uint64_t)G.head * 64 : snap + (uint64_t)k * 64;
     st_drop(dst, lane, sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
   }
 }
@@ -326,11 +331,11 @@ struct M1rArgs {
   GVS_VSCAN_FIELDS
   const uint4* mpos;
   const OpState* ops;
-  const uint4* msnap;
-  const uint4* mdummy;  // B x 1 KiB
+  const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions
   M1Out* m1out;
   uint64_t N;
   KeyCtx kc;
+  uint32_t diag;  // diagnostic variants (test library only, GVS_DIAG)
 };
 
 struct M1rOp {
@@ -350,13 +355,16 @@ struct M1rOp {
                       (!null && cls == 1u) ? 1u : 0u, 0u);
   }
   __device__ static uint4 f_of(const Args& a, uint32_t p) { return f_of_pos(uni4(a.mpos[p]).x); }
-  __device__ static const uint4* src_of(const Args& a, uint32_t p, uint4 mp) {
-    return (mp.x & kMPosHead) ? a.msnap + (uint64_t)mp.y * 64 : a.mdummy + (uint64_t)p * 64;
+  // every op reads its own position's line (heads find their group's
+  // snapshot there; the others' lines are read and ignored)
+  __device__ static const uint4* src_of(const Args& a, uint32_t p, uint4) {
+    return a.msnapp + (uint64_t)p * 64;
   }
-  __device__ static uint4 value_of(const Args& a, uint32_t p, uint4) {
-    const uint4 mp = uni4(a.mpos[p]);
-    return ld_row<false>(&src_of(a, p, mp)[lane_id()]);
+  // k_vscan_a: every op's line is read, the defining op's kept
+  __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4*) {
+    return ld_row<false>(&src_of(a, p, make_uint4(0, 0, 0, 0))[lane_id()]);
   }
+  __device__ static uint4 value_fin(uint4, uint4 v) { return v; }
 };
 
 __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
   if (a.scal->error) return;
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
-  // each op's snapshot (heads) or own dummy line, read once
+  // each op's own MSNAPP line, read once
   uint4 As[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
     const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;
     const uint4 A = As[j];
-    const uint4 ol = line_load(a.ops + seq);  // OpState: id is 32-bit words 10..13
+    const uint4 ol = line_load(a.ops + ((a.diag & 2u) ? p : seq));  // OpState: id is 32-bit words 10..13
     const uint4 myid = make_uint4(line_u32(ol, 10), line_u32(ol, 11), line_u32(ol, 12), line_u32(ol, 13));
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 0u, 0u), cf);
     const uint4 pv = sel4(head, A, cv);

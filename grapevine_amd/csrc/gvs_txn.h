@@ -168,6 +168,8 @@ constexpr uint32_t kPosHead = 1u << 20, kPosLast = 1u << 21, kPosNull = 1u << 22
 struct RtxV {
   uint32_t reset;  // position starts a partition
   uint32_t cnt;    // row heads since the last partition start
+  uint32_t hp;     // position of the latest row head (kNone: none yet)
+  uint32_t pad;
 };
 
 struct RtxArgs {
@@ -186,9 +188,10 @@ struct RtxOp {
   // a batch that already failed (e.g. a slot overflow before its row keys
   // were written) stops here
   __device__ static bool stop(const Args& a) { return a.scal->error != 0u; }
-  __device__ static V identity() { return V{0u, 0u}; }
+  __device__ static V identity() { return V{0u, 0u, kNone, 0u}; }
   __device__ static V combine(const V& a, const V& b) {
-    return b.reset ? b : V{a.reset, a.cnt + b.cnt};
+    const uint32_t hp = b.hp != kNone ? b.hp : a.hp;
+    return b.reset ? V{b.reset, b.cnt, hp, 0u} : V{a.reset, a.cnt + b.cnt, hp, 0u};
   }
   __device__ static void row_of(const Args& a, uint32_t p, uint64_t& row, uint32_t& w) {
     const uint64_t k = a.rkeys[p];
@@ -202,7 +205,7 @@ struct RtxOp {
     row_of(a, p, row, w);
     if (p) row_of(a, p - 1, prow, pw);
     const bool head = row != kRNullRow && (p == 0 || row != prow);
-    return V{(uint32_t)(p == 0 || w != pw), head ? 1u : 0u};
+    return V{(uint32_t)(p == 0 || w != pw), head ? 1u : 0u, head ? p : kNone, 0u};
   }
   __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
     uint64_t row, nrow = ~0ull;
@@ -222,10 +225,12 @@ struct RtxOp {
     const uint32_t seq = (uint32_t)a.rkeys[p] & kSeqMask;
     a.rpos[p] = make_uint4(seq | (head ? kPosHead : 0u) | (last ? kPosLast : 0u) | (null ? kPosNull : 0u),
                            null ? kNone : w * a.c + kk, w, o);
-    // the row's LAST op writes the slot descriptor: the row, the stamp, and
-    // the position whose final state (k_rr2_c) the next pass applies
+    // the row's LAST op writes the slot descriptor: the row, the stamp, the
+    // position whose final state (k_rr2_c) the next pass applies, and the
+    // row's first op (the pass writes the row's snapshot at that position)
+    const uint32_t hp = combine(ex, loc).hp;
     uint4 rec[8];
-    rec[0] = make_uint4(o, a.stamp, p, 0u);
+    rec[0] = make_uint4(o, a.stamp, p, hp);
 #pragma unroll
     for (int i = 1; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
     const uint64_t idx = last ? (uint64_t)w * a.c + kk : (uint64_t)a.W * a.c + p;
@@ -246,12 +251,13 @@ struct R2Args {
   const uint4* tcur;   // this batch's slot descriptors (W*c records of 128 B)
   const uint4* tprev;  // the previous applied batch's
   uint32_t stamp_cur, stamp_prev;
-  const uint4* pbuf;   // B final row states of the previous batch, by its sorted position
-  const uint4* psd;    // B x 128 B: their target rows (x, y = physical row, z = valid), one line each
-  const uint4* pdum;   // W*c x 1 KiB read for the slots no row uses
-  const uint4* psdum;  // AUTH: W*c x 128 B, their side-entry lines
-  uint4* snap;         // W*c snapshots for this batch
-  uint4* snapid;       // W*c x 128 B: each snapshot's first line (identity), for k_rr1
+  const uint4* ps;     // W*c x 1 KiB: the previous batch's final row states, by slot
+                       // (every slot's line is read, used or not)
+  const uint4* psds;   // AUTH: W*c x 128 B, their side entries {row lo, row hi, valid, slot}
+  uint4* snap;         // W*c x 1 KiB: sink of the slots this batch does not use
+  uint4* snapid;       // W*c x 128 B: the same for the identity lines
+  uint4* snapp;        // B x 1 KiB: each touched row's snapshot at its first op's position
+  uint4* snapidp;      // B x 128 B: its first line (identity), for k_rr1
   uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
   Scal* scal;
   uint32_t W, S, c;
@@ -330,7 +336,7 @@ template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   constexpr uint32_t kT = 64u * NW;  // rows per tile
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
-  __shared__ uint32_t s_pp[kSlotMax];  // slot -> position of its final state in P
+  __shared__ uint32_t s_sh[kSlotMax];  // this batch's slot -> position of the row's first op
   __shared__ uint32_t s_np, s_ns;
   __shared__ uint4 s_xw[NW * (kXepMax + 1) * 3];
   __shared__ uint4 s_xp[kXepMax * 3];
@@ -360,9 +366,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
     const uint4 ds = a.tcur[(sbase + k) * 8];
     if (dp.y == a.stamp_prev && dp.x < a.S) {
       s_pk[dp.x] = (int16_t)k;
-      s_pp[k] = dp.z;
       atomicAdd(&s_np, 1u);
     }
+    s_sh[k] = ds.w;
     if (ds.y == a.stamp_cur && ds.x < a.S) {
       s_sk[ds.x] = (int16_t)k;
       atomicAdd(&s_ns, 1u);
@@ -433,11 +439,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
         const uint32_t bit = dry_p ? 0u : low;
         const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
         const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + u0];
-        const uint32_t pos = s_pp[(uint32_t)k & (kSlotMax - 1u)];
-        const uint4* src = dry_p ? dry : a.pbuf + (uint64_t)pos * 64;
+        const uint4* src = dry_p ? dry : a.ps + (sbase + (uint64_t)k) * 64;
         const uint4 x = ld_row<true>(&src[lane]);
         if (AUTH) {  // the final state must be the one sealed for this row
-          const uint4 sd = uni4(dry_p ? dry[0] : a.psd[(uint64_t)pos * 8]);
+          const uint4 sd = uni4(dry_p ? dry[0] : a.psds[(sbase + (uint64_t)k) * 8]);
           if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
         }
 #pragma unroll
@@ -454,9 +459,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
         uint4 cur = v[0];
 #pragma unroll
         for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
-        uint4* dst = dry_s ? dry : sslot + (uint64_t)k * 64;
+        // the snapshot goes to the position of the row's first op, so that
+        // every op of the phase-C scans reads its own position's line
+        const uint32_t hp = s_sh[(uint32_t)k & (kSlotMax - 1u)];
+        uint4* dst = dry_s ? dry : a.snapp + (uint64_t)hp * 64;
         st_drop(dst, lane, cur);
-        if (lane < 8) st_drop(dry_s ? dry : a.snapid + (sbase + (uint64_t)k) * 8, lane, cur);
+        if (lane < 8) st_drop(dry_s ? dry : a.snapidp + (uint64_t)hp * 8, lane, cur);
       }
       if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
       if (AUTH) {
@@ -474,10 +482,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       if (tid == 0) s_xt = tot;
     }
   }
-  // unused slots: c reads of final states and c snapshot writes per partition
+  // unused slots (slots are dense from 0: [np, c) were not used by the
+  // previous batch): every slot's final-state line is read once per pass
   for (uint32_t k = np + wave; k < a.c; k += NW) {
-    uint4 x = ld_row<true>(&a.pdum[(sbase + k) * 64 + lane]);
-    if (AUTH) x = xor4(x, uni4(a.psdum[(sbase + k) * 8]));  // as the side entry a P slot reads
+    uint4 x = ld_row<true>(&a.ps[(sbase + k) * 64 + lane]);
+    if (AUTH) x = xor4(x, uni4(a.psds[(sbase + k) * 8]));  // as the side entry a used slot reads
     keep4(x);
   }
   for (uint32_t k = ns + wave; k < a.c; k += NW) {
@@ -505,12 +514,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
 
 struct PsealArgs {
   uint4* pbuf;   // B x 1 KiB
-  uint4* psd;    // B side entries
+  uint4* psd;    // B side entries {row lo, row hi, valid (row's last op), slot}
   uint4* ptag;   // B tags
   SealCtx sc;
   const uint32_t* te;
   Scal* scal;
   uint32_t ep;   // epoch of the P rows (seal: written; unseal: read)
+  uint4* ps;     // unseal: W*c x 1 KiB final states by slot (the pass reads every slot)
+  uint4* psds;   // unseal: W*c x 128 B their side entries
+  uint32_t nslots;  // W*c
 };
 
 template <bool SEAL>
@@ -537,14 +549,33 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
   const uint64_t sdv[2] = {u4lo(x), u4hi(x)};
   uint64_t hdr[2];
   header_prf(a.sc.headk, p0 + ur, a.ep, 2u, sdv, hdr);
+  bool ok = true;
   if (SEAL) {
     wave_seal<U, 8>(a.sc, s_te, 2u, p0, a.ep, v, a.ptag, true, st, hdr);
-  } else if (!wave_unseal<U, 8>(a.sc, s_te, 2u, p0, v, a.ptag, true, st, hdr) && lane == 0) {
-    atomicOr(&a.scal->error, 8u);
+  } else {
+    ok = wave_unseal<U, 8>(a.sc, s_te, 2u, p0, v, a.ptag, true, st, hdr);  // wave-uniform
+    if (!ok && lane == 0) atomicOr(&a.scal->error, 8u);
   }
+  if (SEAL) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) st_drop(a.pbuf, (p0 + u) * 64 + lane, v[u]);
-  if (lane < (uint32_t)U) st_drop(a.psd, (p0 + lane) * 8, SEAL ? sct : xor4(sd, ks));
+    for (int u = 0; u < U; ++u) st_drop(a.pbuf, (p0 + u) * 64 + lane, v[u]);
+    if (lane < (uint32_t)U) st_drop(a.psd, (p0 + lane) * 8, sct);
+  } else {
+    // a row's last op's state goes to its slot's line of PS (the pass reads
+    // PS by slot), every other position's back to its own P line: one 1 KiB
+    // write per position either way
+    const uint4 pt = xor4(sd, ks);  // lane u < U: position p0 + u's side entry
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 e = uni4(shfl4(pt, u));
+      // only an authenticated side entry names a slot (a forged or replayed
+      // one fails the batch and is written back in place)
+      const bool last = ok && e.z != 0u && e.w < a.nslots;
+      st_drop(last ? a.ps : a.pbuf, (last ? (uint64_t)e.w : p0 + u) * 64 + lane, v[u]);
+      if (lane < 8) st_drop(last ? a.psds : a.psd, (last ? (uint64_t)e.w : p0 + u) * 8 + lane,
+                            lane == 0 ? e : make_uint4(0, 0, 0, 0));
+    }
+  }
 }
 
 // ------------------------------------------------------------- k_rr1
@@ -566,9 +597,6 @@ struct Rr1V {
 struct Rr1Args {
   const uint4* rpos;
   const ROp* rop;
-  const uint4* img;
-  const uint4* snap;       // W*c slots
-  const uint4* snapdummy;  // B x 1 KiB (non-heads read their own, fixed bytes)
   uint4* rs;               // B x 128 B
   Rr1V* agg;
   Rr1V* carry;
@@ -577,8 +605,8 @@ struct Rr1Args {
   uint4* g;                // B x 256 B: what pass 0 gathered, by position
   uint32_t pass;           // 0: k_scan_a gathers; 1: k_scan_c reads g
   const uint4* idn;        // B x 128 B: request identity lines (k_meta)
-  const uint4* snapid;     // W*c x 128 B: snapshot identity lines (k_rpass2)
-  const uint4* siddummy;   // B x 128 B (non-heads read their own)
+  const uint4* snapidp;    // B x 128 B: snapshot identity lines at the rows' first
+                           // positions (k_rpass2); every op reads its own
 };
 
 struct Rr1Op {
@@ -618,11 +646,10 @@ struct Rr1Op {
     if (a.pass == 0) {
       const uint4 rp = a.rpos[p];
       const uint32_t seq = rp.x & kSeqMask;
-      const bool head = rp.x & kPosHead;
       uint4 rr[8], im[8], sn[8];  // ROp: {status, slot, kind, flags}, id, ...
       wave_load128(stage, reinterpret_cast<const uint4*>(a.rop + seq), rr);
       wave_load128(stage, a.idn + (uint64_t)seq * 8, im);
-      wave_load128(stage, head ? a.snapid + (uint64_t)rp.y * 8 : a.siddummy + (uint64_t)p * 8, sn);
+      wave_load128(stage, a.snapidp + (uint64_t)p * 8, sn);  // heads: the row's identity
       g[0] = make_uint4(rr[0].z, rr[0].x, 0u, 0u);
       g[1] = rr[1];
 #pragma unroll
@@ -768,35 +795,45 @@ __device__ inline void vrec_store(uint4* rec, uint4 f, uint4 v) {
   if (lane < 8) rec[lane] = lane == 0 ? f : make_uint4(0, 0, 0, 0);
 }
 
-// Select scans (Op::kSelect): the block value is the value of one op, read
-// once.  Merge scans (values synthesized from small per-op data, combined
-// lane-wise by Op::v_combine): the block walks all of its ops.
+// Select scans (Op::kSelect): the block value is the value of one op, the
+// block's defining op d (the last whose element replaces the running value).
+// Every op's rows are read and op d's kept, so the address stream does not
+// depend on which op defines the block (one row read at a data-dependent
+// position per block showed in FETCH_SIZE; DESIGN.md §3 rule 3).  Merge scans
+// (values synthesized from small per-op data, combined lane-wise by
+// Op::v_combine): the block walks all of its ops.
 template <class Op>
 __global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
   if (a.scal->error) return;
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= a.nvb) return;
   uint4 f, v = make_uint4(0, 0, 0, 0);
-  if constexpr (Op::kStash) {
-    // the block's 64 position records read once into LDS; the defining op's
-    // raw rows are kept for phase C (Op::value_stash)
-    __shared__ uint4 s_rec[4][kVBlk * 8];
+  if constexpr (Op::kSelect) {
+    // kStash ops: the block's 64 position records, read once into LDS
+    __shared__ uint4 s_rec[4][Op::kStash ? kVBlk * 8 : 1];
     uint4* rec = s_rec[threadIdx.x >> 6];
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) rec[i * 64 + lane_id()] = Op::rec_line(a, b * kVBlk * 8 + i * 64 + lane_id());
-    wave_lds_sync();
     uint32_t d = 0;
-    f = Op::f_identity();
-    for (uint32_t j = 0; j < kVBlk; ++j) {
-      const uint4 e = Op::f_of_rec(rec + j * 8);
-      d = Op::takes_b(f, e) ? j : d;
-      f = Op::f_combine(f, e);
+    if constexpr (Op::kStash) {
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) rec[i * 64 + lane_id()] = Op::rec_line(a, b * kVBlk * 8 + i * 64 + lane_id());
+      wave_lds_sync();
+      f = Op::f_identity();
+      for (uint32_t j = 0; j < kVBlk; ++j) {
+        const uint4 e = Op::f_of_rec(rec + j * 8);
+        d = Op::takes_b(f, e) ? j : d;
+        f = Op::f_combine(f, e);
+      }
+    } else {
+      f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
     }
-    v = Op::value_stash(a, b, d, f, rec + d * 8);
-  } else if constexpr (Op::kSelect) {
-    uint32_t d;
-    f_walk<Op>(a, b * kVBlk, kVBlk, f, d);
-    v = Op::value_of(a, b * kVBlk + d, f);
+    for (uint32_t j0 = 0; j0 < kVBlk; j0 += 8) {
+      uint4 x[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) x[u] = Op::elem_value(a, b * kVBlk + j0 + u, rec + (Op::kStash ? (j0 + u) * 8 : 0));
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) v = sel4(j0 + u == d, x[u], v);
+    }
+    v = Op::value_fin(f, v);
   } else {
     f = Op::f_identity();
     for (uint32_t j = 0; j < kVBlk; ++j) {
@@ -958,16 +995,15 @@ struct Rr2Args {
   GVS_VSCAN_FIELDS
   const uint4* rs;        // B x 128 B
   const uint4* img;
-  const uint4* snap;
-  const uint4* snapdummy;
-  uint4* pbuf;            // B final states, by sorted position
-  uint4* psd;             // B x 128 B: {physical row lo, hi, valid (the row's last op), 0}
+  const uint4* snapp;     // B x 1 KiB: row snapshots at their first op's position
+  uint4* pbuf;            // B final states, by sorted position (AUTH: all of them,
+                          // sealed next; plain: the positions that are not a row's last)
+  uint4* psd;             // B x 128 B: {physical row lo, hi, valid (the row's last op), slot}
+  uint4* ps;              // plain: W*c x 1 KiB, each row's final state at its slot
   uint4* resp;            // B internal response slots (kRespSlot)
   RRes* rres;
   uint32_t B;
   uint64_t cutoff;
-  uint4* vraw;            // B/64 x 2 KiB: the snapshot and image rows of each block's defining op
-  uint4* vdef;            // B/64 x 128 B: {its position in the block}
 };
 
 // the per-position record words every lane needs (RS lines 0 and 1)
@@ -1017,12 +1053,8 @@ struct Rr2Op {
   __device__ static uint4 ident_of(const Args& a, uint32_t p) {
     return a.rs[(uint64_t)p * 8 + 2 + min(lane_id(), 4u)];
   }
-  // the aggregate value: one 1 KiB read, always a line phase C also reads
-  // (the head's snapshot, or the op's request image)
-  // k_vscan_a: the value of block b's defining op d.  Both of its rows are
-  // read here and kept in vraw, and k_rr2_c takes them from there instead
-  // of reading them again (a row read twice in a batch hits or misses L2
-  // depending on when, which made FETCH_SIZE depend on the data).
+  // k_vscan_a reads the 64 position records of a block once (kStash) and
+  // every op's element value (its snapshot line and request image)
   static constexpr bool kStash = true;
   __device__ static uint4 rec_line(const Args& a, uint64_t i) { return a.rs[i]; }
   __device__ static RsHdr hdr_of_rec(const uint4* r) {
@@ -1030,20 +1062,16 @@ struct Rr2Op {
     return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z};
   }
   __device__ static uint4 f_of_rec(const uint4* r) { return f_of_hdr(hdr_of_rec(r)); }
-  __device__ static uint4 value_stash(const Args& a, uint32_t b, uint32_t d, uint4 f, const uint4* r) {
-    const uint32_t lane = lane_id(), p = b * kVBlk + d;
+  __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4* r) {
+    const uint32_t lane = lane_id();
     const RsHdr h = hdr_of_rec(r);
-    const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)p * 64;
-    const uint4 sv = ld_row<false>(&sp[lane]);
+    const uint4 sv = ld_row<false>(&a.snapp[(uint64_t)p * 64 + lane]);
     const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
-    st_drop(a.vraw, (uint64_t)b * 128 + lane, sv);
-    st_drop(a.vraw, (uint64_t)b * 128 + 64 + lane, iv);
-    if (lane < 8) st_drop(a.vdef, (uint64_t)b * 8 + lane, make_uint4(lane == 0 ? d : 0u, 0, 0, 0));
     const bool from_snap = (h.flags & kRsHead) && rs_setkind(h.flags) != kSetRec;
     const uint4 x = sel4(from_snap, sv, iv);
-    const uint4 v = own_value(h, x, x, r[2 + min(lane, 4u)]);
-    return sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v);
+    return own_value(h, x, x, r[2 + min(lane, 4u)]);
   }
+  __device__ static uint4 value_fin(uint4 f, uint4 v) { return sel4(f.y || !f.z, make_uint4(0, 0, 0, 0), v); }
 };
 
 // failure record: all zero but the request's server time (lane 5 low 8 B)
@@ -1063,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   __shared__ uint4 s_v[4][64];
   __shared__ uint4 s_f[4];
   __shared__ uint4 s_rs[4][16 * 8];  // each wave's 16 RS records
-  __shared__ uint4 s_blk[8 + kVLineU4];  // the block's vdef line and carry record
+  __shared__ uint4 s_blk[kVLineU4];  // the block's carry record
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x, p0 = b * kVBlk + wave * 16;
   // Every global line this kernel needs is read once: a line read twice in a
@@ -1073,10 +1101,9 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
   s_rs[wave][lane] = a.rs[(uint64_t)p0 * 8 + lane];
   s_rs[wave][64 + lane] = a.rs[(uint64_t)p0 * 8 + 64 + lane];
   if (wave == 0) {
-    if (lane < 8) s_blk[lane] = a.vdef[(uint64_t)b * 8 + lane];
     const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
-    s_blk[8 + 8 + lane] = c[8 + lane];
-    if (lane < 8) s_blk[8 + lane] = c[lane];
+    s_blk[8 + lane] = c[8 + lane];
+    if (lane < 8) s_blk[lane] = c[lane];
   }
   __syncthreads();
   auto hdr = [&](uint32_t j) {
@@ -1084,21 +1111,14 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
     return RsHdr{w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z};
   };
   auto ident = [&](uint32_t j) { return s_rs[wave][j * 8 + 2 + min(lane, 4u)]; };
-  // the rows: snapshot (heads) or own dummy row, and request image; the
-  // block's defining op's rows come from vraw (k_vscan_a read them)
-  const uint32_t pdef = b * kVBlk + uni4(s_blk[0]).x;
+  // the rows: every op's own SNAPP line (heads find their row's snapshot
+  // there) and its request image
   uint4 svs[16], ivs[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const RsHdr h = hdr(j);
-    if (p0 + j == pdef) {
-      svs[j] = a.vraw[(uint64_t)b * 128 + lane];
-      ivs[j] = a.vraw[(uint64_t)b * 128 + 64 + lane];
-    } else {
-      const uint4* sp = (h.flags & kRsHead) ? a.snap + (uint64_t)h.slot * 64 : a.snapdummy + (uint64_t)(p0 + j) * 64;
-      svs[j] = ld_row<false>(&sp[lane]);
-      ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
-    }
+    svs[j] = ld_row<false>(&a.snapp[(uint64_t)(p0 + j) * 64 + lane]);
+    ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
   }
   uint4 cf, cv;
   {  // the wave's aggregate from registers, then the carry
@@ -1121,8 +1141,8 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
     s_v[wave][lane] = v;
     if (lane == 0) s_f[wave] = f;
     __syncthreads();
-    cf = uni4(s_blk[8]);
-    cv = s_blk[16 + lane];
+    cf = uni4(s_blk[0]);
+    cv = s_blk[8 + lane];
     for (uint32_t k = 0; k < wave; ++k) {
       const uint4 e = s_f[k];
       cv = Rr2Op::v_combine(cf, cv, e, s_v[k][lane]);
@@ -1164,8 +1184,12 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
       st_drop(a.resp, r0 + 64 + lane, t);
       st_drop(a.rres, (uint64_t)h.seq * 8 + lane, t);
     }
-    st_drop(a.pbuf, (uint64_t)p * 64 + lane, fin);
-    sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, 0u), sd);
+    // the row's final state: plain stores put it at the row's slot (the next
+    // pass reads P by slot), every other position's state in its own P line;
+    // AUTH keeps all of them by position (sealed next, k_pseal)
+    const bool to_slot = a.ps && (h.flags & kRsLast);
+    st_drop(to_slot ? a.ps : a.pbuf, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, fin);
+    sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, h.slot), sd);
   }
   if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);
 }

@@ -61,6 +61,18 @@ def sum_over_ranks(ri, value, device=None):
     return int(t.item())
 
 
+def gather_ints(ri, values, device=None):
+    """Every rank's list of ints (same length on every rank), rank order."""
+    if ri.world == 1:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(ri.world)]
+    dist.all_gather(out, t)
+    return [[int(x) for x in o.cpu().tolist()] for o in out]
+
+
 def broadcast_bytes(ri, data, device=None):
     """rank 0's `data` (bytes) on every rank."""
     if ri.world == 1:

@@ -23,7 +23,10 @@ aad = 1; bytes channel_id = 2; bytes data = 3}` [U]).
 Errors: a request the store answers as a hard error (decode failure, wrong
 field sizes, a proto fail-fast rule) fails with INVALID_ARGUMENT; a bad
 challenge signature with UNAUTHENTICATED; an unknown channel with
-UNAUTHENTICATED.
+UNAUTHENTICATED.  A batch that overflows a fixed bound (nothing applied)
+fails its callers with RESOURCE_EXHAUSTED; any other store failure (integrity,
+device, exhausted epochs: the handle is dead) fails them with UNAVAILABLE and
+stops the server (`fatal` holds the reason).
 """
 import concurrent.futures
 import os
@@ -35,8 +38,11 @@ import time
 import numpy as np
 
 from . import abi, wire
+from .store import GvsError
 
 SERVICE = "grapevine.GrapevineAPI"
+# internal per-call statuses of a batch that failed as a whole
+_ST_OVERFLOW, _ST_FATAL = 0xFFFF0001, 0xFFFF0002
 SCHEME_SECURE, SCHEME_INSECURE = "grapevine", "insecure-grapevine"
 DEFAULT_SECURE_PORT, DEFAULT_INSECURE_PORT = 443, 3229
 
@@ -166,7 +172,7 @@ class GrapevineServer:
     replay them into the oracle)."""
 
     def __init__(self, store, address="127.0.0.1:0", window_ms=2.0, max_batch=1024,
-                 verify=True, clock=None, on_batch=None, workers=64):
+                 verify=True, clock=None, on_batch=None, workers=64, call_timeout=60.0):
         import grpc
         self.grpc = grpc
         self.store, self.window, self.max_batch = store, window_ms * 1e-3, max_batch
@@ -176,6 +182,9 @@ class GrapevineServer:
         self.q = queue.Queue()
         self.stop_evt = threading.Event()
         self.batches = 0
+        self.fatal = None  # set when the store failed for good
+        self.hook_errors = []  # exceptions raised by on_batch
+        self.call_timeout = call_timeout
         self.server = grpc.server(concurrent.futures.ThreadPoolExecutor(max_workers=workers))
         handler = grpc.method_handlers_generic_handler(SERVICE, {
             "Auth": grpc.unary_unary_rpc_method_handler(self._auth),
@@ -218,14 +227,21 @@ class GrapevineServer:
             with ch_lock:
                 rng.draw(32)  # the client drew one for this request too
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, "request larger than a wire slot")
+        if self.fatal is not None:
+            context.abort(grpc.StatusCode.UNAVAILABLE, f"store failed: {self.fatal}")
         with ch_lock:  # draw and enqueue together: the channel's requests keep their order
             p = _Pending(data, rng.draw(32))
             self.q.put(p)
-        p.done.wait()
+        if not p.done.wait(self.call_timeout):
+            context.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "batcher did not answer")
         if p.response:
             return encode_message(cid, p.response)
         if p.status == abi.WIRE_BAD_SIGNATURE:
             context.abort(grpc.StatusCode.UNAUTHENTICATED, "challenge signature does not verify")
+        if p.status == _ST_OVERFLOW:
+            context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, "batch overflowed a fixed bound; retry")
+        if p.status == _ST_FATAL:
+            context.abort(grpc.StatusCode.UNAVAILABLE, f"store failed: {self.fatal}")
         context.abort(grpc.StatusCode.INVALID_ARGUMENT, "request rejected (grapevine.proto:57-64)")
 
     # -- batcher --
@@ -255,17 +271,38 @@ class GrapevineServer:
         now = self.clock()
         times = np.full(len(batch), now, np.uint64)
         chal = np.frombuffer(b"".join(p.challenge for p in batch), np.uint8).reshape(-1, 32)
+        resp, status = [b""] * len(batch), np.full(len(batch), _ST_FATAL, np.uint32)
         try:
-            resp, _, status = self.store.process_wire_batch(
-                msgs, times, challenges=chal if self.verify else None)
-        except Exception:  # the whole batch failed (e.g. overflow): every caller gets an error
-            resp, status = [b""] * len(batch), np.full(len(batch), abi.WIRE_DECODE_ERROR, np.uint32)
-        self.batches += 1
-        if self.on_batch:
-            self.on_batch(msgs, times, chal, resp, status)
-        for p, r, s in zip(batch, resp, status):
-            p.response, p.status = r, int(s)
-            p.done.set()
+            try:
+                resp, _, status = self.store.process_wire_batch(
+                    msgs, times, challenges=chal if self.verify else None)
+            except GvsError as e:
+                if e.code == abi.GVS_ERR_BATCH_OVERFLOW:
+                    # nothing was applied: the callers may retry
+                    status = np.full(len(batch), _ST_OVERFLOW, np.uint32)
+                else:
+                    # integrity failure, device error, exhausted epochs: the
+                    # handle refuses every further call, so stop serving
+                    self._fail(e)
+            except Exception as e:  # noqa: BLE001 - anything else is a server fault
+                self._fail(e)
+            self.batches += 1
+            if self.on_batch:
+                try:
+                    self.on_batch(msgs, times, chal, resp, status)
+                except Exception as e:  # noqa: BLE001 - a hook must not kill the batcher
+                    self.hook_errors.append(e)
+        finally:  # every caller is answered, whatever on_batch or the store did
+            for p, r, s in zip(batch, resp, status):
+                p.response, p.status = r, int(s)
+                p.done.set()
+
+    def _fail(self, err):
+        """A store error that poisons the handle: refuse new calls and stop the
+        gRPC server (its process should exit non-zero; `fatal` says why)."""
+        self.fatal = f"{type(err).__name__}: {err}"
+        self.stop_evt.set()
+        threading.Thread(target=self.server.stop, args=(None,), daemon=True).start()
 
 
 # --------------------------------------------------------------------- client

@@ -208,7 +208,8 @@ int gvs_process_batch(gvs_handle *h, const gvs_request *reqs, uint32_t n,
  * are consecutive in `reqs` and their responses likewise in `out`.  Batches
  * apply in order, each with the semantics of gvs_process_batch; at the first
  * batch that fails, the call returns its error, that batch and the later
- * ones are not applied, and *applied (optional) holds the number applied. */
+ * ones are not applied, and *applied (optional) holds the number applied.
+ * The responses of the unapplied batches are zeroed in `out`. */
 int gvs_process_batches(gvs_handle *h, const gvs_request *reqs, const uint32_t *counts,
                         uint32_t k, gvs_response *out, uint32_t *applied);
 
@@ -271,7 +272,8 @@ int gvs_process_wire_batch(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
  * while batch t is processed).  Batch t has counts[t] messages; the messages
  * of all batches are consecutive in `in` (and in in_lens, times, challenges),
  * their results likewise in out / out_lens / decode_status.  Stops at the
- * first failing batch: its error is returned, *applied = the batches before.
+ * first failing batch: its error is returned, *applied = the batches before,
+ * and the unapplied batches' out / out_lens / decode_status are zeroed.
  * `in` and `out` in pinned memory (gvs_host_alloc) are copied without
  * staging. */
 int gvs_process_wire_batches(gvs_handle *h, const uint8_t *in, uint32_t in_stride,
@@ -350,7 +352,8 @@ int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 
 /* Read-only engine parameters of shard 0: "txn_slots" (transaction slots per
  * message partition, c), "group_slots" (recipient-group slots per mailbox
- * partition). */
+ * partition), "rccl_ranks" / "rccl_rank" (ncclCommCount / ncclCommUserRank of
+ * the store's own RCCL communicator; 0 / -1 when the store has none). */
 int gvs_get_option(gvs_handle *h, const char *key, int64_t *value);
 
 /* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */

@@ -143,6 +143,7 @@ def run_one(store, model, params, n=1024):
     (abi.RAW_MBOX_TAGS, 200 * 16 + 15),   # a mailbox tag
     (abi.RAW_PENDING, 300 * 1024 + 5),    # a pending final state
     (abi.RAW_PENDING_SIDE, 17 * 128 + 2),  # its side entry (target row)
+    (abi.RAW_PENDING_SIDE, 17 * 128 + 12),  # its side entry (the slot its state goes to)
     (abi.RAW_PENDING_TAGS, 900 * 16),     # its tag
 ])
 def test_tamper_is_detected(region, offset):
@@ -221,7 +222,6 @@ def live_slot_descriptors(store):
 @pytest.mark.parametrize("word,delta", [
     (1, 1),   # the stamp: the row's pending final state is hidden
     (0, 1),   # the row: the final state is applied to another row
-    (2, 1),   # the position: another row's final state is applied
 ])
 def test_tampered_slot_descriptor_is_detected(word, delta):
     store, model = make_pair()
@@ -237,6 +237,24 @@ def test_tampered_slot_descriptor_is_detected(word, delta):
     with pytest.raises(GvsError) as ei:
         run_one(store, model, params)
     assert ei.value.code == abi.ERR_INTEGRITY
+
+
+@pytest.mark.parametrize("word", [2, 3])
+def test_descriptor_positions_are_not_trusted(word):
+    """The previous batch's descriptor positions (its last op's P position,
+    word 2; its first op's, word 3) are not consulted by the pass: the final
+    states reach their slots through the authenticated P side entries
+    (k_pseal), so changing them changes nothing."""
+    store, model = make_pair()
+    model.seed(40)
+    params = ffi.gen_params(n_identities=200)
+    run_stream(store, model, params, batches=2, n=1024)
+    d, live = live_slot_descriptors(store)
+    for k in live[:50]:
+        rec = d[k].copy()
+        rec[word] = (int(rec[word]) + 1) % (1 << 32)
+        store.store_raw(abi.RAW_SLOTS, int(k) * 128, rec.tobytes())
+    run_stream(store, model, params, batches=2, n=1024)
 
 
 def test_replayed_pending_state_is_detected():

@@ -5,19 +5,32 @@ launch sequence, the grid/workgroup sizes and the HBM byte counters
 
 Shapes: 64K-request batches (the C3 batch, so the multi-tile sorts and every
 global merge step run) over a 2^20-message store, plain and authenticated
-(DESIGN.md §8), and the routed path (2 shards in one process: k_route_* and
-the padded all-to-all).
+(DESIGN.md §8); the routed path (2 shards in one process: k_route_* and the
+padded all-to-all); the wire path (decode, schnorrkel check, store, encode).
 
-Each mix runs tools/oblivious_probe.py under rocprofv3 in a child process
-(one --kernel-trace run, one --pmc run per counter; counters are never
-combined with other tracing).  The tolerance is derived from noise alone:
-the spread, across the processes, of the same counter on the prefill batches
-that every process runs identically, and the difference between two runs of
-the main mix with the same seed."""
+Every mix runs tools/oblivious_probe.py under rocprofv3 --pmc in a child
+process (one counter per run, never combined with other tracing).  The
+measured batches are seed-controlled: SEEDS x PER_SEED batches, the request
+generator reseeded before each seed's batches, so a difference between two
+mixes can be told from a difference between two draws of the same mix.  The
+prefill batches are identical in every process (same seed, same store state):
+their spread across the processes, and the difference between main and a
+second main process with the same seeds, is the counters' own noise.
+
+Two checks per kernel (DESIGN.md §3 'Results'):
+  * every measured batch of every mix lies within 3x the noise range + 2 KiB
+    of main's median;
+  * no bias: the mean over a mix's measured batches differs from main's mean
+    by less than 5 standard errors (sigma pooled from the identical-input
+    samples) + 0.25 KiB.  This is the check that caught the all-miss-read
+    excess of round 2 (k_m1r_c +20-27 KiB, tests/test_oblivious.py history;
+    profiles/r03_oblivious_bias_before.txt)."""
 import csv
 import glob
+import math
 import os
 import shutil
+import statistics
 import subprocess
 import sys
 
@@ -28,57 +41,53 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROBE = os.path.join(ROOT, "tools", "oblivious_probe.py")
 ALL_MIXES = ["main", "rud", "all_create", "all_miss_read", "hot_next", "hot_next_rud", "deletes"]
-# a hot recipient cannot go through a 2-shard router with the default
-# bucket capacity (it would overflow by design)
-ROUTED_MIXES = ["main", "rud", "all_create", "all_miss_read", "deletes"]
 SHAPES = {
     "plain": dict(args=["--log2n", "20", "--batch", "65536"], mixes=ALL_MIXES),
     "auth": dict(args=["--log2n", "20", "--batch", "65536", "--auth"], mixes=ALL_MIXES),
-    "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2"], mixes=ROUTED_MIXES),
-    # the wire path (decode, schnorrkel check, store, encode), every batch through it.
-    # Launches and grids must not depend on forged signatures or malformed
-    # messages either; the byte counters are compared over requests that
-    # verify and decode (canonical or not): a forged or malformed request
-    # fails at the gRPC level in the reference (grapevine.proto:57-64), which
-    # the host sees, and an all-failing batch is a batch of hard errors, which
-    # take padding keys in the store's sorts.
+    # a hot recipient cannot go through a 2-shard router with the default
+    # bucket capacity (it would overflow by design)
+    "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2"],
+                   mixes=["main", "rud", "all_create", "all_miss_read", "deletes"]),
+    # the wire path: launches and grids must not depend on forged signatures
+    # or malformed messages either; the byte counters of the front-end
+    # kernels are compared over requests that verify and decode (canonical or
+    # not): a forged or malformed request fails at the gRPC level in the
+    # reference (grapevine.proto:57-64), which the host sees.
     "wire": dict(args=["--log2n", "20", "--batch", "16384", "--wire"],
                  mixes=["main", "rud", "wire_forged", "wire_malformed", "wire_noncanonical"],
                  pmc_mixes=["main", "rud", "wire_noncanonical"],
-                 # the store's own kernels are covered by the shapes above
                  pmc_kernels=("k_wire_decode", "sr::k_sr_verify", "k_wire_encode")),
 }
-FILL_BATCHES = 4
-# Known residual, listed rather than hidden in a general floor: the sealed
-# mailbox write pass writes 5-49 cache lines (0.6-6.1 KiB of 67.6 MB) more
-# under the all-miss-read and hot-next mixes than under main, with no sampled
-# noise (r02s-r02z2; DESIGN.md §3 'Results').  Bound: 64 lines.
-RESIDUAL_KIB = {("auth", "WRITE_SIZE", "k_m2x<true>"): 8.0}
+FILL_BATCHES = 3
+SEEDS = (1234, 99, 5)
+PER_SEED = 2
+N_MEAS = len(SEEDS) * PER_SEED
+FLOOR_KIB = 2.0       # per-batch floor (16 lines)
+BIAS_FLOOR_KIB = 0.25  # bias floor (2 lines)
+BIAS_SIGMAS = 5.0
 
 
-def rocprof(args, mix, outdir, shape):
+def rocprof(counter, mix, outdir, shape):
     if shutil.which("rocprofv3") is None:
         pytest.skip("rocprofv3 not available")
     os.makedirs(outdir, exist_ok=True)
-    cmd = (["rocprofv3"] + args + ["-d", outdir, "-o", "run", "--output-format", "csv", "--",
-                                   sys.executable, PROBE, mix, "--fill-batches", str(FILL_BATCHES)]
+    cmd = (["rocprofv3", "--pmc", counter, "-d", outdir, "-o", "run", "--output-format", "csv", "--",
+            sys.executable, PROBE, mix, "--fill-batches", str(FILL_BATCHES),
+            "--seeds", ",".join(map(str, SEEDS)), "--batches", str(PER_SEED)]
            + SHAPES[shape]["args"])
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    return outdir
-
-
-def gvs_rows(path_glob):
-    files = glob.glob(path_glob, recursive=True)
-    assert files, path_glob
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    assert files, outdir
     rows = []
     for f in files:
-        rows += list(csv.DictReader(open(f)))
-    rows = [r for r in rows if "gvs::" in r.get("Kernel_Name", "")]
+        rows += [x for x in csv.DictReader(open(f)) if "gvs::" in x.get("Kernel_Name", "")
+                 and x.get("Counter_Name", counter) == counter]
     key = "Dispatch_Id" if "Dispatch_Id" in rows[0] else "Correlation_Id"
-    rows.sort(key=lambda r: int(r[key]))
-    return rows
+    rows.sort(key=lambda x: int(x[key]))
+    return [(short(x["Kernel_Name"]), x.get("Grid_Size"), x.get("Workgroup_Size"),
+             float(x["Counter_Value"])) for x in rows]
 
 
 def short(name):
@@ -86,14 +95,17 @@ def short(name):
 
 
 def split_batches(vals):
-    """Per-batch lists of (kernel, value); launches before the first batch
-    (k_seal_init at store creation) are dropped.  Routed stores start each
-    batch with the router, one k_route_dest..k_route_fill run per source: a
-    batch starts at the k_route_dest that follows a non-router kernel."""
-    first = ("k_wire_decode" if any(k == "k_wire_decode" for k, _ in vals) else
-             "k_route_dest" if any(k == "k_route_dest" for k, _ in vals) else "k_copy")
+    """Per-batch lists of (kernel, grid, workgroup, value); launches before
+    the first batch (k_seal_init at store creation) are dropped.  Routed
+    stores start each batch with the router, one k_route_dest..k_route_fill
+    run per source: a batch starts at the k_route_dest that follows a
+    non-router kernel."""
+    names = {v[0] for v in vals}
+    first = ("k_wire_decode" if "k_wire_decode" in names else
+             "k_route_dest" if "k_route_dest" in names else "k_copy")
     out, cur, prev = [], None, ""
-    for k, v in vals:
+    for v in vals:
+        k = v[0]
         starts = k == first and not (first == "k_route_dest" and prev.startswith("k_route_")
                                      and prev != "k_route_gather")
         prev = k
@@ -102,102 +114,121 @@ def split_batches(vals):
                 out.append(cur)
             cur = []
         if cur is not None:
-            cur.append((k, v))
+            cur.append(v)
     if cur:
         out.append(cur)
     return out
 
 
-@pytest.fixture(scope="module", params=sorted(SHAPES))
-def traces(request, tmp_path_factory):
-    shape = request.param
-    base = tmp_path_factory.mktemp("obl_" + shape)
-    out = {}
-    for mix in SHAPES[shape]["mixes"]:
-        d = rocprof(["--kernel-trace"], mix, str(base / f"kt_{mix}"), shape)
-        rows = gvs_rows(os.path.join(d, "**", "*kernel_trace.csv"))
-        out[mix] = [(short(r["Kernel_Name"]), r.get("Grid_Size", r.get("Grid_Size_X")),
-                     r.get("Workgroup_Size", r.get("Workgroup_Size_X"))) for r in rows]
-    return shape, out
+_CACHE = {}
 
 
-def test_launch_sequence_and_grids_identical(traces):
-    shape, tr = traces
-    ref = tr["main"]
-    assert len(ref) > 30
-    names = {k for k, _, _ in ref}
-    # the multi-tile sorts of a 64K batch run their global merge steps
+def measure(shape, counter, tmp_root):
+    """{mix: per-batch lists} for every mix of the shape, plus 'main#2' (a
+    second main process: identical inputs)."""
+    key = (shape, counter)
+    if key not in _CACHE:
+        mixes = SHAPES[shape]["mixes"] if counter == "FETCH_SIZE" else \
+            SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"])  # FETCH runs also serve the launch check
+        res = {}
+        for mix in list(mixes) + ["main#2"]:
+            m = mix.split("#")[0]
+            d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}")
+            res[mix] = split_batches(rocprof(counter, m, d, shape))
+        _CACHE[key] = res
+    return _CACHE[key]
+
+
+@pytest.fixture(scope="module")
+def tmp_root(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("obl"))
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_launch_sequence_and_grids_identical(shape, tmp_root):
+    """Every batch of every mix launches the same kernels with the same grids
+    and workgroups, in the same order (from the FETCH_SIZE runs' dispatch
+    records)."""
+    per = measure(shape, "FETCH_SIZE", tmp_root)
+    ref = per["main"]
+    seq = [(k, g, w) for k, g, w, _ in ref[-1]]
+    assert len(seq) > 30
+    names = {k for k, _, _ in seq}
     assert any(n.startswith("k_bitonic_global") for n in names), sorted(names)
     if shape == "routed":
         assert {"k_route_dest", "k_route_pos", "k_route_copy", "k_route_fill",
                 "k_route_gather"} <= names, sorted(names)
     if shape == "wire":
         assert {"k_wire_decode", "sr::k_sr_verify", "k_wire_encode"} <= names, sorted(names)
-    for mix, seq in tr.items():
-        assert seq == ref, f"{shape}: mix {mix} launches differ from main"
+    for mix, bs in per.items():
+        for i, b in enumerate(bs[1:], 1):
+            assert [(k, g, w) for k, g, w, _ in b] == seq, f"{shape}: {mix} batch {i} launches differ"
 
 
-def noise_tolerance(per_mix, repeat, idx, n_meas):
-    """6x the counter's run-to-run noise for kernel `idx`, plus 2 KiB (16
-    cache lines).  Noise is measured on identical inputs only: the spread over
-    the prefill batches that every process runs identically (batch 0 excluded:
-    cold caches), and the difference between two processes that ran the main
-    mix with the same seed (every batch, measured ones included).  The noise
-    is a max over ~10 samples, so a measured batch can exceed 3x of it by
-    chance (r02s: up to 4.3x on sort kernels of ~150 KiB; r02z3: 4.9x and
-    5.4x on k_m1r_c and k_m2x<false>, routed shape, all-miss-read); the 16-line floor
-    covers counters whose sampled noise was 0 (one mailbox write pass, 13
-    lines, DESIGN.md §3 'Results')."""
-    n_pre = min(len(bs) for bs in per_mix.values()) - n_meas
-    noise = 0.0
+def noise_stats(per, idx):
+    """(range, sigma) of kernel `idx` over identical-input samples: the
+    prefill batches (batch 0 excluded: cold start) across every process, and
+    main against main#2 over every batch.  sigma is pooled from the sample
+    variances of those groups."""
+    n_pre = min(len(bs) for bs in per.values()) - N_MEAS
+    rng, ss, dof = 0.0, 0.0, 0
     for i in range(1, n_pre):
-        vals = [bs[i][idx][1] for bs in per_mix.values()]
-        noise = max(noise, max(vals) - min(vals))
-    for a, b in zip(per_mix["main"][1:], repeat[1:]):
-        noise = max(noise, abs(a[idx][1] - b[idx][1]))
-    return noise, 6.0 * noise + 2.0
+        vals = [bs[i][idx][3] for bs in per.values()]
+        rng = max(rng, max(vals) - min(vals))
+        if len(vals) > 1:
+            ss += statistics.variance(vals) * (len(vals) - 1)
+            dof += len(vals) - 1
+    for a, b in zip(per["main"][1:], per["main#2"][1:]):
+        d = a[idx][3] - b[idx][3]
+        rng = max(rng, abs(d))
+        ss += d * d / 2.0
+        dof += 1
+    return rng, math.sqrt(ss / dof) if dof else 0.0
+
+
+def report(shape, counter, lines, bad):
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"oblivious_{counter}_{shape}.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+        f.write(f"violations: {bad}\n")
 
 
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 @pytest.mark.parametrize("counter", ["FETCH_SIZE", "WRITE_SIZE"])
-def test_hbm_bytes_identical(counter, shape, tmp_path):
-    """Per kernel, the byte counter of every measured batch of every mix must
-    equal main's within the counter's own run-to-run noise."""
-    per_mix = {}
-    for mix in SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"]):
-        d = rocprof(["--pmc", counter], mix, str(tmp_path / f"{counter}_{mix}"), shape)
-        rows = gvs_rows(os.path.join(d, "**", "*counter_collection.csv"))
-        vals = [(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
-                if r.get("Counter_Name", counter) == counter]
-        per_mix[mix] = split_batches(vals)
-    # main again, same seed: identical inputs, so any difference is noise
-    d = rocprof(["--pmc", counter], "main", str(tmp_path / f"{counter}_main_repeat"), shape)
-    rows = gvs_rows(os.path.join(d, "**", "*counter_collection.csv"))
-    repeat = split_batches([(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows
-                            if r.get("Counter_Name", counter) == counter])
-    n_meas = 3
-    ref_b = per_mix["main"]
-    kernels = [k for k, _ in ref_b[-1]]
-    lines, bad = [], []
+def test_hbm_bytes_identical(counter, shape, tmp_root):
+    """Per kernel, the byte counter of every measured batch of every mix lies
+    within 3x the counter's identical-input noise range + 2 KiB of main's
+    median, and no mix is biased against main (mean over its measured batches
+    within 5 standard errors + 0.25 KiB)."""
+    per = measure(shape, counter, tmp_root)
+    keep = set(SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"])) | {"main#2"}
+    per = {m: bs for m, bs in per.items() if m in keep}
+    ref_b = per["main"]
+    kernels = [k for k, _, _, _ in ref_b[-1]]
     only = SHAPES[shape].get("pmc_kernels")
+    lines, bad = [], []
     for idx, k in enumerate(kernels):
         if only and k not in only:
             continue
-        noise, tol = noise_tolerance(per_mix, repeat, idx, n_meas)
-        tol = max(tol, RESIDUAL_KIB.get((shape, counter, k), 0.0))
-        ref = sorted(b[idx][1] for b in ref_b[-n_meas:])[1]
-        row = [f"{k[:28]:28s} ref={ref:12.1f} noise={noise:8.2f} tol={tol:8.2f}"]
-        for mix, bs in per_mix.items():
+        rng, sigma = noise_stats(per, idx)
+        tol = 3.0 * rng + FLOOR_KIB
+        main_meas = [b[idx][3] for b in ref_b[-N_MEAS:]]
+        ref = statistics.median(main_meas)
+        mu_main = statistics.fmean(main_meas)
+        se = sigma * math.sqrt(2.0 / N_MEAS)
+        btol = BIAS_SIGMAS * se + BIAS_FLOOR_KIB
+        row = [f"{k[:30]:30s} ref={ref:12.1f} range={rng:8.2f} sigma={sigma:7.2f} tol={tol:7.2f} "
+               f"btol={btol:6.2f}"]
+        for mix, bs in per.items():
             assert [x[0] for x in bs[-1]] == kernels, f"{mix}: kernel sequence differs"
-            dev = max(abs(b[idx][1] - ref) for b in bs[-n_meas:])
-            row.append(f"{mix}:{dev:.2f}")
+            meas = [b[idx][3] for b in bs[-N_MEAS:]]
+            dev = max(abs(v - ref) for v in meas)
+            bias = statistics.fmean(meas) - mu_main
+            row.append(f"{mix}:{dev:.2f}/{bias:+.2f}")
             if dev > tol:
-                bad.append((k, mix, round(dev, 2), round(tol, 2)))
+                bad.append((k, mix, "batch", round(dev, 2), round(tol, 2)))
+            if mix != "main" and abs(bias) > btol:
+                bad.append((k, mix, "bias", round(bias, 2), round(btol, 2)))
         lines.append(" ".join(row))
-    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", f"oblivious_{counter}_{shape}.txt"), "w") as f:
-        for mix, bs in per_mix.items():
-            f.write(f"{mix}: " + " ".join(f"{k}={v:.1f}" for b in bs for k, v in b) + "\n")
-        f.write("\n".join(lines) + "\n")
-        f.write(f"violations: {bad}\n")
+    report(shape, counter, lines, bad)
     assert not bad, f"{counter} depends on the request mix: {bad}"

@@ -14,6 +14,7 @@ import pytest
 
 from grapevine_amd import abi, wire
 from grapevine_amd import server as gs
+from grapevine_amd.store import GvsError
 from oracle import ffi
 from oracle import sr25519 as sr
 
@@ -146,3 +147,52 @@ def test_grpc_flow_over_oracle_double():
     srv, signers, results = run_clients(OracleWireStore(cfg))
     check_results(signers, results)
     assert srv.batches < 3 * 2 * 4 + 4  # calls were batched together
+
+
+class FailingStore:
+    """A store whose batches fail as a whole with a given error code."""
+
+    def __init__(self, code):
+        self.code = code
+
+    def process_wire_batch(self, msgs, times, in_stride=None, out_stride=1042, challenges=None):
+        raise GvsError(self.code, "injected")
+
+
+def _one_call(store, on_batch=None):
+    srv = gs.GrapevineServer(store, window_ms=1.0, verify=False, on_batch=on_batch,
+                             call_timeout=30).start()
+    c = gs.GrapevineClient(f"insecure-grapevine://127.0.0.1:{srv.port}", Signer(random.Random(1))).auth()
+    with pytest.raises(grpc.RpcError) as e:
+        c.query(abi.REQUEST_TYPE_READ)
+    c.close()
+    return srv, e.value.code()
+
+
+def test_overflow_is_resource_exhausted_and_server_keeps_serving():
+    srv, code = _one_call(FailingStore(abi.GVS_ERR_BATCH_OVERFLOW))
+    assert code == grpc.StatusCode.RESOURCE_EXHAUSTED
+    assert srv.fatal is None
+    srv.stop()
+
+
+def test_integrity_failure_stops_the_server():
+    srv, code = _one_call(FailingStore(abi.GVS_ERR_INTEGRITY))
+    assert code == grpc.StatusCode.UNAVAILABLE
+    assert srv.fatal and "injected" in srv.fatal
+    srv.stop()
+
+
+def test_on_batch_exception_does_not_kill_the_batcher():
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024)
+
+    def boom(*_):
+        raise RuntimeError("on_batch failed")
+
+    srv = gs.GrapevineServer(OracleWireStore(cfg), window_ms=1.0, on_batch=boom, call_timeout=30).start()
+    c = gs.GrapevineClient(f"insecure-grapevine://127.0.0.1:{srv.port}", Signer(random.Random(1))).auth()
+    for _ in range(2):  # the second call is served by the same batcher thread
+        assert c.query(abi.REQUEST_TYPE_READ)["status_code"] == abi.STATUS_CODE_NOT_FOUND
+    c.close()
+    assert len(srv.hook_errors) == 2 and srv.batcher.is_alive()
+    srv.stop()

@@ -130,6 +130,11 @@ def main():
     p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
     p.add_argument("--wire", action="store_true", help="wire path with challenge check")
     p.add_argument("--seed", type=int, default=1234, help="generator seed of the measured batches")
+    p.add_argument("--seeds", default="",
+                   help="comma-separated seeds: the measured batches are --batches per seed, the "
+                        "generator reseeded before each seed's batches (seed-controlled runs)")
+    p.add_argument("--no-check", action="store_true",
+                   help="skip the parity asserts of the measured batches (GVS_DIAG variants)")
     a = p.parse_args()
     assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
     S = a.shards if a.shards > 1 else 0
@@ -147,18 +152,20 @@ def main():
             continue
         want = model.process_batch(reqs)
         got = store.process_batch(reqs)
-        assert got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
-    model.seed(a.seed)  # same request-generator state for every mix
+        assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
     params = ffi.gen_params(n_identities=a.identities, bad_auth=0, bad_recipient=0, hard_error=0,
                             zero_recipient=0, **{"miss": 0, **MIXES[a.mix]})
-    for _ in range(a.batches):
+    seeds = [int(x) for x in a.seeds.split(",") if x] or [a.seed]
+    for k in range(len(seeds) * a.batches):
+        if k % a.batches == 0:
+            model.seed(seeds[k // a.batches])  # same request-generator state for every mix
         reqs = model.gen_batch(n, params)
         if wp:
             wp.run(reqs, a.mix)
             continue
         want = model.process_batch(reqs)
         got = store.process_batch(reqs)
-        assert got.tobytes() == want.tobytes(), "parity failure inside the probe"
+        assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe"
     store.synchronize()
     print("probe ok", a.mix, store.stats()["messages"])
 
