@@ -435,10 +435,16 @@ def main():
     known = prefill(torch, store, dev, B, int(N * a.fill), pool, g, 1_700_000_000,
                     per_batch=B - a.expiry)
     n_host = a.host_steps + (3 if a.host_steps else 0)  # pipelined, two one by one, one warm-up
-    batches = gen_batches(torch, dev, B, a.warmup + a.steps + n_host, known, pool, g, 1_800_000_000)
+    batches = gen_batches(torch, dev, B, a.warmup + a.steps + n_host + a.steps, known, pool, g,
+                          1_800_000_000)
+    one_by_one = batches[-a.steps:]  # the same API one call per batch, timed after the checks
     d_out = torch.empty((B, 1040), dtype=torch.uint8, device=dev)
-    d_outs = [torch.empty((B, 1040), dtype=torch.uint8, device=dev) for _ in range(a.steps)]
     nreq = B - a.expiry  # requests per batch (the expiry deletes take the last X slots)
+    # the timed batches back to back in one device array, submitted in one
+    # call (gvs_process_batches_device: no host round trip between batches)
+    timed_in = torch.cat([batches[a.warmup + i][:nreq] for i in range(a.steps)]).contiguous()
+    timed_out = torch.empty((a.steps * nreq, 1040), dtype=torch.uint8, device=dev)
+    d_outs = [timed_out[i * nreq:(i + 1) * nreq] for i in range(a.steps)]
     if a.expiry:
         store.set_expiry_cutoff(1_750_000_000)  # every prefilled message has expired
     store.set_timing(True)
@@ -450,16 +456,14 @@ def main():
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    stage = {}
-    for i in range(a.steps):
-        store.process_batch_device(batches[a.warmup + i].data_ptr(), nreq, d_outs[i].data_ptr())
-        for k, v in store.last_timings().items():
-            stage[k] = stage.get(k, 0.0) + v
+    store.process_batches_device(timed_in.data_ptr(), [nreq] * a.steps, timed_out.data_ptr())
     torch.cuda.synchronize(dev)
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     elapsed = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
-    stage_ms = {k: v / a.steps for k, v in stage.items()}
+    # per-stage HIP-event times (and the message pass's, for the roofline):
+    # the last timed batch's marks
+    stage_ms = dict(store.last_timings())
     st = store.stats()
     d_out = d_outs[-1]
     statuses = torch.bincount(d_out[:, 1024].to(torch.int64), minlength=9)[:9].tolist()
@@ -473,6 +477,19 @@ def main():
               "messages_before": msgs_before, "messages_after": st["messages"],
               "conserved": expired == 0 if not a.expiry else expired >= 0,
               "expired": expired}
+
+    # for comparison: one gvs_process_batch_device call per batch (each call
+    # waits for its batch's verdict before the next is enqueued)
+    gdist.barrier(ri)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for x in one_by_one:
+        store.process_batch_device(x.data_ptr(), nreq, d_out.data_ptr())
+    torch.cuda.synchronize(dev)
+    t_obo = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
+    per_batch_api = {"value": world * nreq * a.steps / t_obo, "unit": "req/s",
+                     "ms_per_batch": t_obo / a.steps * 1e3,
+                     "api": "gvs_process_batch_device, one call (and one host round trip) per batch"}
 
     host_path = None
     if a.host_steps:
@@ -604,7 +621,8 @@ def main():
                        "rccl_ranks": per_rank[0][0],
                        "per_rank": [{"rccl_rank": r[1], "rccl_ranks": r[0], "shard_batch": r[2],
                                      "route_capacity": r[3], "txn_slots": r[4]} for r in per_rank],
-                       "expiry_per_batch": a.expiry},
+                       "expiry_per_batch": a.expiry,
+                       "api": f"gvs_process_batches_device: the {a.steps} timed batches in one call"},
             "roofline": roofline,
             # SURVEY.md §8(d) whole-batch figure: message table and mailbox table
             # (read pass + write pass) read and written, requests in, responses out
@@ -612,6 +630,7 @@ def main():
                                "frac": batch_gbs / HBM_PEAK_GBS,
                                "formula": "2*N*1024 + 4*R*1024 + B*(1088 + 1088), per ms_per_step"},
             "cpu_baseline": cpu,
+            "per_batch_api": per_batch_api,
             "host_path": host_path,
             "front_end": front,
             "checks": checks,

@@ -171,6 +171,8 @@ struct HostPipe {
   uint8_t* hin[2] = {};
   uint8_t* hout[2] = {};
   uint32_t* herr = nullptr;  // pinned: the agreed error word of the batch in each slot
+  uint32_t* errs = nullptr;  // pinned: one error word per batch of gvs_process_batches_device
+  uint32_t nerr = 0;
   hipStream_t copy = nullptr;      // host -> device
   hipStream_t copy_out = nullptr;  // device -> host (its own queue: an H2D of batch t+1
                                    // must not wait behind the D2H of batch t)
@@ -847,7 +849,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   e.stamp_run = e.stamp_next++;
   if (e.stamp_next == kNone) e.stamp_next = 1;
   const uint32_t xbase = B - e.X;
-  hipLaunchKernelGGL(k_copy, dim3(B / 4), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
+  hipLaunchKernelGGL(k_copy, dim3(B / (4 * kCopyPerWave)), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
                      (const uint4*)(e.X ? e.xb2[e.par ^ 1] : nullptr), xbase);
   mark(h, "copy");
   {
@@ -1015,7 +1017,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   else
     hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), 0, s, margs2(h, e));
   if (d_out && n)
-    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
+    hipLaunchKernelGGL(k_out, dim3((n + 4 * kCopyPerWave - 1) / (4 * kCopyPerWave)), dim3(256), 0, s,
+                       (const uint4*)e.resp, n, d_out);
   mark(h, "m2");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
@@ -1442,7 +1445,8 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_kv_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
   if (d_out && n)
-    hipLaunchKernelGGL(k_out, dim3((n + 3) / 4), dim3(256), 0, s, (const uint4*)e.resp, n, d_out);
+    hipLaunchKernelGGL(k_out, dim3((n + 4 * kCopyPerWave - 1) / (4 * kCopyPerWave)), dim3(256), 0, s,
+                       (const uint4*)e.resp, n, d_out);
   mark(h, "kv");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
@@ -1485,6 +1489,7 @@ int gvs_destroy(gvs_handle* h) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (hp.herr) (void)hipHostFree(hp.herr);
+  if (hp.errs) (void)hipHostFree(hp.errs);
   WirePipe& wp = h->wpipe;
   for (int b = 0; b < 2; ++b) {
     for (void* q : {(void*)wp.hin[b], (void*)wp.hout[b], (void*)wp.hchal[b], (void*)wp.hlens[b],
@@ -1689,6 +1694,64 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       if (applied) *applied = t;
     }
     if (!more && t >= enq) break;
+  }
+  return stop;
+}
+
+int gvs_process_batches_device(gvs_handle* h, const void* d_reqs, const uint32_t* counts, uint32_t k,
+                               void* d_out, uint32_t* applied) {
+  if (applied) *applied = 0;
+  if (!h || h->kind != 0 || (k && (!counts || !d_reqs || !d_out))) return GVS_ERR_INVALID_ARG;
+  for (uint32_t t = 0; t < k; ++t)
+    if (counts[t] > max_submit(h)) return GVS_ERR_INVALID_ARG;
+  if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (k == 0) return GVS_OK;
+  GVS_HIP(h, hipSetDevice(h->device));
+  HostPipe& p = h->pipe;  // pinned error words, one per batch
+  if (k > p.nerr) {
+    if (p.errs) (void)hipHostFree(p.errs);
+    p.errs = nullptr;
+    p.nerr = 0;
+    GVS_HIP(h, hipHostMalloc((void**)&p.errs, (size_t)k * sizeof(uint32_t), hipHostMallocDefault));
+    p.nerr = k;
+  }
+  if (int r = reset_errors(h)) return r;
+  const uint4* in = (const uint4*)d_reqs;
+  uint4* out = (uint4*)d_out;
+  std::vector<HostState> snap(k);
+  uint64_t off = 0, total = 0;
+  for (uint32_t t = 0; t < k; ++t) total += counts[t];
+  uint32_t enq = 0;
+  int stop = GVS_OK;
+  // every batch enqueued back to back; the error word is not reset between
+  // them, so the batches behind a failing one do nothing
+  for (uint32_t t = 0; t < k; ++t) {
+    if (int r = check_epoch(h)) {
+      stop = r;
+      break;
+    }
+    snap[t] = save_state(h);
+    if (int r = run_batch(h, in + off * kAbiU4, counts[t], out + off * kAbiU4, false)) return r;
+    if (h->mode != kSingle)
+      if (int r = agree_errors(h)) return r;
+    GVS_HIP(h, hipMemcpyAsync(&p.errs[t], &h->eng[0].scal->error, sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, h->stream));
+    advance(h);  // as if applied; rolled back below if it was not
+    off += counts[t];
+    enq = t + 1;
+  }
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  off = 0;
+  for (uint32_t t = 0; t < enq; ++t) {
+    if (const uint32_t e = p.errs[t]) {
+      restore_state(h, snap[t]);
+      GVS_HIP(h, hipMemsetAsync(out + off * kAbiU4, 0, (size_t)(total - off) * sizeof(gvs_response),
+                                h->stream));
+      GVS_HIP(h, hipStreamSynchronize(h->stream));
+      return decode_error(h, e);
+    }
+    off += counts[t];
+    if (applied) *applied = t + 1;
   }
   return stop;
 }

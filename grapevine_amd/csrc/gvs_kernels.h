@@ -221,29 +221,39 @@ __device__ inline uint32_t block1024_prefix(bool f, uint32_t* s_w, uint32_t* tot
 // of msg id with auth = recipient = the stored recipient, internal type
 // kTypeExpire if the record is valid, else padding.
 constexpr uint32_t kTypeExpire = 0x45585031u;  // never a valid request_type
+constexpr uint32_t kCopyPerWave = 8;  // requests per wave in k_copy / k_out (loads in flight together)
 __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint32_t stride,
                                               uint32_t n, uint32_t B, uint4* __restrict__ img,
                                               uint32_t* __restrict__ types, const uint4* xbuf,
                                               uint32_t xbase) {
-  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr uint32_t R = kCopyPerWave;
+  const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const uint32_t lane = lane_id();
-  if (i >= B) return;
-  uint4 v = make_uint4(0, 0, 0, 0);
-  uint32_t t = 0;
-  if (i >= xbase) {
-    // lanes 0..5 <- record words id, rcpt lo, rcpt hi, rcpt lo, rcpt hi, valid
-    const uint32_t src = lane == 0 ? 0u : (lane < 5 ? 2u - (lane & 1u) : 3u);
-    const uint4* rec = xbuf + (uint64_t)(i - xbase) * 8;
-    const uint4 x = rec[src];
-    t = __shfl(x.x, 5) ? kTypeExpire : 0u;
-    if (lane < 5) v = x;
-    if (lane == 5) v = make_uint4(1u, 0, 0, 0);  // nonzero server time (response unused)
-  } else {
-    if (i < n) v = in[(uint64_t)i * stride + lane];
-    if (i < n && lane == 0) t = in[(uint64_t)i * stride + 64].x;
+  if (i0 >= B) return;
+  uint4 v[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {  // wave-uniform conditions
+    const uint32_t i = i0 + r;
+    v[r] = (i < n && i < xbase) ? in[(uint64_t)i * stride + lane] : make_uint4(0, 0, 0, 0);
   }
-  img[(uint64_t)i * 64 + lane] = v;
-  if (lane == 0) types[i] = t;
+  // type words: lane r < R holds request i0 + r's
+  const uint32_t ti = i0 + min(lane, R - 1u);
+  uint32_t t = (lane < R && ti < n && ti < xbase) ? in[(uint64_t)ti * stride + 64].x : 0u;
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = i0 + r;
+    if (i >= xbase) {
+      // lanes 0..5 <- record words id, rcpt lo, rcpt hi, rcpt lo, rcpt hi, valid
+      const uint32_t src = lane == 0 ? 0u : (lane < 5 ? 2u - (lane & 1u) : 3u);
+      const uint4 x = xbuf[(uint64_t)(i - xbase) * 8 + src];
+      const uint32_t tx = __shfl(x.x, 5) ? kTypeExpire : 0u;
+      v[r] = lane < 5 ? x : (lane == 5 ? make_uint4(1u, 0, 0, 0) : make_uint4(0, 0, 0, 0));  // nonzero server time
+      t = lane == r ? tx : t;
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) img[(uint64_t)(i0 + r) * 64 + lane] = v[r];
+  if (lane < R) types[i0 + lane] = t;
 }
 
 // ------------------------------------------------------------------ k_meta
@@ -712,15 +722,24 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
 }
 // ------------------------------------------------------------------ k_out
 
-// internal response slots (kRespSlot B, whole lines) -> caller layout (1040 B)
+// internal response slots (kRespSlot B, whole lines) -> caller layout (1040 B),
+// kCopyPerWave responses per wave
 __global__ __launch_bounds__(256) void k_out(const uint4* __restrict__ resp, uint32_t n,
                                              uint4* __restrict__ out) {
-  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr uint32_t R = kCopyPerWave;
+  const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const uint32_t lane = lane_id();
-  if (i >= n) return;
-  const uint4* src = resp + (uint64_t)i * (kRespSlot / 16);
-  out[(uint64_t)i * 65 + lane] = src[lane];
-  if (lane == 0) out[(uint64_t)i * 65 + 64] = src[64];
+  if (i0 >= n) return;
+  uint4 v[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r)
+    v[r] = i0 + r < n ? resp[(uint64_t)(i0 + r) * (kRespSlot / 16) + lane] : make_uint4(0, 0, 0, 0);
+  const uint32_t si = i0 + min(lane, R - 1u);
+  const uint4 st = (lane < R && si < n) ? resp[(uint64_t)si * (kRespSlot / 16) + 64] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r)
+    if (i0 + r < n) out[(uint64_t)(i0 + r) * 65 + lane] = v[r];
+  if (lane < R && si < n && i0 + lane < n) out[(uint64_t)si * 65 + 64] = st;
 }
 
 }  // namespace gvs

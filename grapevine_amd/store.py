@@ -24,7 +24,7 @@ _TEST_LIB_PATH = os.path.join(_HERE, "libgvstore_test.so")
 
 EXPORTED = (
     "gvs_config_init", "gvs_create", "gvs_destroy", "gvs_process_batch", "gvs_process_batches",
-    "gvs_process_batch_device", "gvs_access", "gvs_get_stats",
+    "gvs_process_batch_device", "gvs_process_batches_device", "gvs_access", "gvs_get_stats",
     "gvs_synchronize", "gvs_set_option", "gvs_get_option", "gvs_set_timing", "gvs_last_timings", "gvs_last_error", "gvs_version",
     "gvs_comm_unique_id", "gvs_create_sharded", "gvs_storage_seal_row", "gvs_set_expiry_cutoff",
     "gvs_oram_create", "gvs_oram_destroy", "gvs_oram_access_batch", "gvs_oram_access_batch_device",
@@ -68,6 +68,7 @@ def load_library(path=None):
     lib.gvs_destroy.argtypes = [vp]
     lib.gvs_process_batch.argtypes = [vp, vp, u32, vp]
     lib.gvs_process_batch_device.argtypes = [vp, vp, u32, vp]
+    lib.gvs_process_batches_device.argtypes = [vp, vp, vp, u32, vp, ctypes.POINTER(u32)]
     lib.gvs_process_wire_batch.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, u32, vp, vp, vp]
     lib.gvs_process_wire_batches.argtypes = [vp, vp, u32, vp, vp, u32, vp, vp, vp, u32, vp, vp,
                                              ctypes.POINTER(u32)]
@@ -219,6 +220,20 @@ class ObliviousStore:
 
     def process_batch_device(self, d_reqs_ptr, n, d_out_ptr):
         self._check(self.lib.gvs_process_batch_device(self.h, d_reqs_ptr, n, d_out_ptr))
+
+    def process_batches_device(self, d_reqs_ptr, counts, d_out_ptr):
+        """k batches from device memory in one call (gvs_process_batches_device):
+        every batch enqueued before any result is awaited.  Returns the number
+        applied; raises GvsError (with .applied) at the first failing batch."""
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        applied = ctypes.c_uint32(0)
+        rc = self.lib.gvs_process_batches_device(self.h, d_reqs_ptr, c.ctypes.data, len(c), d_out_ptr,
+                                                 ctypes.byref(applied))
+        if rc != 0:
+            err = GvsError(rc, self.lib.gvs_last_error(self.h).decode())
+            err.applied = applied.value
+            raise err
+        return applied.value
 
     @staticmethod
     def _wire_slab(msgs, in_stride):

@@ -226,6 +226,15 @@ int gvs_host_free(gvs_handle *h, void *p);
 int gvs_process_batch_device(gvs_handle *h, const void *d_reqs, uint32_t n,
                              void *d_out);
 
+/* k batches from device memory in one call: batch t has counts[t] requests;
+ * the requests of all batches are consecutive in d_reqs and their responses
+ * likewise in d_out.  Every batch is enqueued before any result is awaited
+ * (no host round trip between batches).  At the first batch that fails, its
+ * error is returned, it and the later ones are not applied, *applied
+ * (optional) holds the number applied and the unapplied responses are zeroed. */
+int gvs_process_batches_device(gvs_handle *h, const void *d_reqs, const uint32_t *counts,
+                               uint32_t k, void *d_out, uint32_t *applied);
+
 /* ---- wire codec ---------------------------------
  * The protobuf messages of api/proto/grapevine.proto:123-176 as the prost
  * structs of types/src/lib.rs:27-120 encode them.  A fully populated

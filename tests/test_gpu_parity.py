@@ -186,3 +186,62 @@ def test_host_pipeline_stops_at_failing_batch():
     d = diff_responses(got[0], cl.process_batch(later), later)
     assert not d, "\n".join(d)
     assert store.dump_messages().tobytes() == cl.dump_messages().tobytes()
+
+
+def test_device_batches_match_oracle():
+    """gvs_process_batches_device: several device-resident batches in one call
+    (no host round trip between them) equal the oracle batch by batch."""
+    torch = pytest.importorskip("torch")
+    store, model = make_pair(4096, 16, 32, 1024)
+    model.seed(16)
+    p = ffi.gen_params(n_identities=300)
+    sizes = [1024, 1, 0, 700, 1024, 1024]
+    batches = [model.gen_batch(n, p) for n in sizes]
+    want = np.concatenate([model.process_batch(b) for b in batches])
+    reqs = np.concatenate(batches)
+    d_in = torch.from_numpy(reqs.view(np.uint8).reshape(-1).copy()).cuda()
+    d_out = torch.zeros(len(reqs) * 1040, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    assert store.process_batches_device(d_in.data_ptr(), sizes, d_out.data_ptr()) == len(sizes)
+    got = d_out.cpu().numpy().view(abi.RESPONSE_DTYPE)
+    d = diff_responses(got, want, reqs)
+    assert not d, "\n".join(d)
+    st = store.stats()
+    assert (st["messages"], st["mailboxes"], st["batches"]) == (model.messages, model.mailboxes, len(sizes))
+    store.close()
+
+
+def test_device_batches_stop_at_failing_batch():
+    """A batch that overflows a router bucket stops gvs_process_batches_device:
+    the batches before it are applied, its and the later responses are zero,
+    and the store goes on from that state."""
+    torch = pytest.importorskip("torch")
+    from grapevine_amd.store import GvsError
+    S = 4
+    cfg = abi.make_config(4096, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=1024,
+                          shard_count=S, route_capacity=320)
+    store, cl = ObliviousStore(cfg), ffi.Cluster(cfg)
+    cl.seed(17)
+    p = ffi.gen_params(n_identities=300)
+    hot = ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60, n_identities=300)
+    ok = [cl.gen_batch(S * 1024, p) for _ in range(2)]
+    want = [cl.process_batch(b) for b in ok]
+    bad = cl.gen_batch(S * 1024, hot)
+    assert cl.process_batch(bad) is None
+    later = cl.gen_batch(S * 1024, p)
+    reqs = np.concatenate(ok + [bad, later])
+    d_in = torch.from_numpy(reqs.view(np.uint8).reshape(-1).copy()).cuda()
+    d_out = torch.full((len(reqs) * 1040,), 0xAB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(GvsError) as ei:
+        store.process_batches_device(d_in.data_ptr(), [S * 1024] * 4, d_out.data_ptr())
+    assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW and ei.value.applied == 2
+    got = d_out.cpu().numpy().view(abi.RESPONSE_DTYPE)
+    for k in range(2):
+        d = diff_responses(got[k * S * 1024:(k + 1) * S * 1024], want[k], ok[k])
+        assert not d, "\n".join(d)
+    assert not got[2 * S * 1024:].view(np.uint8).any(), "unapplied responses must be zero"
+    assert store.stats()["messages"] == cl.messages and store.stats()["batches"] == 2
+    got_later = store.process_batches([later])
+    d = diff_responses(got_later[0], cl.process_batch(later), later)
+    assert not d, "\n".join(d)

@@ -10,30 +10,50 @@ identically.  The mixes include adversarial ones: every request aimed at one
 recipient (hot_next, hot_next_rud), every read missing (all_miss_read), only
 deletes.  A pass whose workgroups did work in proportion to the ops routed to
 them would show the hot mixes here."""
+import csv
+import glob
 import os
+import shutil
 import statistics
+import subprocess
+import sys
 
 import pytest
 
-from test_oblivious import gvs_rows, rocprof, short, split_batches, SHAPES
+from test_oblivious import PROBE, short, split_batches
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MIXES = ["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]
-SHAPES["c3"] = dict(args=["--log2n", "24", "--batch", "65536", "--identities", "200000"],
-                    mixes=MIXES)
+ARGS = ["--log2n", "24", "--batch", "65536", "--identities", "200000", "--fill-batches", "4"]
 N_MEAS = 3
+
+
+def kernel_trace(mix, outdir):
+    """(kernel, duration us) of every gvs kernel of one probe process."""
+    if shutil.which("rocprofv3") is None:
+        pytest.skip("rocprofv3 not available")
+    os.makedirs(outdir, exist_ok=True)
+    cmd = (["rocprofv3", "--kernel-trace", "-d", outdir, "-o", "run", "--output-format", "csv", "--",
+            sys.executable, PROBE, mix] + ARGS)
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = []
+    for f in glob.glob(os.path.join(outdir, "**", "*kernel_trace.csv"), recursive=True):
+        rows += [x for x in csv.DictReader(open(f)) if "gvs::" in x.get("Kernel_Name", "")]
+    key = "Dispatch_Id" if "Dispatch_Id" in rows[0] else "Correlation_Id"
+    rows.sort(key=lambda x: int(x[key]))
+    return [(short(x["Kernel_Name"]), (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3)
+            for x in rows]
 
 
 def test_kernel_durations_independent_of_mix(tmp_path):
     per_mix = {}
     for mix in MIXES:
-        d = rocprof(["--kernel-trace"], mix, str(tmp_path / f"kt_{mix}"), "c3")
-        rows = gvs_rows(os.path.join(d, "**", "*kernel_trace.csv"))
-        vals = [(short(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-                for r in rows]
-        per_mix[mix] = split_batches(vals)
+        per_mix[mix] = [[(k, v) for k, _, _, v in b] for b in
+                        split_batches([(k, None, None, v) for k, v in kernel_trace(mix, str(tmp_path / mix))])]
     ref_b = per_mix["rud"]
     kernels = [k for k, _ in ref_b[-1]]
     n_pre = min(len(bs) for bs in per_mix.values()) - N_MEAS

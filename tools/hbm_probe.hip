@@ -111,6 +111,35 @@ __global__ __launch_bounds__(256, MINW) void k_pipe_stag(v4u* a, uint32_t rows) 
   }
 }
 
+// k_part with block-interleaved partitions: partition w's local row k lives
+// at physical row ((k / G) * W + w) * G + k % G, so that the workgroups in
+// flight together sweep a compact window of the table (grid-stride-like DRAM
+// locality) while each still owns a fixed set of rows
+template <int U, int G, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_ipart(v4u* a, uint32_t rows) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t W = gridDim.x, w = blockIdx.x;
+  for (uint32_t t = 0; t < rows / 256; ++t) {
+    const uint32_t rb = t * 256 + wave * 64;
+    for (uint32_t j = 0; j < 64; j += U) {
+      v4u v[U];
+      uint64_t pr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t k = rb + j + u;
+        pr[u] = ((k / G) * W + w) * G + k % G;
+        v[u] = ld<true>(&a[pr[u] * 64 + lane]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u].x ^= 1u;
+        st<true>(&a[pr[u] * 64 + lane], v[u]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // grid-stride with U independent 16-B accesses in flight per thread: thread t
 // of block b handles elements (b * U + u) * 256 + t, then jumps the grid
 template <int U, bool NT, bool COPY>
@@ -244,6 +273,14 @@ int main(int argc, char** argv) {
     timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe<4, true, 4>), dim3(nb), dim3(256), 0, 0, a, rows); });
     std::snprintf(nm, sizeof nm, "pipe U16 nt w1 rows=%u", rows);
     timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe<16, true, 1>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "ipart U16 G16 nt rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_ipart<16, 16, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "ipart U16 G64 nt rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_ipart<16, 64, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "ipart U16 G256 nt rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_ipart<16, 256, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
+    std::snprintf(nm, sizeof nm, "ipart U16 G1 nt rows=%u", rows);
+    timeit(nm, rw, [&] { hipLaunchKernelGGL((k_ipart<16, 1, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
     std::snprintf(nm, sizeof nm, "pipe U8 nt stag1 rows=%u", rows);
     timeit(nm, rw, [&] { hipLaunchKernelGGL((k_pipe_stag<8, 1, 2>), dim3(nb), dim3(256), 0, 0, a, rows); });
     std::snprintf(nm, sizeof nm, "pipe U8 nt stag7 rows=%u", rows);
