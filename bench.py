@@ -57,6 +57,13 @@ def parse():
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
+    p.add_argument("--predict-shards", type=int, default=0,
+                   help="S > 1: time one GPU holding all S shards of a sharded store (in-process "
+                        "transport, S x the per-GPU load) and print the predicted per-GPU step of an "
+                        "S-GPU run instead of the normal line")
+    p.add_argument("--xgmi-gbs", type=float, default=64.0,
+                   help="--predict-shards: assumed xGMI rate per peer link and direction (GB/s)")
+    p.add_argument("--prediction-json", default=os.path.join(ROOT, "profiles", "scale_prediction.json"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     p.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_auth_latest.json"))
     return p.parse_args()
@@ -388,6 +395,66 @@ def front_end(torch, store, dev, batches, nreq, B):
                                                   "32-B messages; random inputs)"}}
 
 
+def predict_shards(a, torch, dev, json_out):
+    """Per-GPU step of an S-GPU run, measured on one GPU.  One process holds
+    all S shards of a sharded store (gvs_create with shard_count = S: the same
+    router, padded sub-batches and shard pipelines as the RCCL transport, the
+    all-to-all done by device copies), each shard at the per-GPU size (2^log2n
+    messages, 75 % full), and every call carries S x B requests, i.e. S sources
+    of B each.  The GPU then does the work of all S ranks in series, so one
+    rank's share is T / S; the xGMI exchange an S-GPU run adds is priced from
+    its byte count at --xgmi-gbs per link and direction (the S - 1 peers in
+    parallel, requests out and responses back)."""
+    from grapevine_amd import abi
+    from grapevine_amd.store import ObliviousStore
+    S, N, B = a.predict_shards, 1 << a.log2n, a.batch
+    cfg = abi.make_config(N, max_batch=B, device=0, shard_count=S)
+    store = ObliviousStore(cfg)
+    st0 = store.stats()
+    C, SB = st0["route_capacity"], S * B
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x6772617065 + 11)
+    pool = torch.randint(0, 256, (S << 19, 32), dtype=torch.uint8, device=dev, generator=g)  # 2^19 per shard
+    pool[:, 0] |= 1
+    t0 = time.perf_counter()
+    known = prefill(torch, store, dev, SB, int(N * a.fill) * S, pool, g, 1_700_000_000)
+    t_fill = time.perf_counter() - t0
+    batches = gen_batches(torch, dev, SB, a.warmup + a.steps, known, pool, g, 1_800_000_000)
+    d_out = torch.empty((SB, 1040), dtype=torch.uint8, device=dev)
+    for i in range(a.warmup):
+        store.process_batch_device(batches[i].data_ptr(), SB, d_out.data_ptr())
+    timed_in = torch.cat(batches[a.warmup:]).contiguous()
+    timed_out = torch.empty((a.steps * SB, 1040), dtype=torch.uint8, device=dev)
+    store.set_timing(True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    store.process_batches_device(timed_in.data_ptr(), [SB] * a.steps, timed_out.data_ptr())
+    torch.cuda.synchronize(dev)
+    T = (time.perf_counter() - t0) / a.steps
+    viol = sum(check_batch(torch, timed_in[i * SB:(i + 1) * SB], timed_out[i * SB:(i + 1) * SB])[0]
+               for i in range(a.steps))
+    slot = 1152
+    xbytes = (S - 1) * C * slot  # per direction per rank: C slots to each of S - 1 peers
+    x_ms = 2 * (C * slot) / (a.xgmi_gbs * 1e9) * 1e3  # peers in parallel, out and back
+    st = store.stats()
+    line = {"metric": "predicted per-GPU step of an S-GPU sharded run, measured on one GPU",
+            "shards": S, "log2n_per_shard": a.log2n, "batch_per_source": B, "route_capacity": C,
+            "shard_batch": st["shard_batch"], "steps": a.steps, "warmup": a.warmup,
+            "inproc_ms_per_call": T * 1e3, "per_rank_compute_ms": T / S * 1e3,
+            "xgmi_bytes_per_direction_per_rank": xbytes, "xgmi_gbs_assumed": a.xgmi_gbs,
+            "xgmi_ms_out_and_back": x_ms,
+            "predicted_per_gpu_step_ms": T / S * 1e3 + x_ms,
+            "predicted_req_s_at_S": S * B / (T / S + x_ms * 1e-3),
+            "predicted_req_s_per_gpu": B / (T / S + x_ms * 1e-3),
+            "stage_ms_last_call": store.last_timings(), "violations": viol,
+            "messages": st["messages"], "prefill_s": t_fill,
+            "note": "the in-process call includes the router and the device-copy all-to-all of all S "
+                    "sources; T / S is one rank's share"}
+    json_out.write(json.dumps(line) + "\n")
+    json_out.flush()
+    store.close()
+
+
 def main():
     a = parse()
     # RCCL prints a version banner on stdout at communicator creation; keep
@@ -402,6 +469,8 @@ def main():
 
     ri = gdist.rank_info()
     world, rank, local = ri.world, ri.rank, ri.local
+    if a.predict_shards > 1:
+        return predict_shards(a, torch, torch.device("cuda", local), json_out)
     if world > 1:
         torch.cuda.set_device(local)
     gdist.init("nccl")  # torch's RCCL: comm-id broadcast, barriers, max-time reduction
@@ -595,6 +664,19 @@ def main():
                         "hbm_achieved": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
                         "alg_bytes_per_launch": alg_bytes}
         cpu = None if a.no_cpu or world > 1 else cpu_baseline(a.cpu_seconds, a.cpu_threads)
+        # the 8-GPU step as predicted from one GPU (bench.py --predict-shards 8,
+        # profiles/scale_prediction.json), when measured at this size
+        prediction = None
+        try:
+            with open(a.prediction_json) as f:
+                pj = json.load(f)
+            if pj.get("log2n_per_shard") == a.log2n and pj.get("batch_per_source") == B:
+                prediction = {k: pj[k] for k in ("shards", "predicted_per_gpu_step_ms", "predicted_req_s_at_S",
+                                                 "per_rank_compute_ms", "xgmi_ms_out_and_back",
+                                                 "xgmi_gbs_assumed", "route_capacity", "shard_batch")}
+                prediction["source"] = os.path.relpath(a.prediction_json, ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
         R = cfg.mailbox_partitions * cfg.mailbox_partition_slots
         batch_bytes = 2 * N * 1024 + 4 * R * 1024 + B * (1088 + 1088)
         batch_gbs = batch_bytes / (elapsed / a.steps) / 1e9
@@ -631,6 +713,7 @@ def main():
                                "formula": "2*N*1024 + 4*R*1024 + B*(1088 + 1088), per ms_per_step"},
             "cpu_baseline": cpu,
             "per_batch_api": per_batch_api,
+            "scaling_prediction": prediction,
             "host_path": host_path,
             "front_end": front,
             "checks": checks,
