@@ -54,6 +54,8 @@ def parse():
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=8, choices=(4, 8),
                    help="--auth: waves per workgroup of the sealed message pass")
+    p.add_argument("--sealed-fused", type=int, default=1, choices=(0, 1),
+                   help="--auth: AES and BLAKE2b interleaved in the sealed message pass (1) or phased (0)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
@@ -209,7 +211,9 @@ def c1_single_thread():
 def cpu_baseline(budget_s, threads):
     """The reference's CPU path, restated: the grapevine handler over Path ORAM
     (oracle/gvs_pathoram.c: CuckooHashTables over Path ORAM, Z = 4, recursive
-    position map, 6 ORAM accesses per request), cross-checked bit-for-bit against the sequential model in
+    position map, 6 ORAM accesses per request, every block move an aligned cmov
+    over every stash and branch slot, Circuit-ORAM style eviction along the
+    accessed branch and one reverse-lexicographic path), cross-checked bit-for-bit against the sequential model in
     tests/test_pathoram.py.  One independent instance per host thread of this
     process's CPU share (the reference's maps are single-owner, &mut self);
     each is prefilled through its own accesses and then times the C3 mix for
@@ -257,7 +261,8 @@ def cpu_baseline(budget_s, threads):
             "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
             "cpu_share": cpu["share"],
             "c1_single_thread_req_s": c1,
-            "sample": f"PathORAM + CuckooHashTable restatement of the reference CPU path (oracle/gvs_pathoram.c), "
+            "sample": f"PathORAM + CuckooHashTable restatement of the reference CPU path (oracle/gvs_pathoram.c; "
+                      f"aligned-cmov block moves over every stash and branch slot, single-pass eviction), "
                       f"2^{log2n} capacity (tree height reduced from C3's 2^24 to bound memory), "
                       f"{threads} independent instances on {threads} host threads "
                       f"(this process's CPU share of {cpu['logical_cpus']} logical CPUs), C3 mix, "
@@ -497,6 +502,7 @@ def main():
                                       store.get_option("txn_slots")], device=dev)
     if a.auth:
         store.set_option("sealed_pass_waves", a.sealed_waves)
+        store.set_option("sealed_pass_fused", a.sealed_fused)
     g = torch.Generator(device=dev)
     g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
@@ -659,7 +665,8 @@ def main():
             roofline = {"bound": "valu", "achieved": v_ach, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                         "frac": v_ach / VALU_PEAK_GINST if v_ach else None, "traffic": None,
                         "kernel": f"k_rpass2 AUTH (fixed-slot message-table pass, sealed rows; "
-                                  f"{a.sealed_waves} waves per workgroup)",
+                                  f"{a.sealed_waves} waves per workgroup"
+                                  f"{', AES and BLAKE2b interleaved' if a.sealed_fused else ''})",
                         "valu_insts_per_launch": insts, "kernel_ms": rpass_ms,
                         "hbm_achieved": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
                         "alg_bytes_per_launch": alg_bytes}

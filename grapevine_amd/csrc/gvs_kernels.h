@@ -144,6 +144,20 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
 // step of the level (flip, j = k/2): quadruple {x0, x0 + h, m - h, m} with
 // m = x0 ^ (2j - 1) its mirror; else {x0, x0 + h, x0 + j, x0 + j + h}.
 // nq = quadruples with x0 < n.
+//
+// Every index into x[] / v[] is a compile-time constant and the flip is a
+// select, so the four keys stay in registers: a runtime index (the partner
+// chosen by flip) put them in scratch, whose loads the compiler then placed
+// under branches on the key comparisons (scratch traffic is HBM traffic, and
+// it showed in FETCH_SIZE under regular key orders).
+template <typename K>
+__device__ inline void cx_static(K& a, K& b, bool live) {  // a at the lower index
+  const bool sw = live && key_lt(b, a);
+  const K ta = a;
+  a = key_sel(sw, b, a);
+  b = key_sel(sw, ta, b);
+}
+
 template <typename K>
 __global__ __launch_bounds__(256) void k_bitonic_global2(K* data, uint32_t n, uint32_t k,
                                                          uint32_t j, uint32_t nq) {
@@ -154,23 +168,24 @@ __global__ __launch_bounds__(256) void k_bitonic_global2(K* data, uint32_t n, ui
   const uint32_t x0 = g * 2u * j + o;
   const bool flip = (j << 1) == k;
   const uint32_t m = x0 ^ (2u * j - 1u);
-  uint32_t x[4] = {x0, x0 + h, flip ? m - h : x0 + j, flip ? m : x0 + j + h};
-  K v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = x[q] < n ? data[x[q]] : v[0];
-  auto cx = [&](int a, int b) {  // x[a] < x[b]; a key past n is +inf
-    const bool sw = x[b] < n && key_lt(v[b], v[a]);
-    const K ta = v[a];
-    v[a] = key_sel(sw, v[b], v[a]);
-    v[b] = key_sel(sw, ta, v[b]);
-  };
-  cx(0, flip ? 3 : 2);
-  cx(1, flip ? 2 : 3);
-  cx(0, 1);
-  cx(2, 3);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (x[q] < n) data[x[q]] = v[q];
+  const uint32_t x1 = x0 + h, x2 = flip ? m - h : x0 + j, x3 = flip ? m : x0 + j + h;
+  const bool l1 = x1 < n, l2 = x2 < n, l3 = x3 < n;  // x0 < n: nq counts those
+  K v0 = data[x0];
+  K v1 = data[l1 ? x1 : x0];
+  K v2 = data[l2 ? x2 : x0];
+  K v3 = data[l3 ? x3 : x0];
+  // first step: pairs (0, 2), (1, 3), or (0, 3), (1, 2) on a level's first step
+  K b0 = key_sel(flip, v3, v2), b1 = key_sel(flip, v2, v3);
+  cx_static(v0, b0, flip ? l3 : l2);
+  cx_static(v1, b1, flip ? l2 : l3);
+  v2 = key_sel(flip, b1, b0);
+  v3 = key_sel(flip, b0, b1);
+  cx_static(v0, v1, l1);
+  cx_static(v2, v3, l3);
+  data[x0] = v0;
+  if (l1) data[x1] = v1;
+  if (l2) data[x2] = v2;
+  if (l3) data[x3] = v3;
 }
 
 // One step j of merge level k: pair (i, i ^ (2j - 1)) on the level's first
@@ -442,6 +457,18 @@ struct AllocArgs {
 constexpr uint32_t kWinGroup = 8;      // blocks per allocation-window refill
 constexpr uint32_t kWinRing = 16384;  // LDS window ring: one group + one chunk fits
 
+// Free-ring index of entry `off` after the ring counter whose residue is
+// `base` (= counter mod m, computed once per kernel from the wave-uniform
+// counter), off < 2m (window reads run up to B + 1023 past the counter):
+// two selects.  A per-element 64-bit `%` expands to a branch
+// on the high word of its operand, so the code fetched would follow the data
+// (instruction fetch shows in FETCH_SIZE; DESIGN.md §3 rule 6).
+__device__ inline uint32_t ring_at(uint32_t base, uint32_t off, uint32_t m) {
+  uint32_t x = base + off;
+  x = x >= m ? x - m : x;
+  return x >= m ? x - m : x;
+}
+
 // seq-order compact flags (coalesced, fixed) + per-block counts; pflag holds
 // bit 0 pop, bit 1 mailbox-ok create, bits 2..11 / 12..21 their in-block
 // exclusive prefixes
@@ -488,6 +515,8 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   const uint32_t pops = s_off[0][1023], scnt = s_off[1][1023];
   Scal* sc = a.scal;
   const uint64_t tail0 = sc->tail, head0 = sc->head;
+  const uint32_t rs = (uint32_t)a.ring_size;
+  const uint32_t tbase = (uint32_t)(tail0 % a.ring_size), hbase = (uint32_t)(head0 % a.ring_size);
   const uint64_t count1 = sc->count - pops;
   const uint64_t room = a.N - count1;
   const uint64_t m = scnt < room ? scnt : room;
@@ -508,8 +537,8 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
       if (c < a.nblk) {
         const bool pop = f[u] & 1u;
         const uint32_t P = (c ? s_off[0][c - 1] : 0u) + ((f[u] >> 2) & 1023u);
-        const uint64_t pos = pop ? (uint64_t)P : (uint64_t)pops + (i - P);
-        a.ring[(tail0 + pos) % a.ring_size] = pop ? slot[u] : kNone;
+        const uint32_t pos = pop ? P : pops + (i - P);
+        a.ring[ring_at(tbase, pos, rs)] = pop ? slot[u] : kNone;
       }
     }
   }
@@ -527,7 +556,7 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k <= kWinGroup; ++k) {
       const uint32_t pos = loaded + k * 1024;
-      w[k] = pos < need ? a.ring[(head0 + pos + tid) % a.ring_size] : 0u;
+      w[k] = pos < need ? a.ring[ring_at(hbase, pos + tid, rs)] : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k <= kWinGroup; ++k) {
@@ -556,7 +585,7 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
       const uint32_t pos = loaded + k * 1024;
-      v[k] = pos < a.B ? a.ring[(head0 + pos + tid) % a.ring_size] : 0u;
+      v[k] = pos < a.B ? a.ring[ring_at(hbase, pos + tid, rs)] : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) asm volatile("" ::"v"(v[k]));
@@ -666,7 +695,8 @@ __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
   }
   const uint32_t nd = s_off[1023];
   Scal* sc = a.scal;
-  const uint64_t tail = sc->tail0 + sc->pops;
+  const uint32_t rs = (uint32_t)a.ring_size;
+  const uint32_t tbase = (uint32_t)((sc->tail0 + sc->pops) % a.ring_size);
   for (uint32_t c0 = 0; c0 < a.nblk; c0 += 8) {  // no barrier: blocks are independent
     uint32_t f[8], slot[8];
 #pragma unroll
@@ -681,8 +711,8 @@ __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
       if (c < a.nblk) {
         const bool d = f[u] & 1u;
         const uint32_t P = (c ? s_off[c - 1] : 0u) + (f[u] >> 1);
-        const uint64_t pos = d ? (uint64_t)P : (uint64_t)nd + (i - P);
-        a.ring[(tail + pos) % a.ring_size] = d ? slot[u] : kNone;
+        const uint32_t pos = d ? P : nd + (i - P);
+        a.ring[ring_at(tbase, pos, rs)] = d ? slot[u] : kNone;
       }
     }
   }

@@ -61,7 +61,10 @@ __global__ __launch_bounds__(256) void k_bcopy(BcopyArgs a) {
     const uint64_t index = (uint64_t)h.x | ((uint64_t)h.y << 32);
     const bool bad = real && (index >= a.N || h.z > 1u);
     if (bad && lane == 0) atomicOr(&a.scal->error, kKvErr);
-    const uint64_t row = (real && !bad) ? (index % a.W) * a.S + index / a.W : kRNullRow;
+    // 32-bit division (index < N < 2^32 when it counts): a 64-bit one branches
+    // on the dividend's high word
+    const uint32_t ix = (real && !bad) ? (uint32_t)index : 0u;
+    const uint64_t row = (real && !bad) ? (uint64_t)(ix % a.W) * a.S + ix / a.W : kRNullRow;
     if (lane == 0) a.rkeys[i] = r_key(row, 0u, i);
     my_kind = lane == j ? h.z : my_kind;
   }

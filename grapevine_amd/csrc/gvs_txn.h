@@ -30,6 +30,7 @@
 // per-position record is written by whole-line stores (DESIGN.md §3 rules).
 #pragma once
 #include "gvs_kernels.h"
+#include "gvs_seal_fused.h"
 
 namespace gvs {
 
@@ -193,11 +194,16 @@ struct RtxOp {
     const uint32_t hp = b.hp != kNone ? b.hp : a.hp;
     return b.reset ? V{b.reset, b.cnt, hp, 0u} : V{a.reset, a.cnt + b.cnt, hp, 0u};
   }
+  // 32-bit arithmetic and selects only: a 64-bit division expands to a branch
+  // on the dividend's high word, and a branch around it for null rows would
+  // skip code by the data (instruction fetch shows in FETCH_SIZE)
   __device__ static void row_of(const Args& a, uint32_t p, uint64_t& row, uint32_t& w) {
     const uint64_t k = a.rkeys[p];
-    row = k >> 22;
-    if (row >= (uint64_t)a.W * a.S) row = kRNullRow;  // never index past the table
-    w = row == kRNullRow ? a.W : (uint32_t)(row / a.S);
+    const uint64_t n = (uint64_t)a.W * a.S;
+    const bool valid = (k >> 22) < n;  // never index past the table
+    const uint32_t r32 = valid ? (uint32_t)(k >> 22) : 0u;
+    row = valid ? (uint64_t)r32 : kRNullRow;
+    w = valid ? r32 / a.S : a.W;
   }
   __device__ static V local(const Args& a, uint32_t p, uint4*) {
     uint64_t row, prow = ~0ull;
@@ -321,6 +327,69 @@ template <bool NTL>
 __device__ inline uint4 ld_line(const uint4* p) { return ld_row<NTL>(p); }
 
 constexpr uint32_t kSlotMax = 1024;      // transaction slots per partition (c) at most
+
+// One chunk of U rows (partition row rj, physical row r0) of the message
+// pass, plaintext in v: apply the previous batch's final states, snapshot the
+// rows this batch touches, expiry selection.  Returns the expiry count.
+//
+// The first chunk of wave 0 (`first`) runs each loop once "dry" on the
+// workgroup's own dry line, so every workgroup executes the same code whatever
+// its slots hold (instruction fetch shows in FETCH_SIZE, DESIGN.md §3 rule 6).
+// The dry iteration is an extra mask bit (1 << U), taken last by the same loop
+// code: a loop whose first iteration were special could be peeled by the
+// compiler, and then not every workgroup would fetch the loop's code.
+template <int U, bool AUTH>
+__device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uint32_t rj, uint64_t r0,
+                                             bool first, const int16_t* s_pk, const int16_t* s_sk,
+                                             const uint32_t* s_sh, uint64_t sbase, uint4* dry,
+                                             uint32_t xc, uint4* s_xw_w, const uint4* s_xx, uint32_t nx) {
+  const uint32_t lane = lane_id();
+  uint32_t mp = 0, ms = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    mp |= s_pk[rj + u] >= 0 ? (1u << u) : 0u;
+    ms |= s_sk[rj + u] >= 0 ? (1u << u) : 0u;
+  }
+  mp = __builtin_amdgcn_readfirstlane(mp);
+  ms = __builtin_amdgcn_readfirstlane(ms);
+  uint32_t mq = mp | (first ? (1u << U) : 0u);
+  while (mq) {  // rows the previous batch changed: its final state
+    const uint32_t low = mq & (0u - mq);
+    mq &= mq - 1u;
+    const bool dry_p = low == (1u << U);
+    const uint32_t bit = dry_p ? 0u : low;
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+    const int16_t k = dry_p ? (int16_t)0 : s_pk[rj + u0];
+    const uint4* src = dry_p ? dry : a.ps + (sbase + (uint64_t)k) * 64;
+    const uint4 x = ld_row<true>(&src[lane]);
+    if (AUTH) {  // the final state must be the one sealed for this row
+      const uint4 sd = uni4(dry_p ? dry[0] : a.psds[(sbase + (uint64_t)k) * 8]);
+      if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
+  }
+  uint32_t sq = ms | (first ? (1u << U) : 0u);
+  while (sq) {  // rows this batch touches: their snapshot
+    const uint32_t low = sq & (0u - sq);
+    sq &= sq - 1u;
+    const bool dry_s = low == (1u << U);
+    const uint32_t bit = dry_s ? 0u : low;
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31));
+    const int16_t k = dry_s ? (int16_t)0 : s_sk[rj + (u0 & 31u)];
+    uint4 cur = v[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
+    // the snapshot goes to the position of the row's first op, so that
+    // every op of the phase-C scans reads its own position's line
+    const uint32_t hp = s_sh[(uint32_t)k & (kSlotMax - 1u)];
+    uint4* dst = dry_s ? dry : a.snapp + (uint64_t)hp * 64;
+    st_drop(dst, lane, cur);
+    if (lane < 8) st_drop(dry_s ? dry : a.snapidp + (uint64_t)hp * 8, lane, cur);
+  }
+  if (a.xon) xc = x_detect2<U>(a, v, s_xw_w, xc, s_xx, nx);
+  return xc;
+}
 constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose final state is pending
 
 // Authenticated storage: a row the batch touches is sealed with the pending
@@ -332,8 +401,16 @@ constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose fi
 // S must be a multiple).  The sealed pass runs 8 waves of U = 8 rows: they
 // share one AES table, so two waves per SIMD fit the CU's LDS (its VALU work
 // needs both to issue at full rate); the plain pass runs 4 waves of 16 rows.
-template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4>
+//
+// FUSED (AUTH, U = 8, NW = 8): the chunk's crypto runs as two fused
+// iterations (gvs_seal_fused.h), each the 8 keystream blocks of one epoch with
+// one leaf compression interleaved: (A) the read-epoch keystream with the
+// write tag of the chunk before (its ciphertext still in the stage), (B) the
+// write-epoch keystream with the read tag of this chunk.  The write tag of a
+// chunk is therefore stored one chunk later (the last one after the loop).
+template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4, bool FUSED = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
+  static_assert(!FUSED || (AUTH && U == 8), "the fused pass is the sealed one, 8 rows per chunk");
   constexpr uint32_t kT = 64u * NW;  // rows per tile
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
   __shared__ uint32_t s_sh[kSlotMax];  // this batch's slot -> position of the row's first op
@@ -391,6 +468,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   uint4* sslot = a.snap + sbase * 64;
   uint4* dry = a.dry + (uint64_t)w * 64;
   const uint32_t tiles = a.S / kT;
+  // FUSED: the lane's leaf key, and the chunk whose write tag is pending
+  B2State lk{};
+  if constexpr (FUSED) lk = leaf_key128(a.sc, lane & 7u);
+  uint64_t hpend[2] = {0, 0}, prev_r0 = 0;
+  bool have_prev = false;
   for (uint32_t t = 0; t < tiles; ++t) {
     uint32_t xc = 0;
     const uint32_t rb = t * kT + wave * 64;
@@ -410,66 +492,57 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
       const uint64_t r0 = rowbase + rb + j;  // physical row of v[0]
       const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
-      if (AUTH) {
-        const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
-        if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
-          atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-      }
-      uint32_t mp = 0, ms = 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        mp |= s_pk[rb + j + u] >= 0 ? (1u << u) : 0u;
-        ms |= s_sk[rb + j + u] >= 0 ? (1u << u) : 0u;
-      }
-      mp = __builtin_amdgcn_readfirstlane(mp);
-      ms = __builtin_amdgcn_readfirstlane(ms);
-      // The first chunk of wave 0 runs each loop once "dry" on the workgroup's
-      // own dry line, so every workgroup executes the same code whatever its
-      // slots hold (instruction fetch shows in FETCH_SIZE, DESIGN.md §3 rule 6).
-      // The dry iteration is an extra mask bit (1 << U), taken last by the
-      // same loop code: a loop whose first iteration were special could be
-      // peeled by the compiler, and then not every workgroup would fetch the
-      // loop's code.
       const bool first = t == 0 && j == 0 && wave == 0;
-      uint32_t mq = mp | (first ? (1u << U) : 0u);
-      while (mq) {  // rows the previous batch changed: its final state
-        const uint32_t low = mq & (0u - mq);
-        mq &= mq - 1u;
-        const bool dry_p = low == (1u << U);
-        const uint32_t bit = dry_p ? 0u : low;
-        const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
-        const int16_t k = dry_p ? (int16_t)0 : s_pk[rb + j + u0];
-        const uint4* src = dry_p ? dry : a.ps + (sbase + (uint64_t)k) * 64;
-        const uint4 x = ld_row<true>(&src[lane]);
-        if (AUTH) {  // the final state must be the one sealed for this row
-          const uint4 sd = uni4(dry_p ? dry[0] : a.psds[(sbase + (uint64_t)k) * 8]);
-          if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
+      if constexpr (FUSED) {
+        const LdsTe te = lds_te(s_te);
+        // one copy of the fused code: phase 0 = (A), phase 1 = (B)
+#pragma unroll 1
+        for (uint32_t ph = 0; ph < 2; ++ph) {
+          uint64_t m[16], dig[2], tg[2];
+          uint4 ks[8];
+          // the leaf to hash, then the chunk (ciphertext in (A), plaintext in
+          // (B)) waits in the stage instead of registers while the fused code runs
+          stage_leaf8(st, m);
+          wave_lds_sync();
+          stage_rows<U>(v, st);
+          fused_ks8_leaf(a.sc, te, 0u, r0, a.sc.epoch + ph, lk, m, ks, dig);
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u] = xor4(st[stage_slot(u, lane)], ks[u]);
+          const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
+          const uint64_t hh[2] = {ph ? hvr[0] : hpend[0], ph ? hvr[1] : hpend[1]};
+          tag_finish8(dig, hh, tg);
+          const uint32_t ur = (lane >> 2) & 7u;
+          if (ph == 0) {
+            if (have_prev && (lane & 3u) == 0u && lane < 32u)
+              a.mtag[prev_r0 + ur] = make_uint4((uint32_t)tg[0], (uint32_t)(tg[0] >> 32), (uint32_t)tg[1],
+                                                (uint32_t)(tg[1] >> 32));
+            xc = rpass_chunk_merge<U, AUTH>(a, v, rb + j, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+                                            s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
+          } else {
+            const uint4 want = a.mtag[r0 + ur];
+            if (__ballot(lane < 32u && (u4lo(want) != tg[0] || u4hi(want) != tg[1])) != 0ull && lane == 0)
+              atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
+            wave_lds_sync();
+            stage_rows<U>(v, st);  // the new ciphertext: its tag is taken by the next (A)
+            const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
+            hpend[0] = hsr[0];
+            hpend[1] = hsr[1];
+            prev_r0 = r0;
+            have_prev = true;
+          }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
-      }
-      uint32_t sq = ms | (first ? (1u << U) : 0u);
-      while (sq) {  // rows this batch touches: their snapshot
-        const uint32_t low = sq & (0u - sq);
-        sq &= sq - 1u;
-        const bool dry_s = low == (1u << U);
-        const uint32_t bit = dry_s ? 0u : low;
-        const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31));
-        const int16_t k = dry_s ? (int16_t)0 : s_sk[rb + j + (u0 & 31u)];
-        uint4 cur = v[0];
-#pragma unroll
-        for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
-        // the snapshot goes to the position of the row's first op, so that
-        // every op of the phase-C scans reads its own position's line
-        const uint32_t hp = s_sh[(uint32_t)k & (kSlotMax - 1u)];
-        uint4* dst = dry_s ? dry : a.snapp + (uint64_t)hp * 64;
-        st_drop(dst, lane, cur);
-        if (lane < 8) st_drop(dry_s ? dry : a.snapidp + (uint64_t)hp * 8, lane, cur);
-      }
-      if (a.xon) xc = x_detect2<U>(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
-      if (AUTH) {
-        const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
-        wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
+      } else {
+        if (AUTH) {
+          const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
+          if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
+            atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
+        }
+        xc = rpass_chunk_merge<U, AUTH>(a, v, rb + j, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+                                        s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
+        if (AUTH) {
+          const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
+          wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
@@ -481,6 +554,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       __syncthreads();
       if (tid == 0) s_xt = tot;
     }
+  }
+  if constexpr (FUSED) {  // the write tag of the wave's last chunk
+    uint64_t m[16], dig[2], tg[2];
+    stage_leaf8(st, m);
+    leaf_prf128(lk, m, dig);
+    tag_finish8(dig, hpend, tg);
+    if ((lane & 3u) == 0u && lane < 32u)
+      a.mtag[prev_r0 + ((lane >> 2) & 7u)] =
+          make_uint4((uint32_t)tg[0], (uint32_t)(tg[0] >> 32), (uint32_t)tg[1], (uint32_t)(tg[1] >> 32));
   }
   // unused slots (slots are dense from 0: [np, c) were not used by the
   // previous batch): every slot's final-state line is read once per pass

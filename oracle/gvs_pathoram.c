@@ -24,9 +24,12 @@
  * Every request costs exactly six top-level ORAM accesses (occupancy, two
  * per cuckoo access to the mailbox and the message tables, occupancy), real
  * or dummy, so READ / UPDATE / DELETE are indistinguishable by access count
- * (grapevine.proto:120-122).  Data moves inside an access use memcpy rather
- * than constant-time cmov, so this is an optimistic (fast) baseline for the
- * reference's CPU path.
+ * (grapevine.proto:120-122).  Inside an access every block move is an
+ * aligned cmov over every stash and branch slot (mc-oblivious's semantics,
+ * README.md:49-50): the block is selected out of all slots and written back
+ * into all of them under masks, and eviction is a Circuit-ORAM style single
+ * pass with one held block (cmov over every slot of every level), along the
+ * accessed branch and one deterministic reverse-lexicographic path.
  *
  * It is an independent second implementation of the handler: tests check it
  * bit-for-bit against the seqmodel (gvs_oracle.c) on seeded streams, and
@@ -38,6 +41,22 @@
 #include "gvs_oracle.h"
 
 #define Z 4
+#define STASH 32 /* stash entries, every one scanned on every access */
+
+/* ---------------------------------------------------- aligned cmov */
+
+/* All-ones when c, else zero: the masks below select without a branch on
+ * the secret (the C restatement of mc-oblivious's aligned cmov;
+ * README.md:49-50). */
+static inline uint64_t mask_of(int c) { return (uint64_t)0 - (uint64_t)(c != 0); }
+
+/* dst <- src where mask, word by word (block sizes are multiples of 8) */
+static inline void cmov_block(uint8_t *dst, const uint8_t *src, size_t n, uint64_t mask) {
+  uint64_t *d = (uint64_t *)dst;
+  const uint64_t *s = (const uint64_t *)src;
+  for (size_t i = 0; i < n / 8; ++i) d[i] = (d[i] & ~mask) | (s[i] & mask);
+}
+static inline uint64_t cmov_u64(uint64_t a, uint64_t b, uint64_t mask) { return (a & ~mask) | (b & mask); }
 
 /* ------------------------------------------------------------------ ORAM */
 
@@ -49,19 +68,20 @@ typedef struct oram {
   uint8_t *data;    /* nodes * Z * bsz */
   uint64_t *meta;   /* nodes * Z: 0 = empty, else index + 1 */
   uint32_t *leaf;   /* nodes * Z */
-  uint32_t scap, scount;
-  uint8_t *sdata;
+  uint8_t *sdata;   /* STASH entries */
   uint64_t *smeta;
   uint32_t *sleaf;
   uint32_t *pm_plain; /* position map when small */
   struct oram *pm;    /* recursive position map */
   uint32_t pm_ent;    /* leaves per position-map block */
   uint64_t *rng;
-  /* per-access scratch: path (L+1)*Z slots + stash */
+  /* the checked-out branch (root .. leaf, Z slots per level) and the block
+     being accessed */
   uint8_t *wdata;
   uint64_t *wmeta;
   uint32_t *wleaf;
-  uint32_t wcap;
+  uint8_t *tmp, *hold;
+  uint64_t evictions;  /* deterministic eviction paths taken so far */
   uint64_t accesses;
 } oram;
 
@@ -84,6 +104,8 @@ static void oram_free(oram *o) {
   free(o->wdata);
   free(o->wmeta);
   free(o->wleaf);
+  free(o->tmp);
+  free(o->hold);
   oram_free(o->pm);
   free(o);
 }
@@ -102,16 +124,16 @@ static oram *oram_new(uint64_t n, uint32_t bsz, uint64_t *rng) {
   o->data = (uint8_t *)calloc(o->nodes * Z, bsz);
   o->meta = (uint64_t *)calloc(o->nodes * Z, sizeof(uint64_t));
   o->leaf = (uint32_t *)calloc(o->nodes * Z, sizeof(uint32_t));
-  o->scap = 256;
-  o->sdata = (uint8_t *)calloc(o->scap, bsz);
-  o->smeta = (uint64_t *)calloc(o->scap, sizeof(uint64_t));
-  o->sleaf = (uint32_t *)calloc(o->scap, sizeof(uint32_t));
-  o->wcap = (o->L + 1) * Z + o->scap + 1;
-  o->wdata = (uint8_t *)calloc(o->wcap, bsz);
-  o->wmeta = (uint64_t *)calloc(o->wcap, sizeof(uint64_t));
-  o->wleaf = (uint32_t *)calloc(o->wcap, sizeof(uint32_t));
+  o->sdata = (uint8_t *)calloc(STASH, bsz);
+  o->smeta = (uint64_t *)calloc(STASH, sizeof(uint64_t));
+  o->sleaf = (uint32_t *)calloc(STASH, sizeof(uint32_t));
+  o->wdata = (uint8_t *)calloc((size_t)(o->L + 1) * Z, bsz);
+  o->wmeta = (uint64_t *)calloc((size_t)(o->L + 1) * Z, sizeof(uint64_t));
+  o->wleaf = (uint32_t *)calloc((size_t)(o->L + 1) * Z, sizeof(uint32_t));
+  o->tmp = (uint8_t *)calloc(1, bsz);
+  o->hold = (uint8_t *)calloc(1, bsz);
   if (!o->data || !o->meta || !o->leaf || !o->sdata || !o->smeta || !o->sleaf || !o->wdata ||
-      !o->wmeta || !o->wleaf) {
+      !o->wmeta || !o->wleaf || !o->tmp || !o->hold) {
     oram_free(o);
     return NULL;
   }
@@ -162,80 +184,169 @@ static uint32_t pm_swap(oram *o, uint64_t idx, uint32_t newleaf) {
 
 static inline uint64_t path_node(const oram *o, uint32_t leaf, uint32_t depth) {
   /* node at `depth` (0 = root) on the path to `leaf`, heap numbering */
-  uint64_t x = o->leaves - 1 + leaf;
-  for (uint32_t d = o->L; d > depth; --d) x = (x - 1) / 2;
-  return x;
+  return ((o->leaves - 1 + leaf + 1) >> (o->L - depth)) - 1;
 }
 
-/* Path ORAM access: remap, read path + stash, apply fn, greedy evict. */
-static void oram_access(oram *o, uint64_t idx, access_fn fn, void *ctx) {
+static void branch_io(oram *o, uint32_t leaf, int out) {
   const uint32_t bsz = o->bsz;
+  for (uint32_t d = 0; d <= o->L; ++d) {
+    const uint64_t s = path_node(o, leaf, d) * Z;
+    uint8_t *t = o->data + s * bsz, *w = o->wdata + (size_t)d * Z * bsz;
+    memcpy(out ? t : w, out ? w : t, (size_t)Z * bsz);
+    memcpy(out ? o->meta + s : o->wmeta + d * Z, out ? o->wmeta + d * Z : o->meta + s, Z * sizeof(uint64_t));
+    memcpy(out ? o->leaf + s : o->wleaf + d * Z, out ? o->wleaf + d * Z : o->leaf + s, Z * sizeof(uint32_t));
+  }
+}
+
+/* deepest level (0 = root .. L) of branch `b` that a block of leaf `lf`
+ * may live at; -1 for an empty slot */
+static inline int32_t deepest_level(const oram *o, uint64_t meta, uint32_t lf, uint32_t b) {
+  const uint32_t x = lf ^ b;
+  const int32_t h = x ? 31 - __builtin_clz(x) : -1; /* highest set bit of x (lzcnt) */
+  const int32_t d = (int32_t)o->L - h - 1;
+  return meta ? d : -1;
+}
+
+/* Circuit-ORAM style single-pass eviction of the checked-out branch `b`
+ * (Wang, Chan, Shi, CCS 2015: PrepareDeepest, PrepareTarget, EvictOnce):
+ * the metadata passes choose at most one block to move down per level, then
+ * one pass from the stash to the leaf carries it ("hold") with aligned cmov
+ * over every slot of every level.  Level -1 is the stash.  The work done is
+ * the same whatever the slots hold. */
+static void evict_branch(oram *o, uint32_t b) {
+  const uint32_t L = o->L, bsz = o->bsz;
+  int32_t deepest[66], target[66]; /* index level + 1 */
+  /* PrepareDeepest */
+  int32_t src = -2, goal = -1;
+  {
+    int32_t g = -1;
+    for (uint32_t s = 0; s < STASH; ++s) {
+      const int32_t d = deepest_level(o, o->smeta[s], o->sleaf[s], b);
+      g = d > g ? d : g;
+    }
+    src = g >= 0 ? -1 : -2;
+    goal = g;
+  }
+  deepest[0] = -2;
+  for (uint32_t i = 0; i <= L; ++i) {
+    deepest[i + 1] = goal >= (int32_t)i ? src : -2;
+    int32_t l = -1;
+    for (uint32_t z = 0; z < Z; ++z) {
+      const int32_t d = deepest_level(o, o->wmeta[i * Z + z], o->wleaf[i * Z + z], b);
+      l = d > l ? d : l;
+    }
+    const int c = l > goal;
+    goal = c ? l : goal;
+    src = c ? (int32_t)i : src;
+  }
+  /* PrepareTarget */
+  int32_t dest = -2;
+  src = -2;
+  for (int32_t i = (int32_t)L; i >= -1; --i) {
+    target[i + 1] = -2;
+    const int hit = i == src;
+    target[i + 1] = hit ? dest : target[i + 1];
+    dest = hit ? -2 : dest;
+    src = hit ? -2 : src;
+    int empty = 0;
+    if (i >= 0)
+      for (uint32_t z = 0; z < Z; ++z) empty |= o->wmeta[i * Z + z] == 0;
+    const int take = ((dest == -2 && empty) || target[i + 1] != -2) && deepest[i + 1] != -2;
+    src = take ? deepest[i + 1] : src;
+    dest = take ? i : dest;
+  }
+  /* EvictOnce: level -1 (stash) .. L */
+  uint64_t hmeta = 0;
+  uint32_t hleaf = 0;
+  int32_t hdest = -2;
+  for (int32_t i = -1; i <= (int32_t)L; ++i) {
+    const uint32_t nslot = i < 0 ? STASH : Z;
+    uint8_t *bd = i < 0 ? o->sdata : o->wdata + (size_t)i * Z * bsz;
+    uint64_t *bm = i < 0 ? o->smeta : o->wmeta + (size_t)i * Z;
+    uint32_t *bl = i < 0 ? o->sleaf : o->wleaf + (size_t)i * Z;
+    /* the held block drops here */
+    const int drop = hmeta != 0 && i == hdest;
+    uint8_t *tw = o->tmp; /* towrite */
+    cmov_block(tw, o->hold, bsz, mask_of(drop));
+    const uint64_t twm = drop ? hmeta : 0;
+    const uint32_t twl = drop ? hleaf : 0;
+    hmeta = drop ? 0 : hmeta;
+    hdest = drop ? -2 : hdest;
+    /* pick up the block of this level that goes deepest */
+    const int pick = target[i + 1] != -2;
+    int32_t best = -1, bz = -1;
+    for (uint32_t z = 0; z < nslot; ++z) {
+      const int32_t d = deepest_level(o, bm[z], bl[z], b);
+      const int c = d > best;
+      best = c ? d : best;
+      bz = c ? (int32_t)z : bz;
+    }
+    for (uint32_t z = 0; z < nslot; ++z) {
+      const uint64_t m = mask_of(pick && (int32_t)z == bz);
+      cmov_block(o->hold, bd + (size_t)z * bsz, bsz, m);
+      hmeta = cmov_u64(hmeta, bm[z], m);
+      hleaf = (uint32_t)cmov_u64(hleaf, bl[z], m);
+      bm[z] = cmov_u64(bm[z], 0, m);
+    }
+    hdest = pick ? target[i + 1] : hdest;
+    /* the dropped block takes the first empty slot */
+    int placed = !drop;
+    for (uint32_t z = 0; z < nslot; ++z) {
+      const int c = !placed && bm[z] == 0;
+      const uint64_t m = mask_of(c);
+      cmov_block(bd + (size_t)z * bsz, tw, bsz, m);
+      bm[z] = cmov_u64(bm[z], twm, m);
+      bl[z] = (uint32_t)cmov_u64(bl[z], twl, m);
+      placed |= c;
+    }
+    if (!placed) abort(); /* the targets guarantee room */
+  }
+}
+
+/* reverse-lexicographic eviction path g (Gentry et al.; Circuit ORAM) */
+static uint32_t revlex(const oram *o, uint64_t g) {
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < o->L; ++k) r |= (uint32_t)((g >> k) & 1u) << (o->L - 1 - k);
+  return r;
+}
+
+/* Path ORAM access with aligned-cmov block moves: remap, check out the
+ * branch, select the block out of every stash and branch slot, apply fn,
+ * move it to the first free stash slot, evict along the branch and along one
+ * deterministic path, check in. */
+static void oram_access(oram *o, uint64_t idx, access_fn fn, void *ctx) {
+  const uint32_t bsz = o->bsz, W = (o->L + 1) * Z;
   const uint32_t newleaf = (uint32_t)(sm64(o->rng) % o->leaves);
   const uint32_t old = pm_swap(o, idx, newleaf) % (uint32_t)o->leaves;
   o->accesses++;
-  /* gather path (root..leaf) and stash into the work set */
-  uint32_t w = 0;
-  uint64_t nodes[64];
-  /* the whole path is read, empty slots included (an oblivious ORAM reads and
-     writes every bucket of the path whatever it holds) */
-  for (uint32_t d = 0; d <= o->L; ++d) {
-    nodes[d] = path_node(o, old, d);
-    const uint64_t s = nodes[d] * Z;
-    memcpy(o->wdata + (size_t)w * bsz, o->data + s * bsz, (size_t)Z * bsz);
-    for (uint32_t z = 0; z < Z; ++z) {
-      o->wmeta[w + z] = o->meta[s + z];
-      o->wleaf[w + z] = o->leaf[s + z];
-    }
-    w += Z;
+  branch_io(o, old, 0);
+  /* the block, out of every slot (zero if it is new) */
+  uint8_t *t = o->hold; /* hold is free outside evict_branch */
+  memset(t, 0, bsz);
+  for (uint32_t s = 0; s < STASH; ++s)
+    cmov_block(t, o->sdata + (size_t)s * bsz, bsz, mask_of(o->smeta[s] == idx + 1));
+  for (uint32_t w = 0; w < W; ++w)
+    cmov_block(t, o->wdata + (size_t)w * bsz, bsz, mask_of(o->wmeta[w] == idx + 1));
+  fn(ctx, t);
+  /* the block leaves its slot and goes to the first free stash slot with its
+     new leaf (a block stays only on the path of its own leaf) */
+  for (uint32_t s = 0; s < STASH; ++s) o->smeta[s] = cmov_u64(o->smeta[s], 0, mask_of(o->smeta[s] == idx + 1));
+  for (uint32_t w = 0; w < W; ++w) o->wmeta[w] = cmov_u64(o->wmeta[w], 0, mask_of(o->wmeta[w] == idx + 1));
+  uint64_t placed = 0;
+  for (uint32_t s = 0; s < STASH; ++s) {
+    const uint64_t m = ~placed & mask_of(o->smeta[s] == 0);
+    cmov_block(o->sdata + (size_t)s * bsz, t, bsz, m);
+    o->smeta[s] = cmov_u64(o->smeta[s], idx + 1, m);
+    o->sleaf[s] = (uint32_t)cmov_u64(o->sleaf[s], newleaf, m);
+    placed |= m;
   }
-  for (uint32_t i = 0; i < o->scount; ++i) {
-    memcpy(o->wdata + (size_t)w * bsz, o->sdata + (size_t)i * bsz, bsz);
-    o->wmeta[w] = o->smeta[i];
-    o->wleaf[w] = o->sleaf[i];
-    ++w;
-  }
-  /* locate (or create) the target block */
-  uint32_t t = w;
-  for (uint32_t i = 0; i < w; ++i)
-    if (o->wmeta[i] == idx + 1) t = i;
-  /* empty slots are never placed back */
-  if (t == w) {
-    memset(o->wdata + (size_t)w * bsz, 0, bsz);
-    o->wmeta[w] = idx + 1;
-    ++w;
-  }
-  o->wleaf[t] = newleaf;
-  fn(ctx, o->wdata + (size_t)t * bsz);
-  /* greedy eviction from the leaf up */
-  uint8_t placed[1024];
-  for (uint32_t i = 0; i < w; ++i) placed[i] = o->wmeta[i] == 0;
-  for (int d = (int)o->L; d >= 0; --d) {
-    uint32_t cnt = 0;
-    const uint32_t shift = o->L - (uint32_t)d;
-    const uint64_t base = nodes[d] * Z;
-    for (uint32_t i = 0; i < w && cnt < Z; ++i) {
-      if (placed[i] || (o->wleaf[i] >> shift) != (old >> shift)) continue;
-      memcpy(o->data + (base + cnt) * bsz, o->wdata + (size_t)i * bsz, bsz);
-      o->meta[base + cnt] = o->wmeta[i];
-      o->leaf[base + cnt] = o->wleaf[i];
-      placed[i] = 1;
-      ++cnt;
-    }
-    for (; cnt < Z; ++cnt) {
-      memset(o->data + (base + cnt) * bsz, 0, bsz);
-      o->meta[base + cnt] = 0;
-    }
-  }
-  uint32_t sc = 0;
-  for (uint32_t i = 0; i < w; ++i) {
-    if (placed[i]) continue;
-    if (sc >= o->scap) abort(); /* stash overflow: negligible at Z = 4 */
-    memcpy(o->sdata + (size_t)sc * bsz, o->wdata + (size_t)i * bsz, bsz);
-    o->smeta[sc] = o->wmeta[i];
-    o->sleaf[sc] = o->wleaf[i];
-    ++sc;
-  }
-  o->scount = sc;
+  if (!placed) abort(); /* stash overflow: negligible at Z = 4, 25 % load */
+  evict_branch(o, old);
+  branch_io(o, old, 1);
+  const uint32_t e = revlex(o, o->evictions++);
+  branch_io(o, e, 0);
+  evict_branch(o, e);
+  branch_io(o, e, 1);
 }
 
 /* ---------------------------------------------------- cuckoo hash table */

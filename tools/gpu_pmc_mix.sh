@@ -3,7 +3,7 @@
 # PMC_RUNS="mix:seed ..." (default main:1234 main:99 all_miss_read:1234 all_miss_read:99)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/pmc_mix
+O=${PMC_OUT:-gpurun_out/pmc_mix}
 mkdir -p "$O"
 CTRS=${PMC_CTRS:-TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum}
 ARGS=${PMC_ARGS:---log2n 20 --batch 65536}

@@ -41,6 +41,10 @@ case "$2" in
   probe) step hbm_probe 300 tools/hbm_probe 16 ;;
   tob) tests && step oblivious_all 1000 $PT tests/test_oblivious.py && step hbm_probe 300 tools/hbm_probe 16 && bench ;;
   oblall) step oblivious_all 1150 $PT tests/test_oblivious.py ;;
+  oblplain)  # plain-shape counters, then L2 hit/miss per kernel for two mixes
+    step oblivious_plain 900 $PT tests/test_oblivious.py -k "plain"
+    PMC_KERN=${PMC_KERN:-k_vscan_a,k_rr2_c,k_m2r_c,k_bitonic_global2,k_m1x,k_scan_c} \
+      step pmc_mix 400 bash tools/gpu_pmc_mix.sh ;;
   all) tests && bench && timing ;;
   full) tests && timing && step oblivious_all 1150 $PT tests/test_oblivious.py ;;
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines
