@@ -19,6 +19,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/gvstore.h"
@@ -153,6 +154,8 @@ struct Engine {
 // Router state of one source rank (kLocal: one per virtual rank).
 struct Router {
   uint32_t* dest = nullptr;
+  uint64_t* rkey = nullptr;  // routing keys, sorted per window (hot-key cap)
+  uint32_t* shed = nullptr;
   uint32_t* bcnt = nullptr;
   uint32_t* pos = nullptr;
   uint32_t* tot = nullptr;
@@ -612,6 +615,8 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
 static int router_init(gvs_handle* h, Router& r) {
   const uint64_t B = h->Bsub, SC = (uint64_t)h->S * h->C;
   if (int rc = dalloc_t(h, &r.dest, B)) return rc;
+  if (int rc = dalloc_t(h, &r.rkey, B)) return rc;
+  if (int rc = dalloc_t(h, &r.shed, B)) return rc;
   if (int rc = dalloc_t(h, &r.bcnt, (B / 1024) * h->S)) return rc;
   if (int rc = dalloc_t(h, &r.pos, B)) return rc;
   if (int rc = dalloc_t(h, &r.tot, h->S)) return rc;
@@ -1038,6 +1043,8 @@ static RouteArgs rargs(gvs_handle* h, const Router& r, const Engine& e, const ui
   a.S = h->S;
   a.C = h->C;
   a.dest = r.dest;
+  a.rkey = r.rkey;
+  a.shed = r.shed;
   a.bcnt = r.bcnt;
   a.pos = r.pos;
   a.tot = r.tot;
@@ -1048,14 +1055,19 @@ static RouteArgs rargs(gvs_handle* h, const Router& r, const Engine& e, const ui
   return a;
 }
 
-static void route(gvs_handle* h, const Router& r, const Engine& e, const uint4* in, uint32_t n) {
+static int route(gvs_handle* h, const Router& r, const Engine& e, const uint4* in, uint32_t n) {
   hipStream_t s = h->stream;
   const RouteArgs a = rargs(h, r, e, in, n);
   const uint32_t nblk = h->Bsub / 1024;
   hipLaunchKernelGGL(k_route_dest, dim3(nblk), dim3(1024), 0, s, a);
+  if (int rc = sort_keys<uint64_t, 8>(h, r.rkey, h->Bsub)) return rc;  // by (routing key, index)
+  hipLaunchKernelGGL(k_route_cap, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_route_hist, dim3(nblk), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_route_pos, dim3(nblk), dim3(1024), 0, s, a);
   if (n) hipLaunchKernelGGL(k_route_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_route_fill, dim3((h->S * h->C + 3) / 4), dim3(256), 0, s, a);
+  GVS_HIP(h, hipGetLastError());
+  return GVS_OK;
 }
 
 static int reset_errors(gvs_handle* h) {
@@ -1130,7 +1142,7 @@ static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d
   for (uint32_t k = 0; k < n_src; ++k) {
     const uint64_t off = (uint64_t)k * h->Bsub;
     const uint32_t nk = n > off ? (uint32_t)std::min<uint64_t>(n - off, h->Bsub) : 0u;
-    route(h, h->rt[k], h->eng[k], d_in + off * kAbiU4, nk);
+    if (int r = route(h, h->rt[k], h->eng[k], d_in + off * kAbiU4, nk)) return r;
   }
   mark(h, "route");
   if (int r = exchange(h, true)) return r;
@@ -1149,8 +1161,8 @@ static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d
     const uint32_t nk = n > off ? (uint32_t)std::min<uint64_t>(n - off, h->Bsub) : 0u;
     if (nk)
       hipLaunchKernelGGL(k_route_gather, dim3((nk + 3) / 4), dim3(256), 0, h->stream,
-                         (const uint32_t*)h->rt[k].pos, (const uint4*)h->rt[k].back, nk,
-                         d_out + off * kAbiU4);
+                         (const uint32_t*)h->rt[k].pos, (const uint32_t*)h->rt[k].shed,
+                         d_in + off * kAbiU4, (const uint4*)h->rt[k].back, nk, d_out + off * kAbiU4);
   }
   mark(h, "gather");
   GVS_HIP(h, hipGetLastError());
@@ -2371,11 +2383,14 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
 }
 
 
+// the block store's engine handle, for the raw-region hooks above
+gvs_handle* gvs_oram_test_handle(gvs_oram* o) { return o ? o->h : nullptr; }
+
 // The router's placement on the host, with the device's route_dest (see
 // include/gvstore_test.h): slot[i] = d * C + rank of request i among this
 // source's requests for shard d, or 0xFFFFFFFF past C.
 int gvs_route_plan(const gvs_config* cfg, const gvs_request* reqs, uint32_t n, uint32_t* slot,
-                   uint32_t* capacity, uint32_t* shard_batch_out) {
+                   uint32_t* capacity, uint32_t* shard_batch_out, uint8_t* shed) {
   if (!cfg || (n && (!reqs || !slot))) return GVS_ERR_INVALID_ARG;
   if (int rc = validate(cfg)) return rc;
   const uint32_t S = cfg->shard_count ? cfg->shard_count : 1u, B = cfg->max_batch;
@@ -2394,9 +2409,25 @@ int gvs_route_plan(const gvs_config* cfg, const gvs_request* reqs, uint32_t n, u
   a.kc.hk1 = ld64(cfg->secret_key + 24);
   a.kc.nshards = S;
   std::vector<uint32_t> cnt(S, 0);
+  std::vector<uint64_t> keys(n);
+  std::vector<uint32_t> dest(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t k;
+    dest[i] = route_dest_key(a, i, k);
+    keys[i] = ((uint64_t)k << 32) | i;
+  }
+  std::sort(keys.begin(), keys.end());  // the hot-key cap, as k_route_cap
+  if (shed) std::fill(shed, shed + n, (uint8_t)0);
+  for (uint32_t j = kRouteKeyCap; j < n; ++j) {
+    const uint32_t k = (uint32_t)(keys[j] >> 32), i = (uint32_t)keys[j];
+    if ((k & 3u) != kKeyNone && (uint32_t)(keys[j - kRouteKeyCap] >> 32) == k) {
+      dest[i] = i % S;
+      if (shed) shed[i] = 1;
+    }
+  }
   bool over = false;
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t d = route_dest(a, i);
+    const uint32_t d = dest[i];
     const uint32_t r = cnt[d]++;
     over |= r >= C;
     slot[i] = r < C ? d * C + r : kNone;

@@ -13,6 +13,15 @@
 // all-to-all.  Slots are 1152 B (9 whole 128-B lines) so that no line is ever
 // shared between two requests; every slot is written by one wave.  Sizes seen
 // outside the device are S, C and B only.
+//
+// Hot keys [D] (DESIGN.md §6 "Hot keys"): a source routes at most kRouteKeyCap
+// requests per routing key (the mailbox a create or a next-message op
+// addresses, the id of a by-id op) in one window.  The later ones are shed:
+// they travel as hard errors to the shard i mod S (spread like malformed
+// requests, so they never load the hot key's shard) and the source answers
+// them INTERNAL_ERROR (8) with the request's time.  One recipient can then put
+// at most kRouteKeyCap requests of one kind into a bucket, and a hostile
+// client fails only its own excess requests instead of the whole window.
 #pragma once
 #include "gvs_device.h"
 
@@ -21,11 +30,15 @@ namespace gvs {
 constexpr uint32_t kSlotU4 = kRespSlot / 16;  // 72 x 16 B per routed slot
 constexpr uint32_t kAbiU4 = 65;               // gvs_request / gvs_response: 1040 B
 constexpr uint32_t kShardsMax = 64;
+constexpr uint32_t kRouteKeyCap = 64;  // requests routed per routing key, per source window
+constexpr uint32_t kKeyNone = 0u;      // routing-key class of unkeyed requests (never shed)
 
 struct RouteArgs {
   const uint4* in;   // caller requests (kAbiU4 stride)
   uint32_t n, B, S, C;
   uint32_t* dest;    // B
+  uint64_t* rkey;    // B: routing key << 32 | index, sorted by k_route_cap's caller
+  uint32_t* shed;    // B: 1 = shed (the key's cap was reached)
   uint32_t* bcnt;    // nblk * S: per-block per-shard counts
   uint32_t* pos;     // B: slot in `send`, or kNone
   uint32_t* tot;     // S: per-shard totals of this source
@@ -35,9 +48,12 @@ struct RouteArgs {
   KeyCtx kc;
 };
 
-// request i -> owning shard (S = padding, i >= n).  Host and device: the
-// test library's gvs_route_plan runs this same function on the CPU.
-__host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
+// request i -> owning shard (S = padding, i >= n) and its 32-bit routing key
+// (low 2 bits: 1 create, 2 next-message op, 3 by-id op, 0 unkeyed).  Host and
+// device: the test library's gvs_route_plan runs this same function on the
+// CPU; oracle/gvs_oracle.c gvo_route_key restates the key.
+__host__ __device__ inline uint32_t route_dest_key(const RouteArgs& a, uint32_t i, uint32_t& key) {
+  key = kKeyNone;
   if (i >= a.n) return a.S;
   const uint4* r = a.in + (uint64_t)i * kAbiU4;
   const uint4 c0 = r[0], c1 = r[1], c2 = r[2], c3 = r[3], c4 = r[4];
@@ -54,20 +70,70 @@ __host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
   const uint32_t by_key = shard_of_hash(lo, a.S);
   const uint32_t by_id = id_shard(a.kc, u4lo(c0), u4hi(c0), a.N);
   const uint32_t spread = i % a.S;
+  const uint32_t kh = (uint32_t)(lo >> 32) & ~3u, ki = (c0.x ^ c0.y ^ c0.z ^ c0.w) & ~3u;
   if (hard) return spread;
-  if (type == 1u) return rcpt_zero ? spread : by_key;
-  if (next) return by_key;
+  if (type == 1u) {
+    key = rcpt_zero ? kKeyNone : kh | 1u;
+    return rcpt_zero ? spread : by_key;
+  }
+  if (next) {
+    key = kh | 2u;
+    return by_key;
+  }
+  key = ki | 3u;
   return by_id != kNone ? by_id : spread;
 }
 
-// dest of every request + per-block per-shard histogram (all S bins stored)
+__host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
+  uint32_t key;
+  return route_dest_key(a, i, key);
+}
+
+// dest and routing key of every request (padding: unkeyed)
 __global__ __launch_bounds__(1024) void k_route_dest(RouteArgs a) {
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  uint32_t key;
+  a.dest[i] = route_dest_key(a, i, key);
+  a.rkey[i] = ((uint64_t)key << 32) | i;
+}
+
+// Over the keys sorted by (key, index): a request is shed when the request
+// kRouteKeyCap places before it has the same key (it is at least the
+// (kRouteKeyCap + 1)-th of its key in this window); a shed request goes to
+// shard i mod S.  One workgroup: the flags go through an LDS bitmap indexed
+// by request, so the data-dependent permutation (sorted position -> request)
+// stays inside one XCD's L2 (DESIGN.md §3 rule 4: scattered 4-B writes from
+// many workgroups made FETCH_SIZE follow the key order), and shed / dest are
+// written in request order.
+constexpr uint32_t kRouteCapWords = 16384;  // bitmap words: B <= 2^19
+__global__ __launch_bounds__(1024) void k_route_cap(RouteArgs a) {
+  __shared__ uint32_t s_bits[kRouteCapWords];
+  const uint32_t nw = (a.B + 31) / 32;
+  for (uint32_t w = threadIdx.x; w < nw; w += 1024) s_bits[w] = 0;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < a.B; j += 1024) {
+    const uint64_t k = a.rkey[j];
+    const uint64_t kp = a.rkey[j >= kRouteKeyCap ? j - kRouteKeyCap : j];
+    const uint32_t key = (uint32_t)(k >> 32), i = (uint32_t)k;
+    const bool shed = j >= kRouteKeyCap && (key & 3u) != kKeyNone && (uint32_t)(kp >> 32) == key;
+    atomicOr(&s_bits[i >> 5], (shed ? 1u : 0u) << (i & 31u));  // one per position, always
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.B; i += 1024) {
+    const bool shed = (s_bits[i >> 5] >> (i & 31u)) & 1u;
+    const uint32_t d = a.dest[i];
+    a.shed[i] = shed ? 1u : 0u;
+    a.dest[i] = shed ? i % a.S : d;
+  }
+}
+
+// per-block per-shard histogram of the final destinations (all S bins stored)
+__global__ __launch_bounds__(1024) void k_route_hist(RouteArgs a) {
   __shared__ uint32_t s_h[kShardsMax];
   const uint32_t tid = threadIdx.x, i = blockIdx.x * 1024 + tid;
   if (tid < a.S) s_h[tid] = 0;
   __syncthreads();
-  const uint32_t d = route_dest(a, i);
-  a.dest[i] = d;
+  const uint32_t d = a.dest[i];
   if (d < a.S) atomicAdd(&s_h[d], 1u);
   __syncthreads();
   if (tid < a.S) a.bcnt[blockIdx.x * a.S + tid] = s_h[tid];
@@ -117,7 +183,10 @@ __global__ __launch_bounds__(256) void k_route_copy(RouteArgs a) {
   const uint4* src = a.in + (uint64_t)i * kAbiU4;
   uint4* dst = a.send + (uint64_t)p * kSlotU4;
   dst[lane] = src[lane];
-  if (lane < 8) dst[64 + lane] = lane == 0 ? src[64] : make_uint4(0, 0, 0, 0);
+  // a shed request travels as a hard error (type 0): the shard changes nothing
+  const uint4 t = src[64];
+  const uint32_t sh = a.shed[i];
+  if (lane < 8) dst[64 + lane] = lane == 0 ? make_uint4(sh ? 0u : t.x, t.y, t.z, t.w) : make_uint4(0, 0, 0, 0);
 }
 
 // one wave per slot: zero-fill the slots no request took
@@ -132,8 +201,13 @@ __global__ __launch_bounds__(256) void k_route_fill(RouteArgs a) {
   if (lane < 8) dst[64 + lane] = z;
 }
 
-// one wave per request: its response (slot layout) back to the caller layout
+// one wave per request: its response (slot layout) back to the caller layout;
+// a shed request's response is INTERNAL_ERROR with the request's time (the
+// hard-error response its shard sent back is read and replaced, so every
+// request reads the same lines)
 __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ shed,
+                                                      const uint4* __restrict__ in,
                                                       const uint4* __restrict__ back, uint32_t n,
                                                       uint4* __restrict__ out) {
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
@@ -141,8 +215,11 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
   const uint32_t p = pos[i];
   if (p == kNone) return;  // overflowed batch: the call fails, out is undefined
   const uint4* src = back + (uint64_t)p * kSlotU4;
-  out[(uint64_t)i * kAbiU4 + lane] = src[lane];
-  if (lane == 0) out[(uint64_t)i * kAbiU4 + 64] = src[64];
+  const uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
+  const bool sh = shed[i] != 0u;
+  const uint4 fail = lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0);
+  out[(uint64_t)i * kAbiU4 + lane] = sh ? fail : src[lane];
+  if (lane == 0) out[(uint64_t)i * kAbiU4 + 64] = sh ? make_uint4(8u, 0, 0, 0) : src[64];
 }
 
 // single-process shards: OR of every shard's error word into each of them

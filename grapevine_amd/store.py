@@ -36,7 +36,7 @@ EXPORTED = (
     "gvs_host_alloc", "gvs_host_free", "gvs_process_wire_batches",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
-                 "gvs_route_plan")
+                 "gvs_route_plan", "gvs_oram_test_handle")
 
 
 def test_hooks_enabled():
@@ -96,7 +96,9 @@ def load_library(path=None):
         lib.gvs_dump_raw.argtypes = [vp, u32, u32, u64, vp, u64]
         lib.gvs_store_raw.argtypes = [vp, u32, u32, u64, vp, u64]
         P32 = ctypes.POINTER(u32)
-        lib.gvs_route_plan.argtypes = [ctypes.POINTER(abi.GvsConfig), vp, u32, vp, P32, P32]
+        lib.gvs_route_plan.argtypes = [ctypes.POINTER(abi.GvsConfig), vp, u32, vp, P32, P32, vp]
+        lib.gvs_oram_test_handle.argtypes = [vp]
+        lib.gvs_oram_test_handle.restype = vp
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p
@@ -120,26 +122,29 @@ def load_library(path=None):
     lib.gvs_omap_last_error.argtypes = [vp]
     lib.gvs_omap_last_error.restype = ctypes.c_char_p
     for name in EXPORTED + (TEST_EXPORTED if hooks else ()):
-        if name not in ("gvs_last_error", "gvs_version", "gvs_oram_last_error", "gvs_omap_last_error"):
+        if name not in ("gvs_last_error", "gvs_version", "gvs_oram_last_error", "gvs_omap_last_error",
+                        "gvs_oram_test_handle"):
             getattr(lib, name).restype = i32
     if path is None:
         _LIB = lib
     return lib
 
 
-def route_plan(config, reqs):
+def route_plan(config, reqs, with_shed=False):
     """The router's placement of one source's batch, on the host (test
     library, gvs_route_plan): -> (slot per request, C, shard pipeline size,
-    overflowed)."""
+    overflowed[, shed flags])."""
     lib = load_library(_TEST_LIB_PATH)
     reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
     slot = np.zeros(len(reqs), dtype=np.uint32)
+    shed = np.zeros(len(reqs), dtype=np.uint8)
     cap, be = ctypes.c_uint32(), ctypes.c_uint32()
     rc = lib.gvs_route_plan(ctypes.byref(config), reqs.ctypes.data, len(reqs), slot.ctypes.data,
-                            ctypes.byref(cap), ctypes.byref(be))
+                            ctypes.byref(cap), ctypes.byref(be), shed.ctypes.data)
     if rc not in (0, abi.GVS_ERR_BATCH_OVERFLOW):
         raise GvsError(rc, "gvs_route_plan failed")
-    return slot, cap.value, be.value, rc == abi.GVS_ERR_BATCH_OVERFLOW
+    out = (slot, cap.value, be.value, rc == abi.GVS_ERR_BATCH_OVERFLOW)
+    return out + (shed.astype(bool),) if with_shed else out
 
 
 def comm_unique_id():
@@ -431,6 +436,23 @@ class BlockStore:
     def access_device(self, d_ops, n, d_out):
         """Device pointers (ints): n ops in, n x 1024 bytes out."""
         self._check(self.lib.gvs_oram_access_batch_device(self.h, d_ops, n, d_out))
+
+    def _raw_handle(self):
+        if not hasattr(self.lib, "gvs_oram_test_handle"):
+            raise RuntimeError("raw regions need the test library (GVS_TEST_HOOKS=1)")
+        return self.lib.gvs_oram_test_handle(self.h)
+
+    def dump_raw(self, region, offset, nbytes):
+        """Raw device bytes of the block table (abi.RAW_MESSAGES), its tags
+        (RAW_MSG_TAGS) or its pending final states (RAW_PENDING*).  Test use."""
+        out = np.zeros(nbytes, dtype=np.uint8)
+        self._check(self.lib.gvs_dump_raw(self._raw_handle(), 0, region, offset, out.ctypes.data, nbytes))
+        return out
+
+    def store_raw(self, region, offset, data):
+        """Overwrite raw device bytes (tamper tests of the sealed block store)."""
+        buf = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+        self._check(self.lib.gvs_store_raw(self._raw_handle(), 0, region, offset, buf.ctypes.data, len(buf)))
 
     def set_timing(self, on=True):
         self._check(self.lib.gvs_oram_set_timing(self.h, 1 if on else 0))

@@ -29,14 +29,21 @@ int gvs_dump_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset
 int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offset,
                   const void *src, uint64_t bytes);
 
+/* The engine handle under a block store (gvs_oram_*), so that the raw-region
+ * hooks above reach its sealed block table (region 0), its tags (3) and its
+ * pending final states (5, 6, 7): tamper tests of the sealed block store. */
+gvs_handle *gvs_oram_test_handle(gvs_oram *o);
+
 /* The router's placement of one source's batch, computed on
  * the host by the device's own routing function: slot[i] = d * C + (rank of
  * request i among this batch's requests for shard d), or 0xFFFFFFFF when that
- * rank is >= C (the batch then overflows: GVS_ERR_BATCH_OVERFLOW).  Also
- * reports C and the shard pipeline size.  No device is touched; the CPU
+ * rank is >= C (the batch then overflows: GVS_ERR_BATCH_OVERFLOW).  shed[i]
+ * (may be NULL) = 1 when request i is past its routing key's cap (it then
+ * travels to shard i mod S as a hard error and is answered INTERNAL_ERROR).
+ * Also reports C and the shard pipeline size.  No device is touched; the CPU
  * multi-process tests use it to run the real placement over gloo. */
 int gvs_route_plan(const gvs_config *cfg, const gvs_request *reqs, uint32_t n, uint32_t *slot,
-                   uint32_t *capacity, uint32_t *shard_batch);
+                   uint32_t *capacity, uint32_t *shard_batch, uint8_t *shed);
 
 #ifdef __cplusplus
 }

@@ -96,6 +96,8 @@ def lib():
         L.gvo_id_decode_shard.restype = ctypes.c_int
         L.gvo_route.argtypes = [ctypes.c_char_p, vp, u32, u32, u64]
         L.gvo_route.restype = u32
+        L.gvo_route_key.argtypes = [ctypes.c_char_p, vp]
+        L.gvo_route_key.restype = u32
         L.gvo_route_capacity.argtypes = [u32, u32]
         L.gvo_route_capacity.restype = u32
         L.gvo_cluster_create.argtypes = [ctypes.POINTER(abi.GvsConfig)]
@@ -158,6 +160,33 @@ def route(config, reqs):
     return np.array([lib().gvo_route(key, reqs[i:i + 1].ctypes.data, i % B, config.shard_count,
                                      config.msg_capacity) for i in range(len(reqs))],
                     dtype=np.uint32)
+
+
+def route_key(config, reqs):
+    """Routing key of each request (gvo_route_key; low 2 bits 0 = unkeyed)."""
+    reqs = np.ascontiguousarray(reqs, dtype=abi.REQUEST_DTYPE)
+    key = bytes(config.secret_key)
+    return np.array([lib().gvo_route_key(key, reqs[i:i + 1].ctypes.data) for i in range(len(reqs))],
+                    dtype=np.uint32)
+
+
+ROUTE_KEY_CAP = 64  # gvo_oracle.h GVO_ROUTE_KEY_CAP
+
+
+def route_shed(config, reqs, B=None):
+    """The requests the router sheds (gvs_route.h, DESIGN.md §6 "Hot keys"):
+    in each source window of B (default: the config's max_batch), those past
+    the ROUTE_KEY_CAP-th of their routing key; unkeyed requests never."""
+    B = B or config.max_batch
+    key = route_key(config, reqs)
+    shed = np.zeros(len(reqs), dtype=bool)
+    for s0 in range(0, len(reqs), B):
+        seen = {}
+        for i in range(s0, min(len(reqs), s0 + B)):
+            k = int(key[i])
+            shed[i] = (k & 3) != 0 and seen.get(k, 0) >= ROUTE_KEY_CAP
+            seen[k] = seen.get(k, 0) + 1
+    return shed
 
 
 def route_capacity(batch, n_shards):

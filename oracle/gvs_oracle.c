@@ -726,6 +726,30 @@ uint32_t gvo_route(const uint8_t key[32], const gvs_request *rq, uint32_t i, uin
   return spread;
 }
 
+/* The routing key of a request (gvs_route.h route_dest_key): low 2 bits 1 =
+ * create (its recipient's mailbox), 2 = next-message op (the caller's
+ * mailbox), 3 = by-id op (its id), 0 = unkeyed (hard errors, zero
+ * recipients), which are never shed. */
+uint32_t gvo_route_key(const uint8_t key[32], const gvs_request *rq) {
+  const uint32_t t = rq->request_type;
+  const int id_zero = is_zero(rq->msg_id, 16);
+  if (is_hard_error(rq)) return 0;
+  const int next = (t == GVS_REQUEST_READ || t == GVS_REQUEST_DELETE) && id_zero;
+  uint64_t hi, lo;
+  if (t == GVS_REQUEST_CREATE) {
+    if (is_zero(rq->recipient, 32)) return 0;
+    gvo_recipient_hash(key + 16, rq->recipient, &hi, &lo);
+    return ((uint32_t)(lo >> 32) & ~3u) | 1u;
+  }
+  if (next) {
+    gvo_recipient_hash(key + 16, rq->auth_identity, &hi, &lo);
+    return ((uint32_t)(lo >> 32) & ~3u) | 2u;
+  }
+  uint32_t w[4];
+  memcpy(w, rq->msg_id, 16);
+  return ((w[0] ^ w[1] ^ w[2] ^ w[3]) & ~3u) | 3u;
+}
+
 uint32_t gvo_route_capacity(uint32_t batch, uint32_t n_shards) {
   if (n_shards <= 1) return batch;
   double mu = (double)((batch + n_shards - 1) / n_shards);
@@ -741,6 +765,8 @@ struct gvo_cluster {
   gvs_request *sub;
   gvs_response *subout;
   uint32_t *dest, *cnt;
+  uint8_t *shed;
+  uint64_t *keys;
 };
 
 /* Ops per shard pipeline for m routed slots plus expiry deletes: the smaller
@@ -768,7 +794,9 @@ gvo_cluster *gvo_cluster_create(const gvs_config *cfg) {
   c->subout = (gvs_response *)malloc((size_t)c->S * c->C * sizeof(gvs_response));
   c->dest = (uint32_t *)malloc((size_t)c->S * c->B * sizeof(uint32_t));
   c->cnt = (uint32_t *)malloc((size_t)c->S * c->S * sizeof(uint32_t));
-  if (!c->shard || !c->sub || !c->subout || !c->dest || !c->cnt) {
+  c->shed = (uint8_t *)malloc((size_t)c->S * c->B);
+  c->keys = (uint64_t *)malloc((size_t)c->B * sizeof(uint64_t));
+  if (!c->shard || !c->sub || !c->subout || !c->dest || !c->cnt || !c->shed || !c->keys) {
     gvo_cluster_destroy(c);
     return NULL;
   }
@@ -795,31 +823,62 @@ void gvo_cluster_destroy(gvo_cluster *c) {
   free(c->subout);
   free(c->dest);
   free(c->cnt);
+  free(c->shed);
+  free(c->keys);
   free(c);
 }
 
 uint32_t gvo_cluster_capacity(const gvo_cluster *c) { return c->C; }
 gvo_model *gvo_cluster_shard(gvo_cluster *c, uint32_t k) { return k < c->S ? c->shard[k] : NULL; }
 
-/* n <= S*B requests; source rank k submitted [k*B, (k+1)*B) */
+static int cmp_u64(const void *a, const void *b) {
+  const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+  return x < y ? -1 : x > y;
+}
+
+/* n <= S*B requests; source rank k submitted [k*B, (k+1)*B).
+ * Hot keys [D] (gvs_route.h): in each source's window, the requests of one
+ * routing key after its GVO_ROUTE_KEY_CAP-th are shed: they go to shard
+ * (index mod S) as hard errors (no state change) and are answered
+ * INTERNAL_ERROR with the request's time. */
 int gvo_cluster_process(gvo_cluster *c, const gvs_request *reqs, uint32_t n, gvs_response *out) {
   if (n > c->S * c->B) return GVS_ERR_INVALID_ARG;
   memset(c->cnt, 0, (size_t)c->S * c->S * sizeof(uint32_t));
+  memset(c->shed, 0, n);
+  for (uint32_t s0 = 0; s0 < n; s0 += c->B) {
+    const uint32_t m = n - s0 < c->B ? n - s0 : c->B;
+    for (uint32_t i = 0; i < m; ++i)
+      c->keys[i] = ((uint64_t)gvo_route_key(c->cfg.secret_key, &reqs[s0 + i]) << 32) | i;
+    qsort(c->keys, m, sizeof(uint64_t), cmp_u64);
+    for (uint32_t j = GVO_ROUTE_KEY_CAP; j < m; ++j) {
+      const uint32_t k = (uint32_t)(c->keys[j] >> 32);
+      if ((k & 3u) && (uint32_t)(c->keys[j - GVO_ROUTE_KEY_CAP] >> 32) == k)
+        c->shed[s0 + (uint32_t)c->keys[j]] = 1;
+    }
+  }
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t src = i / c->B, d = gvo_route(c->cfg.secret_key, &reqs[i], i % c->B, c->S,
                                            c->cfg.msg_capacity);
+    if (c->shed[i]) d = (i % c->B) % c->S;
     c->dest[i] = d;
     if (++c->cnt[src * c->S + d] > c->C) return GVS_ERR_BATCH_OVERFLOW; /* nothing applied */
   }
   for (uint32_t d = 0; d < c->S; ++d) {
     uint32_t m = 0;
     for (uint32_t i = 0; i < n; ++i)
-      if (c->dest[i] == d) c->sub[m++] = reqs[i];
+      if (c->dest[i] == d) {
+        c->sub[m] = reqs[i];
+        if (c->shed[i]) c->sub[m].request_type = 0; /* travels as a hard error */
+        ++m;
+      }
     int rc = gvo_process_batch(c->shard[d], c->sub, m, c->subout);
     if (rc) return rc;
     m = 0;
     for (uint32_t i = 0; i < n; ++i)
-      if (c->dest[i] == d) out[i] = c->subout[m++];
+      if (c->dest[i] == d) {
+        out[i] = c->subout[m++];
+        if (c->shed[i]) resp_fail(&out[i], GVS_STATUS_INTERNAL_ERROR, reqs[i].timestamp);
+      }
   }
   return GVS_OK;
 }

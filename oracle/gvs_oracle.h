@@ -87,6 +87,8 @@ void gvo_gen_batch(const gvo_model *m, const gvo_gen_params *p, uint64_t *rng,
 uint32_t gvo_route(const uint8_t key[32], const gvs_request *rq, uint32_t i, uint32_t n_shards,
                    uint64_t n_slots);
 uint32_t gvo_route_capacity(uint32_t batch, uint32_t n_shards);
+#define GVO_ROUTE_KEY_CAP 64u /* requests routed per routing key per source window */
+uint32_t gvo_route_key(const uint8_t key[32], const gvs_request *rq);
 typedef struct gvo_cluster gvo_cluster;
 gvo_cluster *gvo_cluster_create(const gvs_config *cfg); /* cfg->shard_count shards */
 void gvo_cluster_destroy(gvo_cluster *c);

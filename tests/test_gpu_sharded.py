@@ -61,22 +61,55 @@ def test_local_shards_drain_and_capacity():
 
 
 def test_local_shards_bucket_overflow_applies_nothing():
+    """One source sends more requests for one shard than C (many recipients,
+    none past its routing key's cap): the whole batch fails on every shard."""
     S = 4
     store, cl = sharded_pair(S, C=320)
     cl.seed(49)
     run_stream(store, cl, ffi.gen_params(n_identities=300), batches=2, n=S * 1024)
     before = store.dump_messages()
     msgs = store.stats()["messages"]
-    hot = cl.gen_batch(S * 1024, ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60,
-                                                n_identities=300))
-    assert cl.process_batch(hot) is None
+    batch = cl.gen_batch(S * 1024, ffi.gen_params(n_identities=300))
+    pool = cl.gen_batch(16 * 1024, ffi.gen_params(create=100, read=0, update=0, delete=0,
+                                                  n_identities=4000))
+    d0 = pool[ffi.route(cl.config, pool) == 0]
+    batch[:400] = d0[:400]  # source 0: 400 creates for shard 0 > C = 320
+    assert cl.process_batch(batch) is None
     with pytest.raises(GvsError) as ei:
-        store.process_batch(hot)
+        store.process_batch(batch)
     assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW
     assert store.stats()["messages"] == msgs
     assert store.dump_messages().tobytes() == before.tobytes()
     # the store keeps working after a rejected batch
     run_stream(store, cl, ffi.gen_params(n_identities=300), batches=2, n=S * 1024)
+
+
+@pytest.mark.parametrize("mix", ["hot_create", "hot_next", "hot_next_rud"])
+def test_local_shards_hot_recipient_is_shed(mix):
+    """A hot recipient (60-100 % of a source's window on one mailbox) no
+    longer overflows its bucket: the requests past the routing key's cap are
+    shed (spread to other shards as hard errors, answered INTERNAL_ERROR with
+    their time) and the batch is applied, bit for bit as the cluster model
+    says (DESIGN.md §6 "Hot keys")."""
+    S = 4
+    store, cl = sharded_pair(S)  # the default C: mean + 8 sigma + 64 covers the cap's 2 x 64
+    cl.seed(53)
+    run_stream(store, cl, ffi.gen_params(n_identities=300), batches=3, n=S * 1024)
+    p = {"hot_create": ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60, n_identities=300),
+         "hot_next": ffi.gen_params(create=30, read=35, update=0, delete=35, nxt=100, hot=100,
+                                    n_identities=300),
+         "hot_next_rud": ffi.gen_params(create=0, read=50, update=0, delete=50, nxt=100, hot=100,
+                                        n_identities=300)}[mix]
+    for b in range(3):
+        reqs = cl.gen_batch(S * 1024, p)
+        want = cl.process_batch(reqs)
+        assert want is not None
+        assert (want["status_code"] == abi.STATUS_CODE_INTERNAL_ERROR).sum() > S * 100
+        got = store.process_batch(reqs)
+        d = diff_responses(got, want, reqs)
+        assert not d, f"batch {b}: " + "\n".join(d)
+        assert store.stats()["messages"] == cl.messages
+    assert store.dump_messages().shape[0] > 0
 
 
 def test_rccl_single_rank_routed_path():

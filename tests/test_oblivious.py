@@ -44,10 +44,11 @@ ALL_MIXES = ["main", "rud", "all_create", "all_miss_read", "hot_next", "hot_next
 SHAPES = {
     "plain": dict(args=["--log2n", "20", "--batch", "65536"], mixes=ALL_MIXES),
     "auth": dict(args=["--log2n", "20", "--batch", "65536", "--auth"], mixes=ALL_MIXES),
-    # a hot recipient cannot go through a 2-shard router with the default
-    # bucket capacity (it would overflow by design)
+    # hot recipients go through the 2-shard router too: the requests past
+    # their routing key's cap are shed (DESIGN.md §6 "Hot keys")
     "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2"],
-                   mixes=["main", "rud", "all_create", "all_miss_read", "deletes"]),
+                   mixes=["main", "rud", "all_create", "all_miss_read", "hot_next", "hot_next_rud",
+                          "deletes"]),
     # the wire path: launches and grids must not depend on forged signatures
     # or malformed messages either; the byte counters of the front-end
     # kernels are compared over requests that verify and decode (canonical or

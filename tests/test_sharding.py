@@ -108,17 +108,25 @@ def test_single_shard_cluster_equals_plain_model():
     assert cl.messages == m.messages and cl.mailboxes == m.mailboxes
 
 
+def shed_mask(cfg, reqs, B):
+    return ffi.route_shed(cfg, reqs, B)
+
+
 @pytest.mark.parametrize("S", [2, 4, 8])
 def test_sharding_preserves_unsharded_semantics(S):
     """Same logical request stream into an unsharded model and an S-shard
     cluster (ample capacity everywhere): identical statuses and identical
-    records except for the message ids, which name their shard."""
+    records except for the message ids, which name their shard.  Requests the
+    router sheds (a source's ops past their routing key's cap; early batches
+    hit few ids many times) go to the unsharded model as hard errors and come
+    back from the cluster as INTERNAL_ERROR with their time."""
     rng = np.random.default_rng(100 + S)
     B = 1024
     single = ffi.Model(abi.make_config(1 << 16, mailbox_partitions=64, mailbox_partition_slots=64,
                                        max_batch=S * B))
     cl = ffi.Cluster(cluster_cfg(S, N=1 << 15, B=B, Q=32, Sr=64, C=B))
     ids_single, ids_cluster, owners = [], [], []
+    n_shed = 0
     pool = [ffi.identity(i) for i in range(120)]
     for batch in range(8):
         n = S * B
@@ -147,9 +155,16 @@ def test_sharding_preserves_unsharded_semantics(S):
         for i in np.nonzero(refs >= 0)[0]:
             r_single[i]["msg_id"] = np.frombuffer(ids_single[refs[i]], np.uint8)
             r_cluster[i]["msg_id"] = np.frombuffer(ids_cluster[refs[i]], np.uint8)
+        shed = shed_mask(cl.config, r_cluster, B)
+        n_shed += int(shed.sum())
+        r_single["request_type"][shed] = 0
         o1 = single.process_batch(r_single)
         o2 = cl.process_batch(r_cluster)
         assert o2 is not None
+        assert (o2["status_code"][shed] == abi.STATUS_CODE_INTERNAL_ERROR).all(), batch
+        assert (o2["record"]["timestamp"][shed] == r_cluster["timestamp"][shed]).all(), batch
+        o1["status_code"][shed] = abi.STATUS_CODE_INTERNAL_ERROR
+        o1["record"]["timestamp"][shed] = r_cluster["timestamp"][shed]
         assert np.array_equal(o1["status_code"], o2["status_code"]), batch
         for f in ("sender", "recipient", "timestamp", "payload"):
             assert np.array_equal(o1["record"][f], o2["record"][f]), (batch, f)
@@ -159,17 +174,54 @@ def test_sharding_preserves_unsharded_semantics(S):
             owners.append((bytes(reqs[i]["auth_identity"]), bytes(reqs[i]["recipient"])))
     assert single.messages == cl.messages > 0
     assert single.mailboxes == cl.mailboxes
+    assert n_shed > 0  # the cap was exercised
 
 
 def test_bucket_overflow_rejects_whole_batch():
+    """A source whose requests for one shard exceed C (many recipients, none
+    past its cap) fails the whole batch: nothing is applied anywhere."""
     S = 4
-    cl = ffi.Cluster(cluster_cfg(S, C=320))
+    cfg = cluster_cfg(S, C=320)
+    cl = ffi.Cluster(cfg)
     cl.seed(21)
     p = ffi.gen_params(n_identities=300)
     assert cl.process_batch(cl.gen_batch(S * 1024, p)) is not None
     before = [cl.shard(k).digest() for k in range(S)]
     msgs = cl.messages
+    batch = cl.gen_batch(S * 1024, p)
+    pool = cl.gen_batch(16 * 1024, ffi.gen_params(create=100, read=0, update=0, delete=0,
+                                                  n_identities=4000))
+    d0 = pool[ffi.route(cfg, pool) == 0]
+    assert len(d0) >= 400
+    batch[:400] = d0[:400]  # source 0: 400 creates for shard 0 > C = 320
+    assert not shed_mask(cfg, batch, 1024)[:400].any()
+    assert cl.process_batch(batch) is None
+    assert [cl.shard(k).digest() for k in range(S)] == before and cl.messages == msgs
+
+
+def test_hot_recipient_is_shed_not_rejected():
+    """A source that sends 60 % of its window to one recipient no longer fails
+    the batch for everyone (README.md:78-84; DESIGN.md §6 "Hot keys"): its
+    first ROUTE_KEY_CAP creates for that recipient are routed, the rest are
+    answered INTERNAL_ERROR with their time, and every other request is
+    answered as the unsharded store answers it (with the shed ones turned into
+    hard errors)."""
+    S = 4
+    cfg = cluster_cfg(S, C=320)
+    cl = ffi.Cluster(cfg)
+    cl.seed(21)
+    p = ffi.gen_params(n_identities=300)
+    assert cl.process_batch(cl.gen_batch(S * 1024, p)) is not None
     hot = cl.gen_batch(S * 1024, ffi.gen_params(create=100, read=0, update=0, delete=0, hot=60,
                                                 n_identities=300))
-    assert cl.process_batch(hot) is None  # one recipient takes > C of a source's slots
-    assert [cl.shard(k).digest() for k in range(S)] == before and cl.messages == msgs
+    shed = shed_mask(cfg, hot, 1024)
+    assert shed.sum() > S * 400
+    msgs = cl.messages
+    out = cl.process_batch(hot)
+    assert out is not None
+    assert (out["status_code"][shed] == abi.STATUS_CODE_INTERNAL_ERROR).all()
+    assert (out["record"]["timestamp"][shed] == hot["timestamp"][shed]).all()
+    assert not out["record"]["payload"][shed].any() and not out["record"]["sender"][shed].any()
+    ok = out["status_code"] == 1
+    assert ok[~shed].sum() > 0 and not ok[shed].any()
+    assert cl.messages == msgs + int(ok.sum())
