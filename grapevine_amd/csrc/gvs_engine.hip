@@ -1160,7 +1160,8 @@ static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d
     const uint64_t off = (uint64_t)k * h->Bsub;
     const uint32_t nk = n > off ? (uint32_t)std::min<uint64_t>(n - off, h->Bsub) : 0u;
     if (nk)
-      hipLaunchKernelGGL(k_route_gather, dim3((nk + 3) / 4), dim3(256), 0, h->stream,
+      hipLaunchKernelGGL(k_route_gather, dim3((nk + 4 * kGatherPerWave - 1) / (4 * kGatherPerWave)),
+                         dim3(256), 0, h->stream,
                          (const uint32_t*)h->rt[k].pos, (const uint32_t*)h->rt[k].shed,
                          d_in + off * kAbiU4, (const uint4*)h->rt[k].back, nk, d_out + off * kAbiU4);
   }

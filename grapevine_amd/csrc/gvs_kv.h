@@ -51,6 +51,7 @@ __global__ __launch_bounds__(256) void k_bcopy(BcopyArgs a) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) rec[c] = make_uint4(0, 0, 0, 0);
   uint32_t my_kind = 0;
+  uint64_t my_key = 0;
   for (uint32_t j = 0; j < 64; ++j) {
     const uint32_t i = i0 + j;
     const bool real = i < a.n;
@@ -65,9 +66,10 @@ __global__ __launch_bounds__(256) void k_bcopy(BcopyArgs a) {
     // on the dividend's high word
     const uint32_t ix = (real && !bad) ? (uint32_t)index : 0u;
     const uint64_t row = (real && !bad) ? (uint64_t)(ix % a.W) * a.S + ix / a.W : kRNullRow;
-    if (lane == 0) a.rkeys[i] = r_key(row, 0u, i);
+    my_key = lane == j ? r_key(row, 0u, i) : my_key;
     my_kind = lane == j ? h.z : my_kind;
   }
+  a.rkeys[i0 + lane] = my_key;  // the wave's 64 keys in one store: whole lines
   rec[0] = make_uint4(my_kind, 1u, 0u, 0u);
   wave_store128(stage + wave * 64 * 8, a.meta, i0 + lane, rec);
 }

@@ -718,12 +718,16 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       }
       wave_seal<kMU>(a.sc, s_te, 1u, r0, ep, v, a.btag, true, st);
     }
+    if (!AUTH) {  // the chunk's side entries: one store, kMU lanes (one whole line at kMU = 8;
+                  // eight 16-B stores of one line from one lane left partial lines behind)
+      uint4 mine = sd[0];
+#pragma unroll
+      for (int u = 1; u < kMU; ++u) mine = sel4(lane == (uint32_t)u, sd[u], mine);
+      if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
+    }
 #pragma unroll
     for (int u = 0; u < kMU; ++u) {
-      if (j0 + u < a.Sr) {
-        st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
-        if (!AUTH && lane == 0) side[j0 + u] = sd[u];
-      }
+      if (j0 + u < a.Sr) st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
       va[u] = vb[u];
     }
   }

@@ -201,25 +201,43 @@ __global__ __launch_bounds__(256) void k_route_fill(RouteArgs a) {
   if (lane < 8) dst[64 + lane] = z;
 }
 
-// one wave per request: its response (slot layout) back to the caller layout;
-// a shed request's response is INTERNAL_ERROR with the request's time (the
-// hard-error response its shard sent back is read and replaced, so every
-// request reads the same lines)
+// the responses (slot layout) back to the caller layout, kGatherPerWave
+// requests per wave: 8 rows of 1040 B are 65 whole lines, so every output line
+// is written by one wave (one wave per request left the line two requests
+// share to two waves, whose partial write-backs moved WRITE_SIZE with the
+// timing).  A shed request's response is INTERNAL_ERROR with the request's
+// time: its shard's hard-error response and its request's time word are read
+// for every request and selected, so every request reads the same lines.
+constexpr uint32_t kGatherPerWave = 8;
 __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict__ pos,
                                                       const uint32_t* __restrict__ shed,
                                                       const uint4* __restrict__ in,
                                                       const uint4* __restrict__ back, uint32_t n,
                                                       uint4* __restrict__ out) {
-  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
-  if (i >= n) return;
-  const uint32_t p = pos[i];
-  if (p == kNone) return;  // overflowed batch: the call fails, out is undefined
-  const uint4* src = back + (uint64_t)p * kSlotU4;
-  const uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
-  const bool sh = shed[i] != 0u;
-  const uint4 fail = lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0);
-  out[(uint64_t)i * kAbiU4 + lane] = sh ? fail : src[lane];
-  if (lane == 0) out[(uint64_t)i * kAbiU4 + 64] = sh ? make_uint4(8u, 0, 0, 0) : src[64];
+  constexpr uint32_t R = kGatherPerWave;
+  const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R, lane = lane_id();
+  if (i0 >= n) return;
+  uint4 v[R], tw[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {  // wave-uniform conditions
+    const uint32_t i = min(i0 + r, n - 1u);
+    const uint32_t p = pos[i];
+    // an overflowed batch (p == kNone) fails as a whole; out is then undefined
+    v[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + lane] : make_uint4(0, 0, 0, 0);
+    tw[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + 64] : make_uint4(0, 0, 0, 0);
+    const uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
+    const bool s = shed[i] != 0u;
+    v[r] = s ? (lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0)) : v[r];
+    tw[r] = s ? make_uint4(8u, 0, 0, 0) : tw[r];
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r)
+    if (i0 + r < n) out[(uint64_t)(i0 + r) * kAbiU4 + lane] = v[r];
+  // the status words: lane r writes request r's
+  uint4 t = tw[0];
+#pragma unroll
+  for (uint32_t r = 1; r < R; ++r) t = lane == r ? tw[r] : t;
+  if (lane < R && i0 + lane < n) out[(uint64_t)(i0 + lane) * kAbiU4 + 64] = t;
 }
 
 // single-process shards: OR of every shard's error word into each of them
