@@ -107,13 +107,18 @@ struct alignas(16) Key128 {
   uint64_t hi, lo;
 };
 
-struct Scal {  // persistent device scalars + per-batch temporaries
+struct alignas(128) Scal {  // persistent device scalars + per-batch temporaries
+  // The error word has a line of its own: every workgroup of every kernel
+  // reads it first (a scalar load), and the counters below are written by
+  // atomics and single threads during the batch, so sharing their line made
+  // the scalar reads' L2 hits depend on what else touched it.
+  uint32_t error, pad0[31];
   uint64_t count, ctr, head, tail, n_mailboxes, batches;
-  uint32_t error, pad0;
   // per batch
   uint64_t pops, scnt, m, count1, head0, tail0, nd;
-  uint64_t pad1[4];
+  uint64_t pad1[3];
 };
+static_assert(sizeof(Scal) == 256, "Scal: two lines");
 
 struct KeyCtx {
   uint64_t pk0, pk1, hk0, hk1;
