@@ -96,14 +96,24 @@ struct KvHdr {
   uint64_t prow;
 };
 
-__device__ inline KvHdr kv_hdr(const KvArgs& a, uint32_t p) {
-  const uint4 rp = uni4(a.rpos[p]);
+// A position's record (8 uint4, read once per kernel through LDS: a line read
+// twice hits or misses L2 depending on the traffic in between, whose
+// addresses depend on the data): word 0 its RPOS entry, word 1 its op's meta
+// word, 2..7 the rest of the meta line (the whole line is read).
+__device__ inline uint4 kv_rec_line(const KvArgs& a, uint64_t i) {
+  const uint32_t k = (uint32_t)i & 7u;
+  const uint4 rp = a.rpos[i >> 3];
+  const uint4 m = a.meta[(uint64_t)(rp.x & kSeqMask) * 8 + ((k + 7u) & 7u)];
+  return k == 0u ? rp : m;
+}
+
+__device__ inline KvHdr kv_hdr_rec(const KvArgs& a, const uint4* r) {
+  const uint4 rp = uni4(r[0]), m = uni4(r[1]);
   KvHdr h;
   h.seq = rp.x & kSeqMask;
   h.flags = rp.x;
   h.slot = rp.y;
   h.prow = (rp.x & kPosNull) ? 0ull : (uint64_t)rp.z * a.S + rp.w;
-  const uint4 m = uni4(shfl4(line_load(a.meta + (uint64_t)h.seq * 8), 0));
   h.kind = m.x;
   h.e0 = m.y;
   h.ovf = m.z;
@@ -114,7 +124,8 @@ __device__ inline KvHdr kv_hdr(const KvArgs& a, uint32_t p) {
 struct KvOp {
   using Args = KvArgs;
   static constexpr bool kSelect = true;
-  static constexpr bool kStash = false;
+  static constexpr bool kStash = true;  // each position's record read once (kv_rec_line)
+  __device__ static uint4 rec_line(const Args& a, uint64_t i) { return kv_rec_line(a, i); }
   __device__ static uint4 f_identity() { return make_uint4(kTId, 0, 0, 0); }
   // a then b: function composition of the transforms
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
@@ -146,7 +157,16 @@ struct KvOp {
     const bool head = h.flags & kPosHead, null = h.flags & kPosNull;
     return sel4(null, make_uint4(kTConst, 0, 0, 0), sel4(head, hd, o));
   }
-  __device__ static uint4 f_of(const Args& a, uint32_t p) { return f_of_hdr(kv_hdr(a, p)); }
+  // (the stash scan takes f from the record; S is in the args, not the record)
+  __device__ static uint4 f_of_rec(const uint4* r) {
+    const uint4 rp = uni4(r[0]), m = uni4(r[1]);
+    KvHdr h{};
+    h.flags = rp.x;
+    h.kind = m.x;
+    h.e0 = m.y;
+    h.ovf = m.z;
+    return f_of_hdr(h);
+  }
   // value of position p's element: the op's image when its own transform
   // supplies the value (WRITE; INSERT into an absent row), else the snapshot
   // (a head whose own transform keeps the row), zero for REMOVE / null
@@ -157,8 +177,8 @@ struct KvOp {
   }
   // k_vscan_a: every op's two rows (its SNAPP line and its image) are read,
   // the defining op's value kept: addresses that do not depend on the ops
-  __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4*) {
-    const KvHdr h = kv_hdr(a, p);
+  __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4* r) {
+    const KvHdr h = kv_hdr_rec(a, r);
     const bool head = h.flags & kPosHead;
     const uint4 sv = ld_row<false>(&a.snapp[(uint64_t)p * 64 + lane_id()]);
     const uint4 iv = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane_id()]);
@@ -177,13 +197,18 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
   if (a.scal->error) return;
   __shared__ uint4 s_v[4][64];
   __shared__ uint4 s_f[4];
+  __shared__ uint4 s_rec[4][16 * 8];  // each wave's 16 position records
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  uint4* rec = s_rec[wave];
+  rec[lane] = kv_rec_line(a, (uint64_t)p0 * 8 + lane);
+  rec[64 + lane] = kv_rec_line(a, (uint64_t)p0 * 8 + 64 + lane);
+  wave_lds_sync();
   // each op's own SNAPP line (heads: the row's snapshot) and its image, read once
   uint4 svs[16], ivs[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    const KvHdr h = kv_hdr(a, p0 + j);
+    const KvHdr h = kv_hdr_rec(a, rec + j * 8);
     svs[j] = ld_row<false>(&a.snapp[(uint64_t)(p0 + j) * 64 + lane]);
     ivs[j] = ld_row<false>(&a.img[(uint64_t)h.seq * 64 + lane]);
   }
@@ -192,7 +217,7 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
     uint4 f = KvOp::f_identity(), v = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
-      const KvHdr h = kv_hdr(a, p0 + j);
+      const KvHdr h = kv_hdr_rec(a, rec + j * 8);
       const uint4 e = KvOp::f_of_hdr(h);
       const bool head = h.flags & kPosHead;
       const uint4 o = KvOp::own_f(h);
@@ -208,7 +233,7 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
-    const KvHdr h = kv_hdr(a, p);
+    const KvHdr h = kv_hdr_rec(a, rec + j * 8);
     const bool head = h.flags & kPosHead, null = h.flags & kPosNull, last = h.flags & kPosLast;
     const uint4 sv = svs[j], iv = ivs[j];
     // the state before the op

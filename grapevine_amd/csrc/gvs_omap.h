@@ -263,37 +263,63 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   __shared__ uint16_t s_npfx[kSlotMax + 1];
   __shared__ int16_t s_pend[kSlotMax + 1];
   __shared__ uint32_t s_w[4], s_ng;
-  const uint32_t tid = threadIdx.x, w = blockIdx.x;
+  const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = lane_id(), wave = tid >> 6;
   if (a.scal->error) return;
   if (tid == 0) s_ng = 0;
   __syncthreads();
-  for (uint32_t k = tid; k < a.c; k += 256) {
-    const uint4* r = a.ogt + ((uint64_t)w * a.c + k) * 8;
-    const uint4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-    GroupO G;
-    G.hi = u4lo(r2);
-    G.lo = u4hi(r2) & kOHashMask;
-    G.key[0] = r1.x;
-    G.key[1] = r1.y;
-    G.key[2] = r1.z;
-    G.key[3] = r1.w;
-    G.fk = r0.y;
-    G.fe = r0.z;
-    G.cr = r0.w;
-    G.real = r0.x == a.stamp ? 1u : 0u;
-    G.row = -1;
-    G.e0 = 0;
-    G.head = r3.x;
-    G.pad = 0;
-    g[k] = G;
-    atomicAdd(&s_ng, G.real);
+  // Global reads cover whole 128-B lines in one instruction (a line read in
+  // parts by several instructions is fetched whole or in halves depending on
+  // timing): a group record by 8 lanes, words 1..3 shuffled to its first lane.
+  for (uint32_t k0 = wave * 8; k0 < a.c; k0 += 32) {  // c only
+    const uint32_t k = k0 + (lane >> 3);
+    const uint4 x = a.ogt[((uint64_t)w * a.c + min(k, a.c - 1u)) * 8 + (lane & 7u)];
+    const int l0 = (int)(lane & ~7u);
+    const uint4 r0 = x, r1 = shfl4(x, l0 + 1), r2 = shfl4(x, l0 + 2), r3 = shfl4(x, l0 + 3);
+    if ((lane & 7u) == 0u && k < a.c) {
+      GroupO G;
+      G.hi = u4lo(r2);
+      G.lo = u4hi(r2) & kOHashMask;
+      G.key[0] = r1.x;
+      G.key[1] = r1.y;
+      G.key[2] = r1.z;
+      G.key[3] = r1.w;
+      G.fk = r0.y;
+      G.fe = r0.z;
+      G.cr = r0.w;
+      G.real = r0.x == a.stamp ? 1u : 0u;
+      G.row = -1;
+      G.e0 = 0;
+      G.head = r3.x;
+      G.pad = 0;
+      g[k] = G;
+      atomicAdd(&s_ng, G.real);
+    }
   }
   __syncthreads();
   const uint32_t ng = s_ng;
   uint4* kd = a.kdir + (uint64_t)w * a.S * 2;
-  // match every row's key
-  for (uint32_t j = tid; j < a.S; j += 256) {
-    const uint4 key = kd[j * 2], h = kd[j * 2 + 1];
+  // match every row's key.  The directory entries are read once and kept in
+  // registers for the rewrite (a line read twice hits or misses L2 depending
+  // on the traffic in between: FETCH_SIZE would depend on the keys)
+  // Each wave reads its 64 entries (2 KiB) as two whole-line loads, entry
+  // j = tid + 256 it to lane tid % 64 by shuffles (S >= 256, a power of two).
+  constexpr uint32_t kIt = kRowsMax / 256;
+  uint4 dkey[kIt], dh[kIt];
+  const int se = (int)((2u * lane) & 63u);
+#pragma unroll
+  for (uint32_t it = 0; it < kIt; ++it) {
+    const uint32_t j0 = it * 256 + wave * 64;
+    if (j0 >= a.S) break;  // S only
+    const uint4 lo = kd[(uint64_t)j0 * 2 + lane], hi = kd[(uint64_t)j0 * 2 + 64 + lane];
+    const uint4 klo = shfl4(lo, se), khi = shfl4(hi, se), hlo = shfl4(lo, se + 1), hhi = shfl4(hi, se + 1);
+    dkey[it] = sel4(lane < 32u, klo, khi);
+    dh[it] = sel4(lane < 32u, hlo, hhi);
+  }
+#pragma unroll
+  for (uint32_t it = 0; it < kIt; ++it) {
+    const uint32_t j = tid + it * 256;
+    if (j >= a.S) break;
+    const uint4 key = dkey[it], h = dh[it];
     const bool used = nz4(key);
     const int k = find_group_o(g, ng, a.c, u4lo(h), u4hi(h) & kOHashMask);
     const GroupO& G = g[k >= 0 ? k : 0];
@@ -330,18 +356,25 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   // the directory after the batch: a group's key stays or arrives where its
   // final state exists (transform applied to e0; an overflowed group never
   // exists)
-  for (uint32_t j = tid; j < a.S; j += 256) {
+#pragma unroll
+  for (uint32_t it = 0; it < kIt; ++it) {
+    const uint32_t j = tid + it * 256;
+    if (j >= a.S) break;
     const int16_t m = s_m[j];
     const uint32_t k = (uint32_t)(m & 0x3fff);
     const GroupO& G = g[m >= 0 ? k : 0u];
     const uint32_t efin = G.fk == kTId ? G.e0 : (G.fk == kTConst ? G.fe : 1u);
-    uint4 key = kd[j * 2], h = kd[j * 2 + 1];
+    uint4 key = dkey[it], h = dh[it];
     const uint4 gk = make_uint4(G.key[0], G.key[1], G.key[2], G.key[3]);
     const uint4 gh = make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)G.lo, (uint32_t)(G.lo >> 32));
     key = sel4(m >= 0, sel4(efin != 0u, gk, make_uint4(0, 0, 0, 0)), key);
     h = sel4(m >= 0, sel4(efin != 0u, gh, make_uint4(0, 0, 0, 0)), h);
-    kd[j * 2] = key;
-    kd[j * 2 + 1] = h;
+    // back as two whole-line stores: word 2e + b of a half is entry e's key (b = 0) or hash
+    const int e = (int)(lane >> 1);
+    const uint4 klo = shfl4(key, e), khi = shfl4(key, 32 + e), hlo = shfl4(h, e), hhi = shfl4(h, 32 + e);
+    const uint64_t j0 = (uint64_t)j - lane;
+    kd[j0 * 2 + lane] = sel4(lane & 1u, hlo, klo);
+    kd[j0 * 2 + 64 + lane] = sel4(lane & 1u, hhi, khi);
   }
   // each group's result to its head position (slots without a group: dummies)
   for (uint32_t k = tid; k < a.c; k += 256) {

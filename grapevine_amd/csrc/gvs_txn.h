@@ -547,6 +547,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
     }
+    // The waves meet after every tile, expiry or not: without the barrier they
+    // drift apart and the plain pass runs 4-5% slower.  A barrier after every
+    // chunk as well gains another 2%, but moves the pass's WRITE_SIZE with the
+    // request mix by 90-135 KiB (profiles/r03n_pass_ab.txt): not taken.
     if (lane == 0) s_xc[wave] = xc;
     __syncthreads();
     if (a.xon) {

@@ -12,6 +12,9 @@ state and checks the responses.
 one device, the router kernels k_route_* and the padded all-to-all), against
 the oracle's cluster model.
 
+--oram / --omap run the block store or the key-value map instead, with the
+op mixes of KV_MIXES (2^log2n blocks or rows, --batch ops per batch).
+
 --wire runs every batch (prefill included) through gvs_process_wire_batch:
 protobuf requests in 1200-B slots, decoded, their schnorrkel signatures
 checked against per-request challenges, the store, responses encoded.  The
@@ -43,6 +46,79 @@ MIXES = {
     "wire_noncanonical": dict(create=25, read=25, update=25, delete=25, nxt=50),
 }
 WIRE_STRIDE = 1200
+
+# --oram / --omap (the block store and the key-value map):
+# op mixes as (pool, op probabilities); pool "uniform" = every block / the
+# prefilled keys, "hot" = 64 of them, "one" = a single block, "fresh" = keys
+# never inserted
+KV_MIXES = {
+    "oram": {
+        "main": ("uniform", 0.5), "all_read": ("uniform", 0.0), "all_write": ("uniform", 1.0),
+        "hot": ("hot", 0.5), "chain": ("one", 0.5),
+    },
+    "omap": {
+        "main": ("uniform", (0.3, 0.3, 0.25, 0.15)), "all_read": ("uniform", (1, 0, 0, 0)),
+        "all_insert": ("fresh", (0, 0, 1, 0)), "all_remove": ("uniform", (0, 0, 0, 1)),
+        "hot": ("hot", (0.3, 0.3, 0.25, 0.15)), "miss": ("fresh", (1, 0, 0, 0)),
+    },
+}
+KV_SECRET = bytes((0x51 + 11 * i) & 0xFF for i in range(32))
+
+
+def run_kv(a, kind):
+    """The block store or the key-value map: a prefill identical in every
+    process, then --batches batches per seed of the chosen mix, each checked
+    bit-exact against the sequential oracle (oracle/gvs_kv.c)."""
+    import numpy as np
+    from grapevine_amd.store import BlockStore, KeyValueMap
+    assert a.mix in KV_MIXES[kind], f"{kind} mixes: {sorted(KV_MIXES[kind])}"
+    cap, B = 1 << a.log2n, a.batch
+    cfg = abi.make_oram_config(cap, max_batch=B, secret_key=KV_SECRET)
+    if kind == "oram":
+        store, model = BlockStore(cfg), ffi.OramModel(cap)
+    else:
+        store, model = KeyValueMap(cfg), ffi.OmapModel(cap, KV_SECRET)
+    keys = np.random.default_rng(5).integers(0, 256, (cap // 8, 16), dtype=np.uint8)
+    keys[:, 0] |= 1  # no all-zero key
+
+    def ops_of(rng, pool, p):
+        if kind == "oram":
+            ops = np.zeros(B, dtype=abi.BLOCK_OP_DTYPE)
+            blocks = {"uniform": np.arange(cap), "hot": np.arange(64) * 4099 % cap,
+                      "one": np.array([77])}[pool]
+            ops["index"] = rng.choice(blocks, B)
+            ops["op"] = (rng.random(B) < p).astype(np.uint32)
+            ops["data"] = rng.integers(0, 256, (B, 1024), dtype=np.uint8)
+            return ops
+        ops = np.zeros(B, dtype=abi.OMAP_OP_DTYPE)
+        if pool == "fresh":
+            k = rng.integers(0, 256, (B, 16), dtype=np.uint8)
+            k[:, 0] |= 1
+        else:
+            k = (keys if pool == "uniform" else keys[:64])[rng.integers(0, len(keys) if pool == "uniform"
+                                                                        else 64, B)]
+        ops["key"] = k
+        ops["op"] = rng.choice(4, B, p=p)
+        ops["value"] = rng.integers(0, 256, (B, 1024), dtype=np.uint8)
+        return ops
+
+    def check(ops, what):
+        got, want = store.access(ops), model.access(ops)
+        if not a.no_check:
+            assert got.tobytes() == want.tobytes(), f"parity failure inside the probe ({what})"
+
+    rng = np.random.default_rng(77)
+    for _ in range(a.fill_batches):  # writes / inserts of the key pool
+        check(ops_of(rng, "uniform", 1.0 if kind == "oram" else (0, 0, 1, 0)), "prefill")
+    pool, p = KV_MIXES[kind][a.mix]
+    seeds = [int(x) for x in a.seeds.split(",") if x] or [a.seed]
+    for sd in seeds:
+        rng = np.random.default_rng(sd)
+        for _ in range(a.batches):
+            check(ops_of(rng, pool, p), a.mix)
+    store.close()
+    model.close()
+    print("probe ok", kind, a.mix)
 
 
 class WirePath:
@@ -120,7 +196,7 @@ class WirePath:
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("mix", choices=sorted(MIXES))
+    p.add_argument("mix", choices=sorted(set(MIXES) | set(KV_MIXES["oram"]) | set(KV_MIXES["omap"])))
     p.add_argument("--log2n", type=int, default=20)
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--batches", type=int, default=3)
@@ -135,7 +211,11 @@ def main():
                         "generator reseeded before each seed's batches (seed-controlled runs)")
     p.add_argument("--no-check", action="store_true",
                    help="skip the parity asserts of the measured batches (GVS_DIAG variants)")
+    p.add_argument("--oram", action="store_true", help="the block store (gvs_oram_*)")
+    p.add_argument("--omap", action="store_true", help="the key-value map (gvs_omap_*)")
     a = p.parse_args()
+    if a.oram or a.omap:
+        return run_kv(a, "oram" if a.oram else "omap")
     assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
     S = a.shards if a.shards > 1 else 0
     cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth, shard_count=S)
