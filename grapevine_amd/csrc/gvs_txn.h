@@ -488,9 +488,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
     }
     for (uint32_t j = 0; j < 64; j += U) {
       uint4 v[U];
+      const uint32_t rj = rb + j;
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rb + j + u) * 64 + lane]);
-      const uint64_t r0 = rowbase + rb + j;  // physical row of v[0]
+      for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rj + u) * 64 + lane]);
+      const uint64_t r0 = rowbase + rj;  // physical row of v[0]
       const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
       const bool first = t == 0 && j == 0 && wave == 0;
       if constexpr (FUSED) {
@@ -516,7 +517,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
             if (have_prev && (lane & 3u) == 0u && lane < 32u)
               a.mtag[prev_r0 + ur] = make_uint4((uint32_t)tg[0], (uint32_t)(tg[0] >> 32), (uint32_t)tg[1],
                                                 (uint32_t)(tg[1] >> 32));
-            xc = rpass_chunk_merge<U, AUTH>(a, v, rb + j, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+            xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
                                             s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
           } else {
             const uint4 want = a.mtag[r0 + ur];
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
           if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
             atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
         }
-        xc = rpass_chunk_merge<U, AUTH>(a, v, rb + j, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+        xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
                                         s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
         if (AUTH) {
           const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rb + j + u) * 64 + lane], v[u]);
+      for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
     }
     // The waves meet after every tile, expiry or not: without the barrier they
     // drift apart and the plain pass runs 4-5% slower.  A barrier after every

@@ -20,3 +20,21 @@ def pytest_configure(config):
 def oracle_lib():
     from oracle import ffi
     return ffi.lib()
+
+
+@pytest.hookimpl(trylast=True)  # after -m deselection
+def pytest_collection_modifyitems(config, items):
+    """GPU sessions start torch's HIP runtime before libgvstore's.  torch
+    bundles its own libamdhip64; when the engine's runtime (/opt/rocm) has
+    opened the device first, torch's finds no device ("No HIP GPUs are
+    available") and the tests that hand the engine torch tensors fail, while
+    the other order works.  CPU sessions do not import torch here."""
+    if not any(it.get_closest_marker("gpu") for it in items):
+        return
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.zeros(1, device="cuda")
+        torch.cuda.synchronize()
