@@ -54,7 +54,7 @@ def parse():
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=8, choices=(4, 8),
                    help="--auth: waves per workgroup of the sealed message pass")
-    p.add_argument("--sealed-fused", type=int, default=1, choices=(0, 1),
+    p.add_argument("--sealed-fused", type=int, default=0, choices=(0, 1),
                    help="--auth: AES and BLAKE2b interleaved in the sealed message pass (1) or phased (0)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "

@@ -235,7 +235,8 @@ struct gvs_handle {
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   int sealed_nw = 8;         // waves per workgroup of the sealed message pass (4 or 8; option)
-  int sealed_fused = 1;      // sealed message pass with AES and BLAKE2b interleaved (option)
+  int sealed_fused = 0;      // sealed message pass with AES and BLAKE2b interleaved (option; it
+                             // spills 33 VGPRs to scratch and is no faster: off by default)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;

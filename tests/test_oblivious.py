@@ -4,7 +4,7 @@ launch sequence, the grid/workgroup sizes and the HBM byte counters
 (rocprofv3 FETCH_SIZE, WRITE_SIZE) must not depend on the request mix.
 
 Shapes: 64K-request batches (the C3 batch, so the multi-tile sorts and every
-global merge step run) over a 2^20-message store, plain and authenticated
+global merge step run) over a 2^20-message store (2^21 authenticated), plain and authenticated
 (DESIGN.md §8); the routed path (2 shards in one process: k_route_* and the
 padded all-to-all); the block store and the key-value map (DESIGN.md §10);
 the wire path (decode, schnorrkel check, store, encode).
@@ -44,7 +44,9 @@ PROBE = os.path.join(ROOT, "tools", "oblivious_probe.py")
 ALL_MIXES = ["main", "rud", "all_create", "all_miss_read", "hot_next", "hot_next_rud", "deletes"]
 SHAPES = {
     "plain": dict(args=["--log2n", "20", "--batch", "65536"], mixes=ALL_MIXES),
-    "auth": dict(args=["--log2n", "20", "--batch", "65536", "--auth"], mixes=ALL_MIXES),
+    # 2^21 messages: 512-row partitions, so the sealed pass runs its production
+    # shape (8 waves per workgroup, gvs_engine.hip launch_rpass2) as at C3 / C5
+    "auth": dict(args=["--log2n", "21", "--batch", "65536", "--auth"], mixes=ALL_MIXES),
     # hot recipients go through the 2-shard router too: the requests past
     # their routing key's cap are shed (DESIGN.md §6 "Hot keys")
     "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2"],
