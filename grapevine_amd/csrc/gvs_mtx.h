@@ -190,28 +190,36 @@ __device__ inline uint32_t load_groups(const MArgs& a, uint32_t q, GroupM* g, ui
                                        bool with_results) {
   if (threadIdx.x == 0) *s_ng = 0;
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < a.cm; k += 256) {
-    const uint4* r = a.gtx + ((uint64_t)q * a.cm + k) * 8;
-    const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
-    uint4 h = make_uint4(0, 0, 0, 0);
-    if (with_results) h = a.m2tx[((uint64_t)q * a.cm + k) * kVLineU4];
-    GroupM G;
-    G.hi = u4lo(r2);
-    G.glo = u4hi(r2);
-    G.n_del = r0.z;
-    G.n_create = r0.w;
-    G.fcs = r1.y;
-    G.len = 0;
-    G.slot = -1;
-    G.flags = 0;
-    G.fl = 0;
-    G.n_succ = h.y;
-    G.mlo = h.z;
-    G.mhi = h.w;
-    G.head = r1.z;
-    G.pad = 0;
-    g[k] = G;
-    atomicAdd(s_ng, r0.x == a.stamp ? 1u : 0u);  // unconditional: no code path skipped
+  // a record by 8 lanes, one whole line per load instruction (words 1..2 go
+  // to the record's first lane by shuffles): a line read in 16-B pieces by
+  // several instructions is fetched whole or in halves depending on timing
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  for (uint32_t k0 = wave * 8; k0 < a.cm; k0 += 32) {  // cm only
+    const uint32_t k = k0 + (lane >> 3);
+    const uint64_t gi = (uint64_t)q * a.cm + min(k, a.cm - 1u);
+    const uint4 x = a.gtx[gi * 8 + (lane & 7u)];
+    const uint4 hx = with_results ? a.m2tx[gi * kVLineU4 + (lane & 7u)] : make_uint4(0, 0, 0, 0);
+    const int l0 = (int)(lane & ~7u);
+    const uint4 r0 = x, r1 = shfl4(x, l0 + 1), r2 = shfl4(x, l0 + 2), h = hx;
+    if ((lane & 7u) == 0u && k < a.cm) {
+      GroupM G;
+      G.hi = u4lo(r2);
+      G.glo = u4hi(r2);
+      G.n_del = r0.z;
+      G.n_create = r0.w;
+      G.fcs = r1.y;
+      G.len = 0;
+      G.slot = -1;
+      G.flags = 0;
+      G.fl = 0;
+      G.n_succ = h.y;
+      G.mlo = h.z;
+      G.mhi = h.w;
+      G.head = r1.z;
+      G.pad = 0;
+      g[k] = G;
+      atomicAdd(s_ng, r0.x == a.stamp ? 1u : 0u);  // unconditional: no code path skipped
+    }
   }
   __syncthreads();
   return *s_ng;
@@ -341,7 +349,14 @@ struct M1rArgs {
 struct M1rOp {
   using Args = M1rArgs;
   static constexpr bool kSelect = true;
-  static constexpr bool kStash = false;
+  // the block's 64 MPOS records read once, one whole line per load instruction
+  // (8 lanes each; a 16-B record loaded by itself fetched its line whole or in
+  // halves depending on timing: FETCH_SIZE moved with the mix)
+  static constexpr bool kStash = true;
+  __device__ static uint4 rec_line(const Args& a, uint64_t i) {
+    return (i & 7u) == 0u ? a.mpos[i >> 3] : make_uint4(0, 0, 0, 0);
+  }
+  __device__ static uint4 f_of_rec(const uint4* r) { return f_of_pos(uni4(r[0]).x); }
   __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
     return sel4(b.x != 0u, b, make_uint4(a.x, a.y + b.y, a.z + b.z, 0u));
@@ -373,11 +388,13 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
   if (a.scal->error) return;
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
-  // each op's own MSNAPP line, read once
+  // the wave's 16 MPOS records in one load (two whole lines), op j's to every
+  // lane by a shuffle; each op's own MSNAPP line, read once
+  const uint4 mp_l = a.mpos[p0 + (lane & 15u)];
   uint4 As[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    const uint4 mp = uni4(a.mpos[p0 + j]);
+    const uint4 mp = uni4(shfl4(mp_l, (int)j));
     As[j] = ld_row<false>(&M1rOp::src_of(a, p0 + j, mp)[lane]);
   }
   uint4 cf, cv;
@@ -385,7 +402,7 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     uint4 f = M1rOp::f_identity(), v = As[0];
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
-      const uint4 e = M1rOp::f_of(a, p0 + j);
+      const uint4 e = M1rOp::f_of_pos(uni4(shfl4(mp_l, (int)j)).x);
       v = sel4(M1rOp::takes_b(f, e), As[j], v);
       f = M1rOp::f_combine(f, e);
     }
@@ -398,7 +415,7 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
-    const uint4 mp = uni4(a.mpos[p]);
+    const uint4 mp = uni4(shfl4(mp_l, (int)j));
     const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
     const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;
     const uint4 A = As[j];
@@ -531,15 +548,24 @@ __global__ __launch_bounds__(256) void k_m2r_c(M2rArgs a) {
   uint4 cf, cv;
   vscan_carry_in<M2rOp>(a, s_v, s_f, cf, cv);
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
+  // the wave's 16 MPOS records and 16 M2G lines, each line read whole by one
+  // load instruction (records handed to every lane by shuffles)
+  const uint4 mp_l = a.mpos[p0 + (lane & 15u)];
+  const uint4 g_lo = a.m2g[(uint64_t)p0 * 8 + lane], g_hi = a.m2g[(uint64_t)p0 * 8 + 64 + lane];
+#pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;
-    const uint4 mp = uni4(a.mpos[p]);
+    const uint4 mp = uni4(shfl4(mp_l, (int)j));
     const bool last = (mp.x & kMPosLast) && !(mp.x & kMPosNull);
-    const uint4 e = M2rOp::f_of(a, p);
-    cv = M2rOp::v_combine(cf, cv, e, M2rOp::value_of(a, p, e));
+    const uint4 gl = j < 8 ? g_lo : g_hi;
+    const int gb = (int)(j & 7u) * 8;
+    const uint4 e = uni4(shfl4(gl, gb));
+    const uint4 id = shfl4(gl, gb + 1);
+    const uint4 val = sel4(e.w != 0u && lane == 2u + mp.w && mp.w < GVS_MAILBOX_SLOTS, id, make_uint4(0, 0, 0, 0));
+    cv = M2rOp::v_combine(cf, cv, e, val);
     cf = M2rOp::f_combine(cf, e);
     // the group's last op writes its result slot, every other op a dummy
-    const uint4 x0 = a.m2g[(uint64_t)p * 8 + 2], x1 = a.m2g[(uint64_t)p * 8 + 3];
+    const uint4 x0 = shfl4(gl, gb + 2), x1 = shfl4(gl, gb + 3);
     const uint64_t o = (last ? (uint64_t)mp.y : (uint64_t)a.Q * a.cm + p) * kVLineU4;
     // value: lanes 0..1 the recipient key (a new mailbox's first 32 B), lanes
     // 2.. the appended ids; header: stamp, creates, removal mask

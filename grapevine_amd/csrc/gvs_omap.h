@@ -376,17 +376,17 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     kd[j0 * 2 + lane] = sel4(lane & 1u, hlo, klo);
     kd[j0 * 2 + 64 + lane] = sel4(lane & 1u, hhi, khi);
   }
-  // each group's result to its head position (slots without a group: dummies)
-  for (uint32_t k = tid; k < a.c; k += 256) {
+  // each group's result to its head position (slots without a group:
+  // dummies), a record by 8 lanes: one whole-line store
+  for (uint32_t k0 = wave * 8; k0 < a.c; k0 += 32) {  // c only
+    const uint32_t k = min(k0 + (lane >> 3), a.c - 1u);
     const GroupO& G = g[k];
     const bool real = k < ng;
     const bool ovf = real && s_need[k] && s_npfx[k] >= nadm;
     const uint64_t prow = G.row >= 0 ? (uint64_t)w * a.S + (uint32_t)G.row : ~0ull;
     const uint64_t idx = real ? G.head : (uint64_t)a.B + (uint64_t)w * a.c + k;
     const uint4 rec0 = make_uint4((uint32_t)prow, (uint32_t)(prow >> 32), (G.e0 ? 1u : 0u) | (ovf ? 2u : 0u), 0u);
-    st_drop(a.ogp, idx * 8, rec0);
-#pragma unroll
-    for (int cc = 1; cc < 8; ++cc) st_drop(a.ogp, idx * 8 + cc, make_uint4(0, 0, 0, 0));
+    if (k0 + (lane >> 3) < a.c) st_drop(a.ogp, idx * 8 + (lane & 7u), sel4((lane & 7u) == 0u, rec0, make_uint4(0, 0, 0, 0)));
   }
 }
 

@@ -1013,17 +1013,30 @@ __global__ __launch_bounds__(256) void k_vscan_b3(typename Op::Args a) {
 // Phase C prologue, second half: given the aggregate (f, v) of this wave's
 // 16 ops, the carry into its first op (block carry, then the aggregates of
 // the block's earlier waves through LDS).
+// The block's carry record into LDS, read by wave 0 only and as whole lines
+// (the flag line by 8 lanes, the value by 64): four waves reading the same
+// lines hit or miss depending on timing, and a 16-B read fetches its line
+// whole or in halves.  The caller's barrier publishes it.
+__device__ inline void vcarry_stage(const uint4* c, uint4* s_c) {
+  const uint32_t lane = lane_id();
+  if ((threadIdx.x >> 6) == 0) {
+    s_c[8 + lane] = c[8 + lane];
+    if (lane < 8) s_c[lane] = c[lane];
+  }
+}
+
 template <class Op>
 __device__ inline void vscan_carry_tail(const typename Op::Args& a, uint4 (*s_v)[64], uint4* s_f,
                                         uint4 f, uint4 v, uint4& cf, uint4& cv) {
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x;
+  __shared__ uint4 s_c[kVLineU4];
+  vcarry_stage(a.vcarry + (uint64_t)b * kVLineU4, s_c);
   s_v[wave][lane] = v;
   if (lane == 0) s_f[wave] = f;
   __syncthreads();
-  const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
-  cf = uni4(c[0]);
-  cv = c[8 + lane];
+  cf = s_c[0];
+  cv = s_c[8 + lane];
   for (uint32_t k = 0; k < wave; ++k) {
     const uint4 e = s_f[k];
     cv = Op::v_combine(cf, cv, e, s_v[k][lane]);
@@ -1048,12 +1061,13 @@ __device__ inline void vscan_carry_in(const typename Op::Args& a, uint4 (*s_v)[6
     v = Op::v_combine(f, v, e, Op::value_of(a, p0 + j, e));
     f = Op::f_combine(f, e);
   }
+  __shared__ uint4 s_c[kVLineU4];
+  vcarry_stage(a.vcarry + (uint64_t)b * kVLineU4, s_c);
   s_v[wave][lane] = v;
   if (lane == 0) s_f[wave] = f;
   __syncthreads();
-  const uint4* c = a.vcarry + (uint64_t)b * kVLineU4;
-  cf = uni4(c[0]);
-  cv = c[8 + lane];
+  cf = s_c[0];
+  cv = s_c[8 + lane];
   for (uint32_t k = 0; k < wave; ++k) {
     const uint4 e = s_f[k];
     cv = Op::v_combine(cf, cv, e, s_v[k][lane]);
