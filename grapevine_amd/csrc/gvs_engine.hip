@@ -836,7 +836,8 @@ static void vscan_fields(A& a, const Engine& e) {
 // the four scan kernels of a 1 KiB copy-forward (phase C is op-specific)
 template <class Op>
 static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
-  hipLaunchKernelGGL(k_vscan_a<Op>, dim3((a.nvb + 3) / 4), dim3(256), 0, s, a);
+  // select scans: one block per workgroup; merge scans: one per wave
+  hipLaunchKernelGGL(k_vscan_a<Op>, dim3(Op::kSelect ? a.nvb : (a.nvb + 3) / 4), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_vscan_b1<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_vscan_b2<Op>, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(k_vscan_b3<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
