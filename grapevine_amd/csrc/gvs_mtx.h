@@ -487,7 +487,15 @@ struct M2rArgs {
 struct M2rOp {
   using Args = M2rArgs;
   static constexpr bool kSelect = false;
-  static constexpr bool kStash = false;
+  // phase A reads each position's M2G line once, whole (k_m2g puts MPOS.w,
+  // the create rank, in word 4)
+  static constexpr bool kStash = true;
+  __device__ static uint4 rec_line(const Args& a, uint64_t i) { return a.m2g[i]; }
+  __device__ static uint4 f_of_rec(const uint4* r) { return uni4(r[0]); }
+  __device__ static uint4 value_of_rec(const uint4* r, uint4 e) {
+    const uint32_t rank = uni4(r[4]).x;
+    return sel4(e.w != 0u && lane_id() == 2u + rank && rank < GVS_MAILBOX_SLOTS, r[1], make_uint4(0, 0, 0, 0));
+  }
   __device__ static uint4 f_identity() { return make_uint4(0, 0, 0, 0); }
   __device__ static uint4 f_combine(uint4 a, uint4 b) {
     return sel4(b.x != 0u, b, make_uint4(a.x, a.y | b.y, a.z | b.z, a.w + b.w));
@@ -522,7 +530,8 @@ __global__ __launch_bounds__(256) void k_m2g(M2rArgs a) {
   if (a.scal->error) return;
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
   uint4* st = stage + (threadIdx.x >> 6) * 64 * 8;
-  const uint32_t mpx = a.mpos[p].x, seq = mpx & kSeqMask;
+  const uint4 mp4 = a.mpos[p];
+  const uint32_t mpx = mp4.x, seq = mpx & kSeqMask;
   uint4 l[8], rec[8];
   wave_load128(st, reinterpret_cast<const uint4*>(a.rres + seq), l);
   const uint32_t status = l[0].x;
@@ -535,8 +544,9 @@ __global__ __launch_bounds__(256) void k_m2g(M2rArgs a) {
   const uint32_t* ow = reinterpret_cast<const uint32_t*>(l);  // OpState: x is words 14..21
   rec[2] = make_uint4(ow[14], ow[15], ow[16], ow[17]);
   rec[3] = make_uint4(ow[18], ow[19], ow[20], ow[21]);
+  rec[4] = make_uint4(mp4.w, 0, 0, 0);  // the op's rank among its group's creates
 #pragma unroll
-  for (int i = 4; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
+  for (int i = 5; i < 8; ++i) rec[i] = make_uint4(0, 0, 0, 0);
   wave_store128(st, a.m2g, p, rec);
 }
 
@@ -545,13 +555,28 @@ __global__ __launch_bounds__(256) void k_m2r_c(M2rArgs a) {
   __shared__ uint4 s_f[4];
   if (a.scal->error) return;
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  uint4 cf, cv;
-  vscan_carry_in<M2rOp>(a, s_v, s_f, cf, cv);
   const uint32_t p0 = blockIdx.x * kVBlk + wave * 16;
   // the wave's 16 MPOS records and 16 M2G lines, each line read whole by one
-  // load instruction (records handed to every lane by shuffles)
+  // load instruction (records handed to every lane by shuffles), read once:
+  // the wave's aggregate comes from them too
   const uint4 mp_l = a.mpos[p0 + (lane & 15u)];
   const uint4 g_lo = a.m2g[(uint64_t)p0 * 8 + lane], g_hi = a.m2g[(uint64_t)p0 * 8 + 64 + lane];
+  uint4 cf, cv;
+  {
+    uint4 f = M2rOp::f_identity(), v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint4 gl = j < 8 ? g_lo : g_hi;
+      const int gb = (int)(j & 7u) * 8;
+      const uint4 e = uni4(shfl4(gl, gb));
+      const uint32_t rank = uni4(shfl4(mp_l, (int)j)).w;
+      const uint4 id = shfl4(gl, gb + 1);
+      v = M2rOp::v_combine(f, v, e, sel4(e.w != 0u && lane == 2u + rank && rank < GVS_MAILBOX_SLOTS, id,
+                                         make_uint4(0, 0, 0, 0)));
+      f = M2rOp::f_combine(f, e);
+    }
+    vscan_carry_tail<M2rOp>(a, s_v, s_f, f, v, cf, cv);
+  }
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
     const uint32_t p = p0 + j;

@@ -924,6 +924,23 @@ __global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
     s_x[wave][lane] = v;  // every wave writes its candidate; op d's wave holds the value
     __syncthreads();
     if (wave == 0) vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, Op::value_fin(f, s_x[d >> 4][lane]));
+  } else if constexpr (Op::kStash) {
+    // merge scans with stashed records: a block per wave, its 64 records
+    // read once (8 whole-line loads in flight together), walked from LDS
+    __shared__ uint4 s_rec[4][kVBlk * 8];
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+    if (b >= a.nvb) return;  // the grid's last workgroup only
+    uint4* rec = s_rec[threadIdx.x >> 6];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) rec[i * 64 + lane] = Op::rec_line(a, (uint64_t)b * kVBlk * 8 + i * 64 + lane);
+    wave_lds_sync();
+    uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
+    for (uint32_t j = 0; j < kVBlk; ++j) {
+      const uint4 e = Op::f_of_rec(rec + j * 8);
+      v = Op::v_combine(f, v, e, Op::value_of_rec(rec + j * 8, e));
+      f = Op::f_combine(f, e);
+    }
+    vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, v);
   } else {
     const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= a.nvb) return;
