@@ -724,6 +724,10 @@ static void sort_tiles(hipStream_t s, K* d, uint32_t n) {
   hipLaunchKernelGGL((k_bitonic_tile<K, E>), dim3(n / L), dim3(1024), 0, s, d, 0u, 1);
   for (uint32_t k = 2 * L; (k >> 1) < n; k <<= 1) {
     uint32_t j = k >> 1;
+    for (; j >= 8 * L; j >>= 4) {  // four steps per launch while all are global
+      const uint32_t nq = lower_count(n, 2 * j, j >> 3);
+      hipLaunchKernelGGL(k_bitonic_global4<K>, dim3((nq + 255) / 256), dim3(256), 0, s, d, n, k, j, nq);
+    }
     for (; j >= 2 * L; j >>= 2) {  // two steps per launch while both are global
       const uint32_t nq = lower_count(n, 2 * j, j >> 1);
       hipLaunchKernelGGL(k_bitonic_global2<K>, dim3((nq + 255) / 256), dim3(256), 0, s, d, n, k, j, nq);
@@ -736,6 +740,9 @@ static void sort_tiles(hipStream_t s, K* d, uint32_t n) {
   }
 }
 
+// Tiles of 1024 keys (EMAX = 1) at every call: 64 workgroups per tile launch
+// for a 64K batch instead of 8-16, which outweighs the extra global steps
+// (C3: both sorts 0.23 -> 0.145 ms per batch, profiles/r03n_pass_ab.txt)
 template <typename K, int EMAX>
 static int sort_keys(gvs_handle* h, K* d, uint32_t n) {
   if (n < 1024 || n % 1024) return GVS_ERR_INTERNAL;
@@ -836,8 +843,7 @@ static void vscan_fields(A& a, const Engine& e) {
 // the four scan kernels of a 1 KiB copy-forward (phase C is op-specific)
 template <class Op>
 static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
-  // select scans: one block per workgroup; merge scans: one per wave
-  hipLaunchKernelGGL(k_vscan_a<Op>, dim3(Op::kSelect ? a.nvb : (a.nvb + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_vscan_a<Op>, dim3((a.nvb + 3) / 4), dim3(256), 0, s, a);  // a block per wave
   hipLaunchKernelGGL(k_vscan_b1<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_vscan_b2<Op>, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(k_vscan_b3<Op>, dim3(a.nvb2), dim3(256), 0, s, a);
@@ -865,7 +871,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
   }
   mark(h, "meta");
-  if (int r = sort_keys<Key128, 4>(h, e.s1keys, B)) return r;
+  if (int r = sort_keys<Key128, 1>(h, e.s1keys, B)) return r;
   mark(h, "sort_s1");
   {
     GtxArgs a{e.s1keys, e.ops, e.mpos, e.gtx, e.gtx_agg, e.gtx_carry, e.scal,
@@ -900,7 +906,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
   }
   mark(h, "alloc");
-  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  if (int r = sort_keys<uint64_t, 1>(h, e.rkeys, B)) return r;
   mark(h, "sort_r");
   {
     RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,
@@ -1062,7 +1068,7 @@ static int route(gvs_handle* h, const Router& r, const Engine& e, const uint4* i
   const RouteArgs a = rargs(h, r, e, in, n);
   const uint32_t nblk = h->Bsub / 1024;
   hipLaunchKernelGGL(k_route_dest, dim3(nblk), dim3(1024), 0, s, a);
-  if (int rc = sort_keys<uint64_t, 8>(h, r.rkey, h->Bsub)) return rc;  // by (routing key, index)
+  if (int rc = sort_keys<uint64_t, 1>(h, r.rkey, h->Bsub)) return rc;  // by (routing key, index)
   hipLaunchKernelGGL(k_route_cap, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_route_hist, dim3(nblk), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_route_pos, dim3(nblk), dim3(1024), 0, s, a);
@@ -1355,7 +1361,7 @@ static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_bcopy, dim3(B / 256), dim3(256), 0, s, a);
   }
   mark(h, "copy");
-  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  if (int r = sort_keys<uint64_t, 1>(h, e.rkeys, B)) return r;
   mark(h, "sort_r");
   {
     RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,
@@ -1411,7 +1417,7 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_ocopy, dim3(B / 256), dim3(256), 0, s, a);
   }
   mark(h, "copy");
-  if (int r = sort_keys<Key128, 4>(h, e.okeys, B)) return r;
+  if (int r = sort_keys<Key128, 1>(h, e.okeys, B)) return r;
   hipLaunchKernelGGL(k_ogather, dim3(B / 256), dim3(256), 0, s, OposArgs{e.okeys, e.kvmeta, e.opr, B});
   mark(h, "sort_k");
   {
@@ -1432,7 +1438,7 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_scan_c<OrowOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
   mark(h, "rows");
-  if (int r = sort_keys<uint64_t, 8>(h, e.rkeys, B)) return r;
+  if (int r = sort_keys<uint64_t, 1>(h, e.rkeys, B)) return r;
   mark(h, "sort_r");
   {
     RtxArgs a{e.rkeys, e.rpos, e.tbuf[e.par], e.rtx_agg, e.rtx_carry, e.scal,

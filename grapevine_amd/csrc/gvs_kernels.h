@@ -188,6 +188,52 @@ __global__ __launch_bounds__(256) void k_bitonic_global2(K* data, uint32_t n, ui
   if (l3) data[x3] = v3;
 }
 
+// Four steps (j .. j/8) of merge level k: each thread owns the 16 keys of a
+// block of 2j at offsets o + a q (q = j/8, o < q, a < 16); on a level's first
+// step (flip) the upper eight are the mirrors of the lower eight, stored in
+// ascending order (v[8 + b] = mirror of lower key 7 - b), so that the three
+// later steps are the same for both.  nq = groups whose lowest key is < n.
+// Static indices only, flip as selects (see k_bitonic_global2).
+template <typename K>
+__global__ __launch_bounds__(256) void k_bitonic_global4(K* data, uint32_t n, uint32_t k,
+                                                         uint32_t j, uint32_t nq) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nq) return;
+  const uint32_t q = j >> 3;
+  const uint32_t base = (p / q) * 2u * j, o = p % q;
+  const bool flip = (j << 1) == k;
+  uint32_t x[16];
+  bool l[16];
+#pragma unroll
+  for (uint32_t a = 0; a < 16; ++a) {
+    // flip: upper key b = mirror of lower key 7 - b = base + j + (q - 1 - o) + b q
+    const uint32_t up = base + j + (flip ? q - 1u - o : o) + (a - 8u) * q;
+    x[a] = a < 8 ? base + o + a * q : up;
+    l[a] = x[a] < n;
+  }
+  K v[16];
+#pragma unroll
+  for (uint32_t a = 0; a < 16; ++a) v[a] = data[l[a] ? x[a] : x[0]];
+  // step j: (a, a + 8), or on a flip (a, 15 - a)
+  K t[8];
+#pragma unroll
+  for (uint32_t a = 0; a < 8; ++a) {
+    t[a] = key_sel(flip, v[15 - a], v[8 + a]);
+    cx_static(v[a], t[a], flip ? l[15 - a] : l[8 + a]);
+  }
+#pragma unroll
+  for (uint32_t a = 0; a < 8; ++a) v[8 + a] = key_sel(flip, t[7 - a], t[a]);
+  // steps j/2, j/4, j/8 inside each half
+#pragma unroll
+  for (uint32_t s = 4; s >= 1; s >>= 1)
+#pragma unroll
+    for (uint32_t a = 0; a < 16; ++a)
+      if ((a & s) == 0u) cx_static(v[a], v[a + s], l[a + s]);
+#pragma unroll
+  for (uint32_t a = 0; a < 16; ++a)
+    if (l[a]) data[x[a]] = v[a];
+}
+
 // One step j of merge level k: pair (i, i ^ (2j - 1)) on the level's first
 // step, else (i, i + j); np = pairs with i < n.
 template <typename K>

@@ -893,37 +893,36 @@ template <class Op>
 __global__ __launch_bounds__(256) void k_vscan_a(typename Op::Args a) {
   if (a.scal->error) return;
   if constexpr (Op::kSelect) {
-    // one block per workgroup: its 64 position records read once into LDS
-    // (two whole-line loads per wave), the block's transform and defining op
-    // d from them, then each wave reads the rows of 16 of the ops and keeps
-    // op d's (every op's rows are read whatever d is)
+    // one block per wave: its 64 position records read once into LDS (8
+    // whole-line loads), the block's transform and defining op d from them,
+    // then every op's rows are read and op d's kept.  (One block per
+    // workgroup, each wave reading 16 ops' rows, ran 2-3x faster and made the
+    // kernel's duration follow how many of the rows the previous kernel had
+    // just written, i.e. the number of groups: tests/test_timing.py,
+    // profiles/r03u_timing_c3.txt.)
     static_assert(Op::kStash, "select scans read their records once (stash)");
-    __shared__ uint4 s_rec[kVBlk * 8];
-    __shared__ uint4 s_x[4][64];
-    const uint32_t b = blockIdx.x, lane = lane_id(), wave = threadIdx.x >> 6;
-    if (b >= a.nvb) return;  // grid-uniform
+    __shared__ uint4 s_rec[4][kVBlk * 8];
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+    if (b >= a.nvb) return;
+    uint4* rec = s_rec[threadIdx.x >> 6];
 #pragma unroll
-    for (uint32_t i = wave; i < 8u; i += 4u)
-      s_rec[i * 64 + lane] = Op::rec_line(a, (uint64_t)b * kVBlk * 8 + i * 64 + lane);
-    __syncthreads();
-    uint4 f = Op::f_identity();
+    for (uint32_t i = 0; i < 8; ++i) rec[i * 64 + lane] = Op::rec_line(a, (uint64_t)b * kVBlk * 8 + i * 64 + lane);
+    wave_lds_sync();
+    uint4 f = Op::f_identity(), v = make_uint4(0, 0, 0, 0);
     uint32_t d = 0;
     for (uint32_t j = 0; j < kVBlk; ++j) {
-      const uint4 e = Op::f_of_rec(s_rec + j * 8);
+      const uint4 e = Op::f_of_rec(rec + j * 8);
       d = Op::takes_b(f, e) ? j : d;
       f = Op::f_combine(f, e);
     }
-    uint4 v = make_uint4(0, 0, 0, 0);
-    for (uint32_t j0 = wave * 16u; j0 < wave * 16u + 16u; j0 += 8) {
+    for (uint32_t j0 = 0; j0 < kVBlk; j0 += 8) {
       uint4 x[8];
 #pragma unroll
-      for (uint32_t u = 0; u < 8; ++u) x[u] = Op::elem_value(a, b * kVBlk + j0 + u, s_rec + (j0 + u) * 8);
+      for (uint32_t u = 0; u < 8; ++u) x[u] = Op::elem_value(a, b * kVBlk + j0 + u, rec + (j0 + u) * 8);
 #pragma unroll
       for (uint32_t u = 0; u < 8; ++u) v = sel4(j0 + u == d, x[u], v);
     }
-    s_x[wave][lane] = v;  // every wave writes its candidate; op d's wave holds the value
-    __syncthreads();
-    if (wave == 0) vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, Op::value_fin(f, s_x[d >> 4][lane]));
+    vrec_store(a.vagg + (uint64_t)b * kVLineU4, f, Op::value_fin(f, v));
   } else if constexpr (Op::kStash) {
     // merge scans with stashed records: a block per wave, its 64 records
     // read once (8 whole-line loads in flight together), walked from LDS
