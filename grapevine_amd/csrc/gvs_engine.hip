@@ -1755,9 +1755,13 @@ int gvs_process_batches_device(gvs_handle* h, const void* d_reqs, const uint32_t
       break;
     }
     snap[t] = save_state(h);
-    if (int r = run_batch(h, in + off * kAbiU4, counts[t], out + off * kAbiU4, false)) return r;
-    if (h->mode != kSingle)
-      if (int r = agree_errors(h)) return r;
+    int r = run_batch(h, in + off * kAbiU4, counts[t], out + off * kAbiU4, false);
+    if (!r && h->mode != kSingle) r = agree_errors(h);
+    if (r) {  // batch t was not (wholly) enqueued: the ones before it still count
+      restore_state(h, snap[t]);
+      stop = r;
+      break;
+    }
     GVS_HIP(h, hipMemcpyAsync(&p.errs[t], &h->eng[0].scal->error, sizeof(uint32_t),
                               hipMemcpyDeviceToHost, h->stream));
     advance(h);  // as if applied; rolled back below if it was not
@@ -1776,6 +1780,10 @@ int gvs_process_batches_device(gvs_handle* h, const void* d_reqs, const uint32_t
     }
     off += counts[t];
     if (applied) *applied = t + 1;
+  }
+  if (stop != GVS_OK && off < total) {  // the batches not applied answer nothing
+    GVS_HIP(h, hipMemsetAsync(out + off * kAbiU4, 0, (size_t)(total - off) * sizeof(gvs_response), h->stream));
+    GVS_HIP(h, hipStreamSynchronize(h->stream));
   }
   return stop;
 }

@@ -415,9 +415,12 @@ __global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+#ifndef GVS_DIAG_NT
+#define GVS_DIAG_NT 0  // diagnostic builds only: every ld_row non-temporal
+#endif
 template <bool NT>
 __device__ inline uint4 ld_row(const uint4* p) {
-  if (NT) {
+  if (NT || GVS_DIAG_NT) {
     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
   }

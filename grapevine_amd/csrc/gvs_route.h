@@ -20,8 +20,13 @@
 // they travel as hard errors to the shard i mod S (spread like malformed
 // requests, so they never load the hot key's shard) and the source answers
 // them INTERNAL_ERROR (8) with the request's time.  One recipient can then put
-// at most kRouteKeyCap requests of one kind into a bucket, and a hostile
-// client fails only its own excess requests instead of the whole window.
+// at most kRouteKeyCap requests of one kind into a bucket, so a hot key fails
+// its own excess instead of the whole window.  The cap is shared by every
+// client of the key: the requests past the first kRouteKeyCap to one mailbox
+// or id in a window are shed whoever sent them (a client that floods a
+// recipient also sheds other senders' creates to it in that window).  Keys
+// are keyed hashes (SipHash with the store's recipient key), so a client
+// cannot aim its requests at another mailbox's or id's key without naming it.
 #pragma once
 #include "gvs_device.h"
 
@@ -64,13 +69,15 @@ __host__ __device__ inline uint32_t route_dest_key(const RouteArgs& a, uint32_t 
   const bool hard = type < 1u || type > 4u || auth_zero || (type == 3u && id_zero);
   const bool next = (type == 2u || type == 4u) && id_zero;
   const uint4 xa = next ? c1 : c3, xb = next ? c2 : c4;
-  // both hashes run for every request (fixed work)
+  // every hash runs for every request (fixed work)
   const uint64_t x[4] = {u4lo(xa), u4hi(xa), u4lo(xb), u4hi(xb)};
   const uint64_t lo = siphash24_blocks(a.kc.hk0, a.kc.hk1, x, 4, 2, 33);
   const uint32_t by_key = shard_of_hash(lo, a.S);
   const uint32_t by_id = id_shard(a.kc, u4lo(c0), u4hi(c0), a.N);
   const uint32_t spread = i % a.S;
-  const uint32_t kh = (uint32_t)(lo >> 32) & ~3u, ki = (c0.x ^ c0.y ^ c0.z ^ c0.w) & ~3u;
+  const uint64_t idw[2] = {u4lo(c0), u4hi(c0)};
+  const uint64_t hid = siphash24_blocks(a.kc.hk0, a.kc.hk1, idw, 2, 3, 17);  // id || 0x03
+  const uint32_t kh = (uint32_t)(lo >> 32) & ~3u, ki = (uint32_t)(hid >> 32) & ~3u;
   if (hard) return spread;
   if (type == 1u) {
     key = rcpt_zero ? kKeyNone : kh | 1u;

@@ -54,7 +54,8 @@ def load_library(path=None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or (_TEST_LIB_PATH if test_hooks_enabled() else _LIB_PATH)
+    # GVS_LIB_OVERRIDE: a diagnostic build of the same engine (tools/, A/B runs)
+    p = path or os.environ.get("GVS_LIB_OVERRIDE") or (_TEST_LIB_PATH if test_hooks_enabled() else _LIB_PATH)
     if not os.path.exists(p):
         raise RuntimeError(f"{os.path.basename(p)} not built at {p}; run `make` (HIP extension missing)")
     lib = ctypes.CDLL(p)

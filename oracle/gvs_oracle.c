@@ -745,9 +745,11 @@ uint32_t gvo_route_key(const uint8_t key[32], const gvs_request *rq) {
     gvo_recipient_hash(key + 16, rq->auth_identity, &hi, &lo);
     return ((uint32_t)(lo >> 32) & ~3u) | 2u;
   }
-  uint32_t w[4];
-  memcpy(w, rq->msg_id, 16);
-  return ((w[0] ^ w[1] ^ w[2] ^ w[3]) & ~3u) | 3u;
+  uint8_t msg[17];  /* keyed: id || 0x03 */
+  memcpy(msg, rq->msg_id, 16);
+  msg[16] = 3;
+  const uint64_t h = gvo_siphash24(ld64(key + 16), ld64(key + 24), msg, 17);
+  return ((uint32_t)(h >> 32) & ~3u) | 3u;
 }
 
 uint32_t gvo_route_capacity(uint32_t batch, uint32_t n_shards) {

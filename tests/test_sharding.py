@@ -225,3 +225,24 @@ def test_hot_recipient_is_shed_not_rejected():
     ok = out["status_code"] == 1
     assert ok[~shed].sum() > 0 and not ok[shed].any()
     assert cl.messages == msgs + int(ok.sum())
+
+@pytest.mark.parametrize("S", [4, 8])
+def test_realistic_traffic_is_never_shed(S):
+    """The routing-key cap (DESIGN.md §6 "Hot keys") changes what a client
+    sees only when one source window sends more than ROUTE_KEY_CAP requests to
+    one mailbox or id: the unsharded store never sheds, so a shed request is a
+    client-visible deviation (INTERNAL_ERROR where the reference would have
+    processed it).  On realistic traffic (the bench's mix over many
+    identities, BASELINE config 3's 64K-request windows split over the
+    sources) nothing is shed, so sharded and unsharded stores answer alike."""
+    B = 8192
+    cl = ffi.Cluster(cluster_cfg(S, N=1 << 16, B=B, Q=64, Sr=64))
+    cl.seed(40 + S)
+    fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=20000)
+    mix = ffi.gen_params(n_identities=20000)
+    for batch in range(5):
+        reqs = cl.gen_batch(S * B, fill if batch < 2 else mix)
+        assert not shed_mask(cl.config, reqs, B).any(), batch
+        out = cl.process_batch(reqs)
+        assert out is not None
+        assert not (out["status_code"] == abi.STATUS_CODE_INTERNAL_ERROR).any(), batch
