@@ -7,7 +7,8 @@ Shapes: 64K-request batches (the C3 batch, so the multi-tile sorts and every
 global merge step run) over a 2^20-message store (2^21 authenticated), plain and authenticated
 (DESIGN.md §8); the routed path (2 shards in one process: k_route_* and the
 padded all-to-all); the block store and the key-value map (DESIGN.md §10);
-the wire path (decode, schnorrkel check, store, encode).
+the expiry sweep; the wire path (decode, schnorrkel check,
+store, encode).
 
 Every mix runs tools/oblivious_probe.py under rocprofv3 --pmc in a child
 process (one counter per run, never combined with other tracing).  The
@@ -59,6 +60,11 @@ SHAPES = {
                  mixes=["main", "all_read", "all_write", "hot", "chain"]),
     "omap": dict(args=["--omap", "--log2n", "20", "--batch", "65536"],
                  mixes=["main", "all_read", "all_insert", "all_remove", "hot", "miss"]),
+    # the expiry sweep (README.md:92-97): the main request mix
+    # with nothing, everything, or a few old rows (in a few partitions) past
+    # the cutoff (tools/oblivious_probe.py --expiry); main runs without a cutoff
+    "expiry": dict(args=["--log2n", "20", "--batch", "65536", "--expiry", "1024"],
+                   mixes=["main", "x_all", "x_few"]),
     # the wire path: launches and grids must not depend on forged signatures
     # or malformed messages either; the byte counters of the front-end
     # kernels are compared over requests that verify and decode (canonical or

@@ -3,15 +3,27 @@ READ, UPDATE and DELETE must be indistinguishable in access patterns *and
 timings*) at the headline shape, BASELINE config 3: a 2^24-message store and
 64K-request batches.
 
-Each mix runs tools/oblivious_probe.py under `rocprofv3 --kernel-trace`; every
-kernel's duration on the measured batches must match the reference mix within
-the run-to-run noise, taken from the prefill batches that every process runs
-identically.  The mixes include adversarial ones: every request aimed at one
-recipient (hot_next, hot_next_rud), every read missing (all_miss_read), only
-deletes.  A pass whose workgroups did work in proportion to the ops routed to
-them would show the hot mixes here."""
+Each mix runs tools/oblivious_probe.py under `rocprofv3 --kernel-trace`.  The
+measured batches are seed-controlled, as in tests/test_oblivious.py: SEEDS x
+PER_SEED batches, the request generator reseeded before each seed's batches,
+so that a mix's difference from the reference can be told from a difference
+between two draws.  The prefill batches are identical in every process, and a
+second reference process runs the reference mix again: both are the noise.
+
+Two checks per kernel (the counter test's, in microseconds):
+  * every measured batch of every mix within 3x the noise range + 2 us of the
+    reference median;
+  * no bias: a mix's mean within 5 standard errors (sigma pooled from the
+    identical-input samples) + 2 us of the reference mean.  A pass whose
+    workgroups did work in proportion to the rows or groups a batch touches
+    shows here under the hot and all-miss mixes.
+
+Shapes: the store under seven mixes, including adversarial ones (every request
+aimed at one recipient, every read missing, only deletes); the expiry sweep
+(README.md:92-97) with nothing, everything or a few old rows expired."""
 import csv
 import glob
+import math
 import os
 import shutil
 import statistics
@@ -25,18 +37,27 @@ from test_oblivious import PROBE, short, split_batches
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MIXES = ["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]
-ARGS = ["--log2n", "24", "--batch", "65536", "--identities", "200000", "--fill-batches", "4"]
-N_MEAS = 3
+ARGS = ["--log2n", "24", "--batch", "65536", "--identities", "200000", "--fill-batches", "3"]
+SHAPES = {
+    "store": dict(args=ARGS, ref="rud",
+                  mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
+    "expiry": dict(args=ARGS + ["--expiry", "1024"], ref="main", mixes=["main", "x_all", "x_few"]),
+}
+SEEDS = (1234, 99, 5)
+PER_SEED = 2
+N_MEAS = len(SEEDS) * PER_SEED
+FLOOR_US = 2.0       # trace-clock jitter floor, per batch and for the bias
+BIAS_SIGMAS = 5.0
 
 
-def kernel_trace(mix, outdir):
+def kernel_trace(mix, outdir, args):
     """(kernel, duration us) of every gvs kernel of one probe process."""
     if shutil.which("rocprofv3") is None:
         pytest.skip("rocprofv3 not available")
     os.makedirs(outdir, exist_ok=True)
     cmd = (["rocprofv3", "--kernel-trace", "-d", outdir, "-o", "run", "--output-format", "csv", "--",
-            sys.executable, PROBE, mix] + ARGS)
+            sys.executable, PROBE, mix, "--seeds", ",".join(map(str, SEEDS)), "--batches", str(PER_SEED)]
+           + args)
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
@@ -49,36 +70,60 @@ def kernel_trace(mix, outdir):
             for x in rows]
 
 
-def test_kernel_durations_independent_of_mix(tmp_path):
-    per_mix = {}
-    for mix in MIXES:
-        per_mix[mix] = [[(k, v) for k, _, _, v in b] for b in
-                        split_batches([(k, None, None, v) for k, v in kernel_trace(mix, str(tmp_path / mix))])]
-    ref_b = per_mix["rud"]
+def check_durations(shape, tmp_path):
+    sh = SHAPES[shape]
+    ref_mix = sh["ref"]
+    per = {}
+    for mix in sh["mixes"] + [ref_mix + "#2"]:
+        d = str(tmp_path / f"{shape}_{mix.replace('#', '_')}")
+        per[mix] = [[(k, v) for k, _, _, v in b] for b in
+                    split_batches([(k, None, None, v) for k, v in
+                                   kernel_trace(mix.split("#")[0], d, sh["args"])])]
+    ref_b = per[ref_mix]
     kernels = [k for k, _ in ref_b[-1]]
-    n_pre = min(len(bs) for bs in per_mix.values()) - N_MEAS
+    n_pre = min(len(bs) for bs in per.values()) - N_MEAS
     lines, bad = [], []
     for idx, k in enumerate(kernels):
-        # noise: spread of the identical prefill batches (batch 0: cold) across
-        # the processes, and of the reference mix's own measured batches
-        spread = 0.0
+        # noise: the identical prefill batches (batch 0: cold) across the
+        # processes, and the reference mix against its second process
+        rng, ss, dof = 0.0, 0.0, 0
         for i in range(1, n_pre):
-            v = [bs[i][idx][1] for bs in per_mix.values()]
-            spread = max(spread, max(v) - min(v))
+            v = [bs[i][idx][1] for bs in per.values()]
+            rng = max(rng, max(v) - min(v))
+            ss += statistics.variance(v) * (len(v) - 1)
+            dof += len(v) - 1
+        for x, y in zip(ref_b[-N_MEAS:], per[ref_mix + "#2"][-N_MEAS:]):
+            dd = x[idx][1] - y[idx][1]
+            rng = max(rng, abs(dd))
+            ss += dd * dd / 2.0
+            dof += 1
+        sigma = math.sqrt(ss / dof) if dof else 0.0
+        tol = 3.0 * rng + FLOOR_US
         own = [b[idx][1] for b in ref_b[-N_MEAS:]]
-        spread = max(spread, max(own) - min(own))
-        ref = statistics.median(own)
-        tol = 3.0 * spread + 2.0  # us; +2 us: launch-to-launch jitter floor of the trace clock
-        row = [f"{k[:30]:30s} ref={ref:10.1f}us spread={spread:7.1f} tol={tol:7.1f}"]
-        for mix, bs in per_mix.items():
+        ref, mu = statistics.median(own), statistics.fmean(own)
+        btol = BIAS_SIGMAS * sigma * math.sqrt(2.0 / N_MEAS) + FLOOR_US
+        row = [f"{k[:30]:30s} ref={ref:10.1f}us range={rng:7.1f} sigma={sigma:6.2f} tol={tol:7.1f} btol={btol:6.1f}"]
+        for mix, bs in per.items():
             assert [x[0] for x in bs[-1]] == kernels, f"{mix}: kernel sequence differs"
-            med = statistics.median(b[idx][1] for b in bs[-N_MEAS:])
-            row.append(f"{mix}:{med - ref:+.1f}")
-            if abs(med - ref) > tol:
-                bad.append((k, mix, round(med - ref, 1), round(tol, 1)))
+            meas = [b[idx][1] for b in bs[-N_MEAS:]]
+            dev = max(abs(v - ref) for v in meas)
+            bias = statistics.fmean(meas) - mu
+            row.append(f"{mix}:{dev:.1f}/{bias:+.1f}")
+            if dev > tol:
+                bad.append((k, mix, "batch", round(dev, 1), round(tol, 1)))
+            if mix != ref_mix and abs(bias) > btol:
+                bad.append((k, mix, "bias", round(bias, 1), round(btol, 1)))
         lines.append(" ".join(row))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "timing_c3.txt"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"timing_c3_{shape}.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
         f.write(f"violations: {bad}\n")
     assert not bad, f"kernel durations depend on the request mix: {bad}"
+
+
+def test_kernel_durations_independent_of_mix(tmp_path):
+    check_durations("store", tmp_path)
+
+
+def test_kernel_durations_independent_of_expiry(tmp_path):
+    check_durations("expiry", tmp_path)

@@ -15,6 +15,13 @@ the oracle's cluster model.
 --oram / --omap run the block store or the key-value map instead, with the
 op mixes of KV_MIXES (2^log2n blocks or rows, --batch ops per batch).
 
+--expiry X turns the expiry sweep on (X records per batch; the
+caller submits batch - X requests).  Its mixes run the main request mix and
+differ in what has expired: x_none (no message), x_all (every message: each
+swept partition finds rows), x_few (the oldest 16 (k + 1) messages at measured
+batch k, consecutive slots: expired rows in a few partitions only).  The
+prefill runs without a cutoff.
+
 --wire runs every batch (prefill included) through gvs_process_wire_batch:
 protobuf requests in 1200-B slots, decoded, their schnorrkel signatures
 checked against per-request challenges, the store, responses encoded.  The
@@ -44,7 +51,21 @@ MIXES = {
     "wire_forged": dict(create=25, read=25, update=25, delete=25, nxt=50),
     "wire_malformed": dict(create=25, read=25, update=25, delete=25, nxt=50),
     "wire_noncanonical": dict(create=25, read=25, update=25, delete=25, nxt=50),
+    # --expiry only: the main mix, with nothing / everything / a few old rows expired
+    "x_none": dict(create=25, read=25, update=25, delete=25, nxt=50),
+    "x_all": dict(create=25, read=25, update=25, delete=25, nxt=50),
+    "x_few": dict(create=25, read=25, update=25, delete=25, nxt=50),
 }
+TS0 = 1_700_000_000  # timestamp of the generator's first request (oracle gvo_gen_batch)
+
+
+def expiry_cutoff(mix, k):
+    """Cutoff before measured batch k of an --expiry mix."""
+    if mix == "x_all":
+        return 1 << 62
+    if mix == "x_few":
+        return TS0 + 1 + 16 * (k + 1)  # request j of the run has time TS0 + 1 + j
+    return 0
 WIRE_STRIDE = 1200
 
 # --oram / --omap (the block store and the key-value map, DESIGN.md §10):
@@ -205,6 +226,7 @@ def main():
     p.add_argument("--identities", type=int, default=5000)
     p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
     p.add_argument("--wire", action="store_true", help="wire path with challenge check")
+    p.add_argument("--expiry", type=int, default=0, help="expiry records per batch (x_* mixes)")
     p.add_argument("--seed", type=int, default=1234, help="generator seed of the measured batches")
     p.add_argument("--seeds", default="",
                    help="comma-separated seeds: the measured batches are --batches per seed, the "
@@ -217,11 +239,14 @@ def main():
     if a.oram or a.omap:
         return run_kv(a, "oram" if a.oram else "omap")
     assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
+    assert bool(a.expiry) == a.mix.startswith("x_") or (a.expiry and a.mix == "main"), \
+        "x_* mixes need --expiry (and --expiry takes x_* mixes or main)"
     S = a.shards if a.shards > 1 else 0
-    cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth, shard_count=S)
+    cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth, shard_count=S,
+                          expiry_per_batch=a.expiry)
     store = ObliviousStore(cfg)
     model = ffi.Cluster(cfg) if S else ffi.Model(cfg)
-    n = a.batch * (S or 1)
+    n = a.batch * (S or 1) - (0 if S else a.expiry)
     model.seed(77)
     fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=a.identities)
     wp = WirePath(store, model, a.identities) if a.wire else None
@@ -239,6 +264,10 @@ def main():
     for k in range(len(seeds) * a.batches):
         if k % a.batches == 0:
             model.seed(seeds[k // a.batches])  # same request-generator state for every mix
+        if a.expiry:
+            cut = expiry_cutoff(a.mix, k)
+            model.set_expiry_cutoff(cut)
+            store.set_expiry_cutoff(cut)
         reqs = model.gen_batch(n, params)
         if wp:
             wp.run(reqs, a.mix)
