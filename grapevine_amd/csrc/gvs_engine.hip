@@ -115,7 +115,7 @@ struct Engine {
   uint4* ptag = nullptr;     // B tags of P (authenticated storage)
   uint4* ps = nullptr;       // W*c x 1 KiB final states by slot (AUTH: + W*c x 128 B side entries)
   uint4* snapp = nullptr;    // B x 1 KiB row snapshots at their first op's position
-  uint4* dryb = nullptr;     // W x 1 KiB
+  uint4* dryb = nullptr;     // W x 4 KiB (k_rpass2: one 1 KiB per dry use)
   RtxV* rtx_agg = nullptr;
   RtxV* rtx_carry = nullptr;
   Rr1V* rr1_agg = nullptr;
@@ -132,7 +132,7 @@ struct Engine {
   uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
   uint4* msnap = nullptr;    // Q*cm x 1 KiB
   uint4* msnapp = nullptr;   // B x 1 KiB (group snapshots by head position)
-  uint4* mdry = nullptr;     // Q x 1 KiB
+  uint4* mdry = nullptr;     // Q x 4 KiB (k_m1x / k_m2x: one 1 KiB per dry use)
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
   GtxV* gtx_carry = nullptr;
@@ -210,6 +210,26 @@ struct WirePipe {
   hipEvent_t h2d[2] = {}, done[2] = {}, d2h[2] = {};
 };
 
+// Pinned bounce buffers of the single-call host APIs (gvs_process_batch, the
+// wire batch, the block store and the map).  A hipMemcpy from or to pageable
+// memory pins the caller's pages in place and unpins them afterwards; the
+// unmapping invalidates the device's TLB, so every kernel of the next batch
+// re-walks the page tables of the buffers it touches, a number of walks (L2
+// uncached reads, counted in FETCH_SIZE) that follows the batch's data
+// (DESIGN.md §3 "Counters").  Pageable caller memory is therefore copied by
+// the host into grow-only pinned buffers and moved by DMA from there.
+struct Bounce {
+  static constexpr int kSlots = 8;  // 0..3 in, 4..7 out
+  void* buf[kSlots] = {};
+  size_t cap[kSlots] = {};
+  struct Out {
+    void* dst;
+    int slot;
+    size_t bytes;
+  };
+  std::vector<Out> pend;  // device -> pinned copies enqueued, to hand to the caller after the sync
+};
+
 struct gvs_handle {
   gvs_config cfg{};
   Mode mode = kSingle;
@@ -240,6 +260,9 @@ struct gvs_handle {
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
+  Bounce bounce;
+  uint8_t* sr_dev = nullptr;  // gvs_sr25519_verify's device staging (grow-only)
+  size_t sr_cap = 0;
   std::vector<void*> allocs;
   std::string err;
 };
@@ -554,7 +577,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     if (h->auth) A(ptag, B);
     A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
     A(snapp, (uint64_t)B * 64);
-    A(dryb, (uint64_t)e.W * 64);
+    A(dryb, (uint64_t)e.W * 256);
     A(rtx_agg, B / kScanT);
     A(rtx_carry, B / kScanT);
     A(rr1_agg, B / kScanT);
@@ -574,7 +597,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(gtx, (QC + B) * 8);
     A(msnap, QC * 64);
     A(msnapp, (uint64_t)B * 64);
-    A(mdry, (uint64_t)e.Q * 64);
+    A(mdry, (uint64_t)e.Q * 256);
     A(m2tx, (QC + B) * kVLineU4);
     A(gtx_agg, B / kScanT);
     A(gtx_carry, B / kScanT);
@@ -950,6 +973,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.cutoff = h->cutoff;
   a.xbuf = e.X ? e.xb2[e.par] : nullptr;
   a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
+  a.diag = diag_bits();
   if (h->auth) {
     a.sc = seal_of(h, e);
     a.te = h->te;
@@ -966,7 +990,18 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     else
       hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+#ifndef GVS_DIAG_RP_NTL
+#define GVS_DIAG_RP_NTL true  // diagnostic builds only: the plain pass's load / store policy
+#define GVS_DIAG_RP_NTS true
+#endif
+    hipLaunchKernelGGL((k_rpass2<16, GVS_DIAG_RP_NTL, GVS_DIAG_RP_NTS, 2>), dim3(e.W), dim3(256), 0, s, a);
+    if (a.diag & 32u)  // diagnostic: the pass again on the same inputs (results wrong)
+      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
+    if (a.diag & 64u) {  // diagnostic: again as a pure stream (no slot work: idempotent)
+      R2Args b = a;
+      b.diag |= 16u;
+      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, b);
+    }
   }
 }
 
@@ -1301,7 +1336,7 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
   A(snapid, WC * 8);
   A(snapidp, (uint64_t)B * 8);
-  A(dryb, (uint64_t)e.W * 64);
+  A(dryb, (uint64_t)e.W * 256);
   A(rtx_agg, B / kScanT);
   A(rtx_carry, B / kScanT);
   const uint64_t nvb = B / kVBlk, nvb2 = (nvb + 63) / 64;
@@ -1514,6 +1549,9 @@ int gvs_destroy(gvs_handle* h) {
   }
   if (hp.herr) (void)hipHostFree(hp.herr);
   if (hp.errs) (void)hipHostFree(hp.errs);
+  for (void* q : h->bounce.buf)
+    if (q) (void)hipHostFree(q);
+  if (h->sr_dev) (void)hipFree(h->sr_dev);
   WirePipe& wp = h->wpipe;
   for (int b = 0; b < 2; ++b) {
     for (void* q : {(void*)wp.hin[b], (void*)wp.hout[b], (void*)wp.hchal[b], (void*)wp.hlens[b],
@@ -1551,19 +1589,20 @@ int gvs_create_sharded(const gvs_config* cfg, const uint8_t comm_id[GVS_COMM_ID_
   return create_common(cfg, kRccl, comm_id, out);
 }
 
+static int h2d(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes);
+static int d2h(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes);
+static int bounce_done(gvs_handle* h, int rc);
+
 int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_response* out) {
   if (!h || (!reqs && n) || (!out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(h->in_stage, reqs, (size_t)n * sizeof(gvs_request),
-                              hipMemcpyHostToDevice, h->stream));
+  h->bounce.pend.clear();
+  if (int r = h2d(h, 0, h->in_stage, reqs, (size_t)n * sizeof(gvs_request))) return r;
   if (int r = run_batch(h, h->in_stage, n, h->out_stage)) return r;
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * sizeof(gvs_response),
-                              hipMemcpyDeviceToHost, h->stream));
-  return finish(h);
+  if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * sizeof(gvs_response))) return r;
+  return bounce_done(h, finish(h));
 }
 
 // memcpy over up to 8 host threads (pinned staging of 64K-request batches:
@@ -1596,6 +1635,53 @@ static bool is_pinned(const void* p) {
     return false;
   }
   return at.type == hipMemoryTypeHost;
+}
+
+static int bounce_grow(gvs_handle* h, int slot, size_t bytes) {
+  Bounce& b = h->bounce;
+  if (b.cap[slot] >= bytes) return GVS_OK;
+  if (b.buf[slot]) GVS_HIP(h, hipHostFree(b.buf[slot]));
+  b.buf[slot] = nullptr;
+  b.cap[slot] = 0;
+  const size_t cap = std::max<size_t>(bytes, 1u << 20);
+  GVS_HIP(h, hipHostMalloc(&b.buf[slot], cap, hipHostMallocDefault));
+  b.cap[slot] = cap;
+  return GVS_OK;
+}
+
+// host -> device from caller memory `src`: pinned memory is copied from
+// directly, pageable memory through bounce slot `slot` (0..3)
+static int h2d(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return GVS_OK;
+  if (!is_pinned(src)) {
+    if (int r = bounce_grow(h, slot, bytes)) return r;
+    par_memcpy(h->bounce.buf[slot], src, bytes);
+    src = h->bounce.buf[slot];
+  }
+  GVS_HIP(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+  return GVS_OK;
+}
+
+// device -> host into caller memory `dst`: pageable memory through bounce
+// slot `slot` (4..7), handed over by bounce_done after the stream's sync
+static int d2h(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return GVS_OK;
+  if (is_pinned(dst)) {
+    GVS_HIP(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+    return GVS_OK;
+  }
+  if (int r = bounce_grow(h, slot, bytes)) return r;
+  GVS_HIP(h, hipMemcpyAsync(h->bounce.buf[slot], src, bytes, hipMemcpyDeviceToHost, h->stream));
+  h->bounce.pend.push_back(Bounce::Out{dst, slot, bytes});
+  return GVS_OK;
+}
+
+// after the call's stream sync (finish): the pageable outputs, on success
+static int bounce_done(gvs_handle* h, int rc) {
+  if (rc == GVS_OK)
+    for (const auto& o : h->bounce.pend) par_memcpy(o.dst, h->bounce.buf[o.slot], o.bytes);
+  h->bounce.pend.clear();
+  return rc;
 }
 
 int gvs_host_alloc(gvs_handle* h, size_t bytes, void** out) {
@@ -1681,9 +1767,16 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       GVS_HIP(h, hipStreamWaitEvent(s, p.h2d[b], 0));
       if (t >= 2) GVS_HIP(h, hipStreamWaitEvent(s, p.d2h[b], 0));  // dout[b] copied out
       snap[b] = save_state(h);
-      if (int r = run_batch(h, p.din[b], n, p.dout[b], false)) return r;
-      if (h->mode != kSingle)
-        if (int r = agree_errors(h)) return r;
+      int rr = run_batch(h, p.din[b], n, p.dout[b], false);
+      if (!rr && h->mode != kSingle) rr = agree_errors(h);
+      if (rr) {  // batch t was not (wholly) enqueued: the ones before it are still collected
+        restore_state(h, snap[b]);
+        stop = rr;
+        more = false;
+      }
+    }
+    if (more) {
+      const uint32_t b = t & 1u, n = counts[t];
       GVS_HIP(h, hipMemcpyAsync(&p.herr[b], &h->eng[0].scal->error, sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, s));
       GVS_HIP(h, hipEventRecord(p.done[b], s));
@@ -1718,6 +1811,12 @@ int gvs_process_batches(gvs_handle* h, const gvs_request* reqs, const uint32_t* 
       if (applied) *applied = t;
     }
     if (!more && t >= enq) break;
+  }
+  if (stop != GVS_OK) {  // the batches not applied answer nothing
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < k; ++i) total += counts[i];
+    GVS_HIP(h, hipStreamSynchronize(p.copy_out));
+    std::memset(out + next_off, 0, (size_t)(total - next_off) * sizeof(gvs_response));
   }
   return stop;
 }
@@ -1950,26 +2049,27 @@ int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
   GVS_HIP(h, hipSetDevice(h->device));
   if (int rc = wire_stage_init(h, true)) return rc;
   WireStage& w = h->wire;
-  hipStream_t s = h->stream;
+  h->bounce.pend.clear();
   if (n) {
-    GVS_HIP(h, hipMemcpyAsync(w.in, in, (size_t)n * in_stride, hipMemcpyHostToDevice, s));
-    GVS_HIP(h, hipMemcpyAsync(w.in_lens, in_lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    GVS_HIP(h, hipMemcpyAsync(w.times, times, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (int r = h2d(h, 0, w.in, in, (size_t)n * in_stride)) return r;
+    if (int r = h2d(h, 1, w.in_lens, in_lens, (size_t)n * 4)) return r;
+    if (int r = h2d(h, 2, w.times, times, (size_t)n * 8)) return r;
     if (challenges)
-      GVS_HIP(h, hipMemcpyAsync(w.chal, challenges, (size_t)n * 32, hipMemcpyHostToDevice, s));
+      if (int r = h2d(h, 3, w.chal, challenges, (size_t)n * 32)) return r;
   }
   if (int r = reset_errors(h)) return r;
   if (int r = wire_batch(h, w.in, in_stride, w.in_lens, n, w.times, challenges ? w.chal : nullptr,
                          w.out, out_stride, w.out_lens, w.sigs, w.status))
     return r;
   if (n) {
-    GVS_HIP(h, hipMemcpyAsync(out, w.out, (size_t)n * out_stride, hipMemcpyDeviceToHost, s));
-    GVS_HIP(h, hipMemcpyAsync(out_lens, w.out_lens, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    if (sigs) GVS_HIP(h, hipMemcpyAsync(sigs, w.sigs, (size_t)n * 64, hipMemcpyDeviceToHost, s));
+    if (int r = d2h(h, 4, out, w.out, (size_t)n * out_stride)) return r;
+    if (int r = d2h(h, 5, out_lens, w.out_lens, (size_t)n * 4)) return r;
+    if (sigs)
+      if (int r = d2h(h, 6, sigs, w.sigs, (size_t)n * 64)) return r;
     if (decode_status)
-      GVS_HIP(h, hipMemcpyAsync(decode_status, w.status, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+      if (int r = d2h(h, 7, decode_status, w.status, (size_t)n * 4)) return r;
   }
-  return finish(h);
+  return bounce_done(h, finish(h));
 }
 
 static int wire_pipe_init(gvs_handle* h) {
@@ -2144,29 +2244,28 @@ int gvs_sr25519_verify(gvs_handle* h, const uint8_t* pks, const uint8_t* msgs, u
   GVS_HIP(h, hipSetDevice(h->device));
   const size_t b_pk = (size_t)n * 32, b_msg = (size_t)n * msg_len, b_sig = (size_t)n * 64,
                b_ok = (size_t)n * 4;
-  uint8_t* d = nullptr;
-  GVS_HIP(h, hipMalloc((void**)&d, b_pk + b_msg + b_sig + b_ok + 64));
-  hipStream_t s = h->stream;
-  int rc = GVS_OK;
-  auto step = [&](hipError_t e) {
-    if (rc == GVS_OK && e != hipSuccess) {
-      h->err = hipGetErrorString(e);
-      rc = GVS_ERR_DEVICE;
-    }
-  };
-  step(hipMemcpyAsync(d, pks, b_pk, hipMemcpyHostToDevice, s));
-  if (b_msg) step(hipMemcpyAsync(d + b_pk, msgs, b_msg, hipMemcpyHostToDevice, s));
-  step(hipMemcpyAsync(d + b_pk + b_msg, sigs, b_sig, hipMemcpyHostToDevice, s));
-  uint32_t* d_ok = (uint32_t*)(d + ((b_pk + b_msg + b_sig + 3) & ~(size_t)3));
-  if (rc == GVS_OK)
-    rc = gvs_sr25519_verify_device(h, d, 32, d + b_pk, msg_len ? msg_len : 1, msg_len,
-                                   d + b_pk + b_msg, 64, n, context, context_len, d_ok);
-  if (rc == GVS_OK) {
-    step(hipMemcpyAsync(ok, d_ok, b_ok, hipMemcpyDeviceToHost, s));
-    step(hipStreamSynchronize(s));
+  const size_t need = b_pk + b_msg + b_sig + b_ok + 64;
+  // grow-only device staging: a hipMalloc / hipFree per call would change the
+  // page tables (and invalidate the TLB) between batches
+  if (h->sr_cap < need) {
+    if (h->sr_dev) GVS_HIP(h, hipFree(h->sr_dev));
+    h->sr_dev = nullptr;
+    h->sr_cap = 0;
+    GVS_HIP(h, hipMalloc((void**)&h->sr_dev, need));
+    h->sr_cap = need;
   }
-  (void)hipFree(d);
-  return rc;
+  uint8_t* d = h->sr_dev;
+  h->bounce.pend.clear();
+  if (int r = h2d(h, 0, d, pks, b_pk)) return r;
+  if (int r = h2d(h, 1, d + b_pk, msgs, b_msg)) return r;
+  if (int r = h2d(h, 2, d + b_pk + b_msg, sigs, b_sig)) return r;
+  uint32_t* d_ok = (uint32_t*)(d + ((b_pk + b_msg + b_sig + 3) & ~(size_t)3));
+  if (int r = gvs_sr25519_verify_device(h, d, 32, d + b_pk, msg_len ? msg_len : 1, msg_len,
+                                        d + b_pk + b_msg, 64, n, context, context_len, d_ok))
+    return bounce_done(h, r);
+  if (int r = d2h(h, 4, ok, d_ok, b_ok)) return r;
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return bounce_done(h, GVS_OK);
 }
 
 int gvs_set_expiry_cutoff(gvs_handle* h, uint64_t cutoff) {
@@ -2540,13 +2639,11 @@ int gvs_oram_access_batch(gvs_oram* o, const gvs_block_op* ops, uint32_t n, uint
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(h->in_stage, ops, (size_t)n * sizeof(gvs_block_op),
-                              hipMemcpyHostToDevice, h->stream));
+  h->bounce.pend.clear();
+  if (int r = h2d(h, 0, h->in_stage, ops, (size_t)n * sizeof(gvs_block_op))) return r;
   if (int r = oram_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * 1024, hipMemcpyDeviceToHost, h->stream));
-  return finish(h);
+  if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * 1024)) return r;
+  return bounce_done(h, finish(h));
 }
 
 int gvs_oram_access_batch_device(gvs_oram* o, const void* d_ops, uint32_t n, void* d_out) {
@@ -2597,14 +2694,11 @@ int gvs_omap_access_batch(gvs_omap* o, const gvs_omap_op* ops, uint32_t n, gvs_o
   gvs_handle* h = o->h;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   GVS_HIP(h, hipSetDevice(h->device));
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(h->in_stage, ops, (size_t)n * sizeof(gvs_omap_op), hipMemcpyHostToDevice,
-                              h->stream));
+  h->bounce.pend.clear();
+  if (int r = h2d(h, 0, h->in_stage, ops, (size_t)n * sizeof(gvs_omap_op))) return r;
   if (int r = omap_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
-  if (n)
-    GVS_HIP(h, hipMemcpyAsync(out, h->out_stage, (size_t)n * sizeof(gvs_omap_result), hipMemcpyDeviceToHost,
-                              h->stream));
-  return finish(h);
+  if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * sizeof(gvs_omap_result))) return r;
+  return bounce_done(h, finish(h));
 }
 
 int gvs_omap_access_batch_device(gvs_omap* o, const void* d_ops, uint32_t n, void* d_out) {

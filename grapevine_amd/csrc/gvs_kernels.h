@@ -468,7 +468,7 @@ struct MArgs {
   const uint4* m2tx;   // Q*cm group results (1152 B) for the write pass
   uint4* msnap;        // Q*cm x 1 KiB: the read pass's sink for unused group slots
   uint4* msnapp;       // B x 1 KiB: group snapshots at their heads' sorted positions
-  uint4* mdry;         // Q x 1 KiB: each workgroup's dry-run line
+  uint4* mdry;         // Q x 4 KiB: each workgroup's dry-run lines (gvs_mtx.h: one 1 KiB per use)
   uint32_t stamp, cm;
 };
 

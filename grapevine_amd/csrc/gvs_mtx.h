@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   // op of k_m1r_c reads line p (an address stream that does not depend on the
   // batch); unused slots write their own line of the MSNAP sink
   uint4* snap = a.msnap + (uint64_t)q * a.cm * 64;
-  uint4* dry = a.mdry + (uint64_t)q * 64;
+  uint4* dry = a.mdry + (uint64_t)q * 256;  // lines 0..63: the row loop's, 64..127: the slot loop's
   for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
     if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
     uint4 v[kMU];
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     if (has_row) continue;
     const bool real = !dry_run && k < ng;
     const uint4 hdr = sel4(real, make_uint4(0u, G.fl, G.flags, (uint32_t)G.slot), make_uint4(0, 0, 0, 0));
-    uint4* dst = dry_run ? dry : real ? a.msnapp + (uint64_t)G.head * 64 : snap + (uint64_t)k * 64;
+    uint4* dst = dry_run ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : snap + (uint64_t)k * 64;
     st_drop(dst, lane, sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
   }
 }
@@ -699,7 +699,9 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   if (tid == 0) atomicAdd(&s_delta, npend);
   __syncthreads();
   const uint4* res = a.m2tx + (uint64_t)q * a.cm * kVLineU4;
-  const uint4* dry = a.mdry + (uint64_t)q * 64;
+  // k_m1x wrote lines 0..127 of the workgroup's dry block; the row loop reads
+  // 128..191 and the slot loop 192..255 (no line is read twice in a kernel)
+  const uint4* dry = a.mdry + (uint64_t)q * 256 + 128;
   uint4* wst = AUTH ? st : s_wst[AUTH ? 0 : wave];
   for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
     if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   for (uint32_t k = wave; k <= a.cm; k += 4) {
     const bool dry_run = k == a.cm;
     if (!dry_run && s_ld[k]) continue;
-    uint4 x = ld_row<true>(dry_run ? &dry[lane] : &res[(uint64_t)k * kVLineU4 + 8 + lane]);
+    uint4 x = ld_row<true>(dry_run ? &dry[64 + lane] : &res[(uint64_t)k * kVLineU4 + 8 + lane]);
     keep4(x);
   }
   // every workgroup adds, zero included: a fixed set of atomics

@@ -264,7 +264,9 @@ struct R2Args {
   uint4* snapid;       // W*c x 128 B: the same for the identity lines
   uint4* snapp;        // B x 1 KiB: each touched row's snapshot at its first op's position
   uint4* snapidp;      // B x 128 B: its first line (identity), for k_rr1
-  uint4* dry;          // W x 1 KiB: each workgroup's dry-run line
+  uint4* dry;          // W x 4 KiB: each workgroup's dry-run lines, one 1 KiB per use
+                       // (merge read, snapshot write, identity write, side read): a line
+                       // touched twice in one kernel hits or misses L2 by the timing
   Scal* scal;
   uint32_t W, S, c;
   // authenticated storage (AUTH instantiations)
@@ -276,6 +278,7 @@ struct R2Args {
   uint64_t cutoff;
   uint4* xbuf;         // records written by this pass
   const uint4* xprev;  // records being deleted by this batch (exclusion)
+  uint32_t diag;       // diagnostic variants (test library only, GVS_DIAG bits 4, 8, 16)
 };
 
 // Expiry detection on a chunk (v1 x_detect plus the exclusion of rows whose
@@ -352,6 +355,7 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
   }
   mp = __builtin_amdgcn_readfirstlane(mp);
   ms = __builtin_amdgcn_readfirstlane(ms);
+  if (a.diag & 16u) mp = ms = 0u;  // diagnostic: no slot work inside the stream
   uint32_t mq = mp | (first ? (1u << U) : 0u);
   while (mq) {  // rows the previous batch changed: its final state
     const uint32_t low = mq & (0u - mq);
@@ -360,10 +364,10 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
     const uint32_t bit = dry_p ? 0u : low;
     const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
     const int16_t k = dry_p ? (int16_t)0 : s_pk[rj + u0];
-    const uint4* src = dry_p ? dry : a.ps + (sbase + (uint64_t)k) * 64;
+    const uint4* src = (dry_p || (a.diag & 12u)) ? dry : a.ps + (sbase + (uint64_t)k) * 64;
     const uint4 x = ld_row<true>(&src[lane]);
     if (AUTH) {  // the final state must be the one sealed for this row
-      const uint4 sd = uni4(dry_p ? dry[0] : a.psds[(sbase + (uint64_t)k) * 8]);
+      const uint4 sd = uni4(dry_p ? dry[3 * 64] : a.psds[(sbase + (uint64_t)k) * 8]);
       if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
     }
 #pragma unroll
@@ -383,9 +387,9 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
     // the snapshot goes to the position of the row's first op, so that
     // every op of the phase-C scans reads its own position's line
     const uint32_t hp = s_sh[(uint32_t)k & (kSlotMax - 1u)];
-    uint4* dst = dry_s ? dry : a.snapp + (uint64_t)hp * 64;
+    uint4* dst = dry_s ? dry + 64 : a.snapp + (uint64_t)hp * 64;
     st_drop(dst, lane, cur);
-    if (lane < 8) st_drop(dry_s ? dry : a.snapidp + (uint64_t)hp * 8, lane, cur);
+    if (lane < 8) st_drop(dry_s ? dry + 2 * 64 : a.snapidp + (uint64_t)hp * 8, lane, cur);
   }
   if (a.xon) xc = x_detect2<U>(a, v, s_xw_w, xc, s_xx, nx);
   return xc;
@@ -466,7 +470,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   const uint64_t rowbase = (uint64_t)w * a.S;
   uint4* part = a.table + rowbase * 64;
   uint4* sslot = a.snap + sbase * 64;
-  uint4* dry = a.dry + (uint64_t)w * 64;
+  uint4* dry = a.dry + (uint64_t)w * 256;
   const uint32_t tiles = a.S / kT;
   // FUSED: the lane's leaf key, and the chunk whose write tag is pending
   B2State lk{};
@@ -571,7 +575,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   }
   // unused slots (slots are dense from 0: [np, c) were not used by the
   // previous batch): every slot's final-state line is read once per pass
-  for (uint32_t k = np + wave; k < a.c; k += NW) {
+  for (uint32_t k = ((a.diag & 8u) ? 0u : (a.diag & 4u) ? a.c : np) + wave; k < a.c; k += NW) {
     uint4 x = ld_row<true>(&a.ps[(sbase + k) * 64 + lane]);
     if (AUTH) x = xor4(x, uni4(a.psds[(sbase + k) * 8]));  // as the side entry a used slot reads
     keep4(x);

@@ -55,7 +55,8 @@ def run(outdir, counters, mix, lib, args, timeout):
     cmd = (["rocprofv3", "--pmc"] + counters + ["-d", outdir, "-o", "run", "--output-format", "csv", "--",
                                                  sys.executable, PROBE, mix, "--fill-batches", "3",
                                                  "--seeds", SEEDS, "--batches", str(PER_SEED)] + args)
-    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    # the test library, as under pytest (tests/conftest.py): GVS_DIAG variants too
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"), GVS_TEST_HOOKS="1")
     if lib:
         env["GVS_LIB_OVERRIDE"] = os.path.join(ROOT, lib)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
@@ -76,6 +77,50 @@ def run(outdir, counters, mix, lib, args, timeout):
     first = ("k_wire_decode" if "k_wire_decode" in ks else "k_route_dest" if "k_route_dest" in ks else
              "k_bcopy" if "k_bcopy" in ks else "k_ocopy" if "k_ocopy" in ks else "k_copy")
     return split(vals, first)
+
+
+def check(res, counters, mixes):
+    """tests/test_oblivious.py's two checks per kernel and counter (the counter
+    in its own unit): noise from the prefill batches across the processes and
+    main against main#2; every measured batch within 3x range + FLOOR of main's
+    median, every mix's mean within 5 standard errors + BIAS_FLOOR of main's."""
+    import math
+    FLOOR, BIAS_FLOOR, SIG = 2.0, 0.25, 5.0
+    out = []
+    ref_b = res["main"]
+    n_pre = min(len(b) for b in res.values()) - N_MEAS
+    for c in counters:
+        bad = []
+        for idx, (k, _) in enumerate(ref_b[-1]):
+            val = lambda b: b[idx][1].get(c, float("nan"))
+            rng, ss, dof = 0.0, 0.0, 0
+            for i in range(1, n_pre):
+                v = [val(res[m][i]) for m in mixes]
+                rng = max(rng, max(v) - min(v))
+                ss += statistics.variance(v) * (len(v) - 1)
+                dof += len(v) - 1
+            if "main#2" in res:
+                for x, y in zip(res["main"][1:], res["main#2"][1:]):
+                    d = val(x) - val(y)
+                    rng = max(rng, abs(d))
+                    ss += d * d / 2.0
+                    dof += 1
+            sigma = math.sqrt(ss / dof) if dof else 0.0
+            tol = 3.0 * rng + FLOOR
+            main_meas = [val(b) for b in ref_b[-N_MEAS:]]
+            ref, mu = statistics.median(main_meas), statistics.fmean(main_meas)
+            btol = SIG * sigma * math.sqrt(2.0 / N_MEAS) + BIAS_FLOOR
+            for m in mixes:
+                meas = [val(b) for b in res[m][-N_MEAS:]]
+                dev = max(abs(v - ref) for v in meas)
+                bias = statistics.fmean(meas) - mu
+                if dev > tol:
+                    bad.append(f"{k}/{m}: batch {dev:.2f} > {tol:.2f}")
+                if m != "main" and abs(bias) > btol:
+                    bad.append(f"{k}/{m}: bias {bias:+.2f} > {btol:.2f}")
+        out.append(f"### check {c}: {len(bad)} violation(s)")
+        out += ["    " + b for b in bad]
+    return out
 
 
 def main():
@@ -111,6 +156,7 @@ def main():
                     v = meas(m)
                     cells.append(f"{m}:{statistics.fmean(v) - mm:+9.1f}[{min(v) - mm:+.0f},{max(v) - mm:+.0f}]")
                 lines.append(f"  {idx:2d} {k[:34]:34s} {mm:12.1f}  " + "  ".join(cells))
+        lines += check(res, counters, mixes)
     txt = "\n".join(lines) + "\n"
     with open(os.path.join(a.outdir, "table.txt"), "w") as f:
         f.write(txt)

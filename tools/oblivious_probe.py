@@ -29,8 +29,11 @@ wire_* mixes are the main mix with every signature forged, every message
 malformed, or every message in a non-canonical encoding.
 """
 import argparse
+import ctypes
 import os
 import sys
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -227,6 +230,9 @@ def main():
     p.add_argument("--auth", action="store_true", help="authenticated storage (DESIGN.md §8)")
     p.add_argument("--wire", action="store_true", help="wire path with challenge check")
     p.add_argument("--expiry", type=int, default=0, help="expiry records per batch (x_* mixes)")
+    p.add_argument("--pinned", action="store_true",
+                   help="requests and responses in pinned host memory (gvs_host_alloc) through "
+                        "gvs_process_batches: no pageable transfer between the batches' kernels")
     p.add_argument("--seed", type=int, default=1234, help="generator seed of the measured batches")
     p.add_argument("--seeds", default="",
                    help="comma-separated seeds: the measured batches are --batches per seed, the "
@@ -250,13 +256,26 @@ def main():
     model.seed(77)
     fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=a.identities)
     wp = WirePath(store, model, a.identities) if a.wire else None
+    if a.pinned:
+        pin_in, pin_out = store.host_array(n, abi.REQUEST_DTYPE), store.host_array(n, abi.RESPONSE_DTYPE)
+
+        def run(reqs):
+            # one batch through gvs_process_batches from pinned buffers
+            pin_in[:len(reqs)] = reqs
+            counts = np.array([len(reqs)], np.uint32)
+            applied = ctypes.c_uint32(0)
+            store._check(store.lib.gvs_process_batches(store.h, pin_in.ctypes.data, counts.ctypes.data, 1,
+                                                       pin_out.ctypes.data, ctypes.byref(applied)))
+            return pin_out[:len(reqs)].copy()
+    else:
+        run = store.process_batch
     for _ in range(a.fill_batches):
         reqs = model.gen_batch(n, fill)
         if wp:
             wp.run(reqs, "main")
             continue
         want = model.process_batch(reqs)
-        got = store.process_batch(reqs)
+        got = run(reqs)
         assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
     params = ffi.gen_params(n_identities=a.identities, bad_auth=0, bad_recipient=0, hard_error=0,
                             zero_recipient=0, **{"miss": 0, **MIXES[a.mix]})
@@ -273,7 +292,7 @@ def main():
             wp.run(reqs, a.mix)
             continue
         want = model.process_batch(reqs)
-        got = store.process_batch(reqs)
+        got = run(reqs)
         assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe"
     store.synchronize()
     print("probe ok", a.mix, store.stats()["messages"])
