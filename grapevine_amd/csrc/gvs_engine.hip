@@ -989,6 +989,9 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
       hipLaunchKernelGGL((k_rpass2<8, true, true, 1, true, 8>), dim3(e.W), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
+  } else if (e.c <= kStageSlots && e.S % (16 * 8) == 0 && !(a.diag & 1024u)) {
+    // the fixed-schedule pass: slot lines staged in LDS (gvs_txn.h k_rpass2s)
+    hipLaunchKernelGGL((k_rpass2s<16, 8>), dim3(e.W), dim3(512), 0, s, a);
   } else {
 #ifndef GVS_DIAG_RP_NTL
 #define GVS_DIAG_RP_NTL true  // diagnostic builds only: the plain pass's load / store policy

@@ -78,17 +78,22 @@ __host__ __device__ inline uint32_t route_dest_key(const RouteArgs& a, uint32_t 
   const uint64_t idw[2] = {u4lo(c0), u4hi(c0)};
   const uint64_t hid = siphash24_blocks(a.kc.hk0, a.kc.hk1, idw, 2, 3, 17);  // id || 0x03
   const uint32_t kh = (uint32_t)(lo >> 32) & ~3u, ki = (uint32_t)(hid >> 32) & ~3u;
-  if (hard) return spread;
-  if (type == 1u) {
-    key = rcpt_zero ? kKeyNone : kh | 1u;
-    return rcpt_zero ? spread : by_key;
-  }
-  if (next) {
-    key = kh | 2u;
-    return by_key;
-  }
-  key = ki | 3u;
-  return by_id != kNone ? by_id : spread;
+  // one selection for every kind (a branch per kind let the compiler sink the
+  // id decode and the id hash into the by-id path, whose code a batch without
+  // by-id ops then never fetched: FETCH_SIZE followed the mix)
+  const bool create = type == 1u;
+  const uint32_t d_cr = rcpt_zero ? spread : by_key;
+  const uint32_t d_id = by_id != kNone ? by_id : spread;
+  const uint32_t k_cr = rcpt_zero ? kKeyNone : (kh | 1u);
+  uint32_t d = d_id, k = ki | 3u;
+  d = next ? by_key : d;
+  k = next ? (kh | 2u) : k;
+  d = create ? d_cr : d;
+  k = create ? k_cr : k;
+  d = hard ? spread : d;
+  k = hard ? kKeyNone : k;
+  key = k;
+  return d;
 }
 
 __host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
@@ -100,7 +105,9 @@ __host__ __device__ inline uint32_t route_dest(const RouteArgs& a, uint32_t i) {
 __global__ __launch_bounds__(1024) void k_route_dest(RouteArgs a) {
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   uint32_t key;
-  a.dest[i] = route_dest_key(a, i, key);
+  uint32_t d = route_dest_key(a, i, key);
+  asm volatile("" : "+v"(d), "+v"(key));  // every request's selection computed in full
+  a.dest[i] = d;
   a.rkey[i] = ((uint64_t)key << 32) | i;
 }
 
@@ -232,7 +239,13 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
     // an overflowed batch (p == kNone) fails as a whole; out is then undefined
     v[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + lane] : make_uint4(0, 0, 0, 0);
     tw[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + 64] : make_uint4(0, 0, 0, 0);
-    const uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
+    uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
+    // pinned: only shed requests use ts and only the others the slot, and the
+    // compiler would otherwise load each under its condition (the time word's
+    // line was then read once per shed request: FETCH_SIZE followed the mix)
+    keep4(ts);
+    keep4(v[r]);
+    keep4(tw[r]);
     const bool s = shed[i] != 0u;
     v[r] = s ? (lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0)) : v[r];
     tw[r] = s ? make_uint4(8u, 0, 0, 0) : tw[r];

@@ -355,7 +355,9 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
   }
   mp = __builtin_amdgcn_readfirstlane(mp);
   ms = __builtin_amdgcn_readfirstlane(ms);
-  if (a.diag & 16u) mp = ms = 0u;  // diagnostic: no slot work inside the stream
+  if (a.diag & (16u | 128u)) mp = ms = 0u;  // diagnostic: no slot work inside the stream
+  if (a.diag & 256u) ms = 0u;                // diagnostic: no snapshot writes inside it
+  if (a.diag & 512u) mp = 0u;                // diagnostic: no final-state reads inside it
   uint32_t mq = mp | (first ? (1u << U) : 0u);
   while (mq) {  // rows the previous batch changed: its final state
     const uint32_t low = mq & (0u - mq);
@@ -367,7 +369,7 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
     const uint4* src = (dry_p || (a.diag & 12u)) ? dry : a.ps + (sbase + (uint64_t)k) * 64;
     const uint4 x = ld_row<true>(&src[lane]);
     if (AUTH) {  // the final state must be the one sealed for this row
-      const uint4 sd = uni4(dry_p ? dry[3 * 64] : a.psds[(sbase + (uint64_t)k) * 8]);
+      const uint4 sd = uni4(shfl4(line_load(dry_p ? dry + 3 * 64 : a.psds + (sbase + (uint64_t)k) * 8), 0));
       if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
     }
 #pragma unroll
@@ -440,28 +442,37 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
     s_xt = 0;
   }
   __syncthreads();
-  // every slot descriptor of this partition, both batches (fixed reads)
+  // every slot descriptor of this partition, both batches (fixed reads): a
+  // record by 8 lanes, one whole line per load instruction (c is a multiple
+  // of 8).  A 16-B load per record fetched each line as a partial request,
+  // and how often the memory side merged those into whole-line reads
+  // (TCC_BUBBLE, counted twice in FETCH_SIZE) followed the timing.
   const uint64_t sbase = (uint64_t)w * a.c;
-  for (uint32_t k = tid; k < a.c; k += kT) {
-    const uint4 dp = a.tprev[(sbase + k) * 8];
-    const uint4 ds = a.tcur[(sbase + k) * 8];
-    if (dp.y == a.stamp_prev && dp.x < a.S) {
-      s_pk[dp.x] = (int16_t)k;
-      atomicAdd(&s_np, 1u);
-    }
-    s_sh[k] = ds.w;
-    if (ds.y == a.stamp_cur && ds.x < a.S) {
-      s_sk[ds.x] = (int16_t)k;
-      atomicAdd(&s_ns, 1u);
+  for (uint32_t k0 = wave * 8; k0 < a.c; k0 += NW * 8) {
+    const uint32_t k = k0 + (lane >> 3);
+    const uint4 xp = a.tprev[(sbase + k) * 8 + (lane & 7u)];
+    const uint4 xc = a.tcur[(sbase + k) * 8 + (lane & 7u)];
+    const uint4 dp = shfl4(xp, (int)(lane & ~7u)), ds = shfl4(xc, (int)(lane & ~7u));
+    if ((lane & 7u) == 0u) {
+      if (dp.y == a.stamp_prev && dp.x < a.S) {
+        s_pk[dp.x] = (int16_t)k;
+        atomicAdd(&s_np, 1u);
+      }
+      s_sh[k] = ds.w;
+      if (ds.y == a.stamp_cur && ds.x < a.S) {
+        s_sk[ds.x] = (int16_t)k;
+        atomicAdd(&s_ns, 1u);
+      }
     }
   }
   // the expiry deletes this batch already carries for this partition
   uint32_t nx = 0;
   if (a.xon && a.xexcl) {
-    if (tid < a.xep) {
-      const uint4 r = a.xprev[((uint64_t)w * a.xep + tid) * 8];
-      const uint4 vld = a.xprev[((uint64_t)w * a.xep + tid) * 8 + 3];
-      s_xx[tid] = sel4(vld.x != 0u, r, make_uint4(0, 0, 0, 0));
+    if (wave == 0) {  // the records as whole lines (8 lanes each), words 0 and 3 by shuffles
+      const uint32_t kr = lane >> 3;
+      const uint4 x = kr < a.xep ? a.xprev[((uint64_t)w * a.xep + kr) * 8 + (lane & 7u)] : make_uint4(0, 0, 0, 0);
+      const uint4 r = shfl4(x, (int)(lane & ~7u)), vld = shfl4(x, (int)((lane & ~7u) + 3u));
+      if ((lane & 7u) == 0u && kr < a.xep) s_xx[kr] = sel4(vld.x != 0u, r, make_uint4(0, 0, 0, 0));
     }
     nx = a.xep;
   }
@@ -575,14 +586,189 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   }
   // unused slots (slots are dense from 0: [np, c) were not used by the
   // previous batch): every slot's final-state line is read once per pass
-  for (uint32_t k = ((a.diag & 8u) ? 0u : (a.diag & 4u) ? a.c : np) + wave; k < a.c; k += NW) {
+  for (uint32_t k = ((a.diag & (8u | 128u | 512u)) ? 0u : (a.diag & 4u) ? a.c : np) + wave; k < a.c; k += NW) {
     uint4 x = ld_row<true>(&a.ps[(sbase + k) * 64 + lane]);
-    if (AUTH) x = xor4(x, uni4(a.psds[(sbase + k) * 8]));  // as the side entry a used slot reads
+    if (AUTH) x = xor4(x, uni4(shfl4(line_load(a.psds + (sbase + k) * 8), 0)));  // as a used slot's read
     keep4(x);
   }
-  for (uint32_t k = ns + wave; k < a.c; k += NW) {
+  for (uint32_t k = ((a.diag & (128u | 256u)) ? 0u : ns) + wave; k < a.c; k += NW) {
     st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
     if (lane < 8) st_drop(a.snapid, (sbase + k) * 8 + lane, make_uint4(0, 0, 0, 0));
+  }
+  if (a.xon && w % a.xk == a.xrot) {
+    __syncthreads();
+    if (wave == 0 && lane < 8 * a.xep) {
+      const uint32_t k = lane >> 3, part8 = lane & 7;
+      const bool valid = k < s_xt;
+      uint4 val = make_uint4(part8 == 3 && valid ? 1u : 0u, 0, 0, 0);
+      if (part8 < 3) val = sel4(valid, s_xp[k * 3 + part8], make_uint4(0, 0, 0, 0));
+      a.xbuf[((uint64_t)(w / a.xk) * a.xep + k) * 8 + part8] = val;
+    }
+  }
+}
+
+// --------------------------------------------------------- k_rpass2s
+//
+// The plain table pass with a fixed memory schedule.  k_rpass2 reads a used
+// slot's final state and writes a touched row's snapshot in the row stream,
+// at the position of the row, so where those 1-KiB accesses fall among the
+// row loads and stores followed the batch.  The memory side's request timing
+// followed it too: FETCH_SIZE counts 128-B reads that arrived with a gap
+// (TCC_BUBBLE) twice, and their number moved with the request mix by 3-6 K per
+// launch (2^20 rows, profiles/r04_*).  Here a workgroup
+//   (1) reads every slot's final state (c lines, used or not) into LDS,
+//   (2) streams its rows: merges and snapshots go through LDS only,
+//   (3) writes every slot's snapshot (c lines; unused slots to their sink),
+// so the order and number of its HBM accesses depend on (S, c) only.  Up to
+// kStageSlots slots (2 x 65 KiB of LDS: one workgroup of NW waves per CU).
+constexpr uint32_t kStageSlots = 64;
+
+template <int U>
+__device__ inline uint32_t stage_chunk(const R2Args& a, uint4 (&v)[U], uint32_t rj, bool first,
+                                       const int16_t* s_pk, const int16_t* s_sk, const uint4* s_fin,
+                                       uint4* s_snp, uint32_t xc, uint4* s_xw_w, const uint4* s_xx,
+                                       uint32_t nx) {
+  const uint32_t lane = lane_id();
+  uint32_t mp = 0, ms = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    mp |= s_pk[rj + u] >= 0 ? (1u << u) : 0u;
+    ms |= s_sk[rj + u] >= 0 ? (1u << u) : 0u;
+  }
+  mp = __builtin_amdgcn_readfirstlane(mp);
+  ms = __builtin_amdgcn_readfirstlane(ms);
+  // the dry iteration (an extra mask bit, taken last) uses LDS slot kStageSlots
+  uint32_t mq = mp | (first ? (1u << U) : 0u);
+  while (mq) {  // rows the previous batch changed: their final state
+    const uint32_t low = mq & (0u - mq);
+    mq &= mq - 1u;
+    const bool dry_p = low == (1u << U);
+    const uint32_t bit = dry_p ? 0u : low;
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+    const uint32_t k = dry_p ? kStageSlots : (uint32_t)s_pk[rj + u0];
+    const uint4 x = s_fin[k * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
+  }
+  uint32_t sq = ms | (first ? (1u << U) : 0u);
+  while (sq) {  // rows this batch touches: their snapshot
+    const uint32_t low = sq & (0u - sq);
+    sq &= sq - 1u;
+    const bool dry_s = low == (1u << U);
+    const uint32_t bit = dry_s ? 0u : low;
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+    const uint32_t k = dry_s ? kStageSlots : (uint32_t)s_sk[rj + u0];
+    uint4 cur = v[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
+    s_snp[k * 64 + lane] = cur;
+  }
+  if (a.xon) xc = x_detect2<U>(a, v, s_xw_w, xc, s_xx, nx);
+  return xc;
+}
+
+// NW waves, chunks of U rows dealt round-robin (round r: wave w streams rows
+// (r NW + w) U ..): S must be a multiple of U NW, c at most kStageSlots.
+template <int U, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_rpass2s(R2Args a) {
+  constexpr uint32_t kR = (uint32_t)U * NW;           // rows per round
+  constexpr uint32_t kPer = kStageSlots / NW;          // slot lines per wave
+  __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
+  __shared__ uint32_t s_sh[kStageSlots];
+  __shared__ uint32_t s_np, s_ns, s_xt;
+  __shared__ uint4 s_fin[(kStageSlots + 1) * 64];      // final states by slot (+ the dry slot)
+  __shared__ uint4 s_snp[(kStageSlots + 1) * 64];      // snapshots by slot (+ the dry slot)
+  __shared__ uint4 s_xw[NW * (kXepMax + 1) * 3];
+  __shared__ uint4 s_xp[kXepMax * 3];
+  __shared__ uint4 s_xx[kXepMax];
+  __shared__ uint32_t s_xc[NW];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t w = blockIdx.x;
+  if (a.scal->error) return;
+  const uint64_t sbase = (uint64_t)w * a.c;
+  // (1) every slot's final-state line, the wave's kPer loads in flight together
+  uint4 fin[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t k = wave + NW * i;
+    fin[i] = k < a.c ? ld_row<true>(&a.ps[(sbase + k) * 64 + lane]) : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t o = tid; o < a.S; o += 64 * NW) {
+    s_pk[o] = -1;
+    s_sk[o] = -1;
+  }
+  if (tid == 0) {
+    s_np = 0;
+    s_ns = 0;
+    s_xt = 0;
+  }
+  __syncthreads();
+  // slot descriptors of both batches, whole lines (k_rpass2)
+  for (uint32_t k0 = wave * 8; k0 < a.c; k0 += NW * 8) {
+    const uint32_t k = k0 + (lane >> 3);
+    const uint4 xp = a.tprev[(sbase + k) * 8 + (lane & 7u)];
+    const uint4 xc = a.tcur[(sbase + k) * 8 + (lane & 7u)];
+    const uint4 dp = shfl4(xp, (int)(lane & ~7u)), ds = shfl4(xc, (int)(lane & ~7u));
+    if ((lane & 7u) == 0u) {
+      if (dp.y == a.stamp_prev && dp.x < a.S) {
+        s_pk[dp.x] = (int16_t)k;
+        atomicAdd(&s_np, 1u);
+      }
+      s_sh[k] = ds.w;
+      if (ds.y == a.stamp_cur && ds.x < a.S) {
+        s_sk[ds.x] = (int16_t)k;
+        atomicAdd(&s_ns, 1u);
+      }
+    }
+  }
+  uint32_t nx = 0;
+  if (a.xon && a.xexcl) {
+    if (wave == 0) {
+      const uint32_t kr = lane >> 3;
+      const uint4 x = kr < a.xep ? a.xprev[((uint64_t)w * a.xep + kr) * 8 + (lane & 7u)] : make_uint4(0, 0, 0, 0);
+      const uint4 r = shfl4(x, (int)(lane & ~7u)), vld = shfl4(x, (int)((lane & ~7u) + 3u));
+      if ((lane & 7u) == 0u && kr < a.xep) s_xx[kr] = sel4(vld.x != 0u, r, make_uint4(0, 0, 0, 0));
+    }
+    nx = a.xep;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t k = wave + NW * i;
+    if (k < a.c) s_fin[k * 64 + lane] = fin[i];
+  }
+  __syncthreads();
+  const uint32_t ns = s_ns;
+  // (2) the rows
+  uint4* part = a.table + (uint64_t)w * a.S * 64;
+  const uint32_t rounds = a.S / kR;
+  for (uint32_t t = 0; t < rounds; ++t) {
+    const uint32_t rj = t * kR + wave * U;
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld_row<true>(&part[(uint64_t)(rj + u) * 64 + lane]);
+    const bool first = t == 0 && wave == 0;
+    const uint32_t xc = stage_chunk<U>(a, v, rj, first, s_pk, s_sk, s_fin, s_snp, 0u,
+                                       s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st_row<true>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
+    if (lane == 0) s_xc[wave] = xc;
+    __syncthreads();
+    if (a.xon) {
+      const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
+      __syncthreads();
+      if (tid == 0) s_xt = tot;
+    }
+  }
+  __syncthreads();
+  // (3) every slot's snapshot: the touched rows' to their first ops'
+  // positions, the unused slots' (zero) to their sink lines
+  uint4* sslot = a.snap + sbase * 64;
+  for (uint32_t k = wave; k < a.c; k += NW) {
+    const bool used = k < ns;
+    const uint32_t hp = s_sh[k];
+    const uint4 x = sel4(used, s_snp[k * 64 + lane], make_uint4(0, 0, 0, 0));
+    st_drop(used ? a.snapp + (uint64_t)hp * 64 : sslot + (uint64_t)k * 64, lane, x);
+    if (lane < 8) st_drop(used ? a.snapidp + (uint64_t)hp * 8 : a.snapid + (sbase + k) * 8, lane, x);
   }
   if (a.xon && w % a.xk == a.xrot) {
     __syncthreads();
