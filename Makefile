@@ -2,7 +2,9 @@
 # test hooks of include/gvstore_test.h, and the CPU oracle (tests only).
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+# bitwise & and | on bools are deliberate in the kernels: no short-circuit
+# branches that skip code by the data (DESIGN.md §3 rule 6)
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-bitwise-instead-of-logical
 
 LIB := grapevine_amd/libgvstore.so
 TESTLIB := grapevine_amd/libgvstore_test.so

@@ -62,6 +62,22 @@ __device__ inline void st_drop(const void* base, uint64_t i, uint4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(i * 16u), 0, 16 /* sc1 */);
 }
 
+// 16-B streaming store of a table or mailbox row (buffer_store ... nt sc1:
+// non-temporal and written through).  The row passes store every row of the
+// table whatever the batch; with plain non-temporal stores the number of
+// 64-B HBM write requests (TCC_EA0_WRREQ) moved by thousands per 2^20-row
+// pass with the timing of the batch's slot traffic, and the reads around them
+// picked up DRAM bubbles (TCC_BUBBLE); written through, both are fixed
+// (profiles/r04d_store_policy.txt) and the pass runs 3% faster.  Same
+// contract as st_drop: `base` wave-uniform, 16 * i below 2^32.
+__device__ inline void st_stream(const void* base, uint64_t i, uint4 x) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v v = {x.x, x.y, x.z, x.w};
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(i * 16u), 0, 2 /* nt */ | 16 /* sc1 */);
+}
+
 // a whole 128-B record of one thread (8 such stores)
 template <class T>
 __device__ inline void st_drop_rec(T* base, uint64_t i, const T& rec) {
@@ -252,6 +268,34 @@ __host__ __device__ inline uint64_t r_key(uint64_t row, uint32_t cls, uint32_t s
 // ------------------------------------------------------------- wave helpers
 
 __device__ inline uint32_t lane_id() { return threadIdx.x & 63u; }
+// order the wave's LDS stores before its later LDS loads (and vice versa)
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Eight 1040-B records (the caller's gvs_request / gvs_response layout) of one
+// wave to `out` (= the first record; i0 a multiple of 8, so the 8320 B are 65
+// whole 128-B lines): record r's 1 KiB in v[r], lane r < 8 holds record r's
+// 16-B tail word.  Staged in the wave's LDS (`st`, 520 x 16 B) and written
+// line by line, each line by one store instruction and written through
+// (st_stream): records written one by one left the line two records share to
+// two instructions, and its partial write-backs moved WRITE_SIZE with the
+// timing.  Records >= nrec are not written.
+__device__ inline void wave_put_rec8(uint4* out, uint4* st, const uint4 (&v)[8], uint4 tail, uint32_t nrec) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (uint32_t r = 0; r < 8; ++r) st[r * 65 + lane] = v[r];
+  if (lane < 8) st[lane * 65 + 64] = tail;
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t j = 0; j < 9; ++j) {
+    const uint32_t o = j * 64 + lane;
+    if (o < 520 && o / 65 < nrec) st_stream(out, o, st[o]);
+  }
+  wave_lds_sync();
+}
 
 __device__ inline uint32_t mbcnt64(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -267,8 +311,10 @@ __device__ inline uint4 shfl4(uint4 v, int src) {
   return r;
 }
 
+// bitwise, not &&: a short-circuit chain may compile to exec-mask branches
+// that skip code by the data (instruction fetch shows in FETCH_SIZE)
 __device__ inline bool eq4(uint4 a, uint4 b) {
-  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+  return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) == 0u;
 }
 __host__ __device__ inline bool nz4(uint4 a) { return (a.x | a.y | a.z | a.w) != 0u; }
 

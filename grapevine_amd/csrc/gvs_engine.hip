@@ -263,6 +263,7 @@ struct gvs_handle {
   Bounce bounce;
   uint8_t* sr_dev = nullptr;  // gvs_sr25519_verify's device staging (grow-only)
   size_t sr_cap = 0;
+  uint32_t* err_pin = nullptr;  // finish(): the error word's pinned landing place
   std::vector<void*> allocs;
   std::string err;
 };
@@ -826,6 +827,10 @@ static AllocArgs aargs(const Engine& e) {
 
 // Diagnostic kernel variants (GVS_DIAG bits; honoured by the test library only,
 // results are then wrong by design: tools/gpu_pmc_mix.sh attribution runs).
+#ifndef GVS_DIAG_RP_NTL
+#define GVS_DIAG_RP_NTL true  // diagnostic builds only: the plain pass's load / store policy
+#define GVS_DIAG_RP_NTS true
+#endif
 #ifdef GVS_TEST_HOOKS
 static uint32_t diag_bits() {
   static const uint32_t d = [] {
@@ -991,12 +996,8 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
       hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
   } else if (e.c <= kStageSlots && e.S % (16 * 8) == 0 && !(a.diag & 1024u)) {
     // the fixed-schedule pass: slot lines staged in LDS (gvs_txn.h k_rpass2s)
-    hipLaunchKernelGGL((k_rpass2s<16, 8>), dim3(e.W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_rpass2s<16, 8, GVS_DIAG_RP_NTL>), dim3(e.W), dim3(512), 0, s, a);
   } else {
-#ifndef GVS_DIAG_RP_NTL
-#define GVS_DIAG_RP_NTL true  // diagnostic builds only: the plain pass's load / store policy
-#define GVS_DIAG_RP_NTS true
-#endif
     hipLaunchKernelGGL((k_rpass2<16, GVS_DIAG_RP_NTL, GVS_DIAG_RP_NTS, 2>), dim3(e.W), dim3(256), 0, s, a);
     if (a.diag & 32u)  // diagnostic: the pass again on the same inputs (results wrong)
       hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
@@ -1281,11 +1282,13 @@ static void advance(gvs_handle* h) {
 static int finish(gvs_handle* h) {
   if (h->mode != kSingle)
     if (int r = agree_errors(h)) return r;  // late flags (M2) too: same verdict on every shard
-  uint32_t e = 0;
-  GVS_HIP(h, hipMemcpyAsync(&e, &h->eng[0].scal->error, sizeof e, hipMemcpyDeviceToHost,
+  // read back into pinned memory: a copy to the stack goes through the
+  // runtime's pageable path (bounce buffers above)
+  if (!h->err_pin) GVS_HIP(h, hipHostMalloc((void**)&h->err_pin, sizeof(uint32_t), hipHostMallocDefault));
+  GVS_HIP(h, hipMemcpyAsync(h->err_pin, &h->eng[0].scal->error, sizeof(uint32_t), hipMemcpyDeviceToHost,
                             h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
-  if (int r = decode_error(h, e)) return r;
+  if (int r = decode_error(h, *h->err_pin)) return r;
   advance(h);
   return GVS_OK;
 }
@@ -1555,6 +1558,7 @@ int gvs_destroy(gvs_handle* h) {
   for (void* q : h->bounce.buf)
     if (q) (void)hipHostFree(q);
   if (h->sr_dev) (void)hipFree(h->sr_dev);
+  if (h->err_pin) (void)hipHostFree(h->err_pin);
   WirePipe& wp = h->wpipe;
   for (int b = 0; b < 2; ++b) {
     for (void* q : {(void*)wp.hin[b], (void*)wp.hout[b], (void*)wp.hchal[b], (void*)wp.hlens[b],

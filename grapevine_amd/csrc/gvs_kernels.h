@@ -290,16 +290,38 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
   constexpr uint32_t R = kCopyPerWave;
   const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const uint32_t lane = lane_id();
+  __shared__ uint4 s_rec[4][R * 65];
   if (i0 >= B) return;
   uint4 v[R];
+  uint32_t t;
+  const uint32_t live = min(n, xbase);
+  if (stride == 65) {
+    // 1040-B records: the wave's R = 8 of them are 65 whole 128-B lines
+    // (aligned: i0 is a multiple of 8), read once each, line by line, and
+    // handed out through LDS.  Record by record, the line two records share
+    // was requested twice, and whether the second request found it in L2
+    // followed the timing (FETCH_SIZE noise of ~50 KiB per batch).
+    uint4* st = s_rec[threadIdx.x >> 6];
+    const uint4* base = in + (uint64_t)i0 * 65;
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {  // wave-uniform conditions
-    const uint32_t i = i0 + r;
-    v[r] = (i < n && i < xbase) ? in[(uint64_t)i * stride + lane] : make_uint4(0, 0, 0, 0);
+    for (uint32_t j = 0; j < (R * 65 + 63) / 64; ++j) {
+      const uint32_t o = j * 64 + lane;
+      if (o < R * 65) st[o] = (i0 + o / 65 < live) ? base[o] : make_uint4(0, 0, 0, 0);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) v[r] = st[r * 65 + lane];
+    t = lane < R ? st[min(lane, R - 1u) * 65 + 64].x : 0u;
+  } else {  // whole-line records (routed slots: 72 x 16 B)
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {  // wave-uniform conditions
+      const uint32_t i = i0 + r;
+      v[r] = i < live ? in[(uint64_t)i * stride + lane] : make_uint4(0, 0, 0, 0);
+    }
+    // type words: lane r < R holds request i0 + r's
+    const uint32_t ti = i0 + min(lane, R - 1u);
+    t = (lane < R && ti < live) ? in[(uint64_t)ti * stride + 64].x : 0u;
   }
-  // type words: lane r < R holds request i0 + r's
-  const uint32_t ti = i0 + min(lane, R - 1u);
-  uint32_t t = (lane < R && ti < n && ti < xbase) ? in[(uint64_t)ti * stride + 64].x : 0u;
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = i0 + r;
@@ -802,10 +824,12 @@ __device__ inline void block_flag_scan(const uint8_t* flag, uint32_t n, uint16_t
 // ------------------------------------------------------------------ k_out
 
 // internal response slots (kRespSlot B, whole lines) -> caller layout (1040 B),
-// kCopyPerWave responses per wave
+// kCopyPerWave responses per wave, written as whole lines (wave_put_rec8)
 __global__ __launch_bounds__(256) void k_out(const uint4* __restrict__ resp, uint32_t n,
                                              uint4* __restrict__ out) {
   constexpr uint32_t R = kCopyPerWave;
+  static_assert(R == 8, "wave_put_rec8");
+  __shared__ uint4 s_rec[4][R * 65];
   const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   const uint32_t lane = lane_id();
   if (i0 >= n) return;
@@ -815,10 +839,7 @@ __global__ __launch_bounds__(256) void k_out(const uint4* __restrict__ resp, uin
     v[r] = i0 + r < n ? resp[(uint64_t)(i0 + r) * (kRespSlot / 16) + lane] : make_uint4(0, 0, 0, 0);
   const uint32_t si = i0 + min(lane, R - 1u);
   const uint4 st = (lane < R && si < n) ? resp[(uint64_t)si * (kRespSlot / 16) + 64] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r)
-    if (i0 + r < n) out[(uint64_t)(i0 + r) * 65 + lane] = v[r];
-  if (lane < R && si < n && i0 + lane < n) out[(uint64_t)si * 65 + 64] = st;
+  wave_put_rec8(out + (uint64_t)i0 * 65, s_rec[threadIdx.x >> 6], v, st, n - i0);
 }
 
 }  // namespace gvs

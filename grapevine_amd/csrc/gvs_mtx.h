@@ -780,7 +780,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < kMU; ++u) {
-      if (j0 + u < a.Sr) st_row<true>(&part[(uint64_t)(j0 + u) * 64 + lane], v[u]);
+      if (j0 + u < a.Sr) st_stream(part, (uint64_t)(j0 + u) * 64 + lane, v[u]);
       va[u] = vb[u];
     }
   }

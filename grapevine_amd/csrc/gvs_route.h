@@ -217,9 +217,7 @@ __global__ __launch_bounds__(256) void k_route_fill(RouteArgs a) {
 
 // the responses (slot layout) back to the caller layout, kGatherPerWave
 // requests per wave: 8 rows of 1040 B are 65 whole lines, so every output line
-// is written by one wave (one wave per request left the line two requests
-// share to two waves, whose partial write-backs moved WRITE_SIZE with the
-// timing).  A shed request's response is INTERNAL_ERROR with the request's
+// is written by one wave, and by one store instruction (wave_put_rec8).  A shed request's response is INTERNAL_ERROR with the request's
 // time: its shard's hard-error response and its request's time word are read
 // for every request and selected, so every request reads the same lines.
 constexpr uint32_t kGatherPerWave = 8;
@@ -229,6 +227,8 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
                                                       const uint4* __restrict__ back, uint32_t n,
                                                       uint4* __restrict__ out) {
   constexpr uint32_t R = kGatherPerWave;
+  static_assert(R == 8, "wave_put_rec8");
+  __shared__ uint4 s_rec[4][R * kAbiU4];
   const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R, lane = lane_id();
   if (i0 >= n) return;
   uint4 v[R], tw[R];
@@ -250,14 +250,11 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
     v[r] = s ? (lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0)) : v[r];
     tw[r] = s ? make_uint4(8u, 0, 0, 0) : tw[r];
   }
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r)
-    if (i0 + r < n) out[(uint64_t)(i0 + r) * kAbiU4 + lane] = v[r];
-  // the status words: lane r writes request r's
+  // the status words: lane r holds request r's
   uint4 t = tw[0];
 #pragma unroll
   for (uint32_t r = 1; r < R; ++r) t = lane == r ? tw[r] : t;
-  if (lane < R && i0 + lane < n) out[(uint64_t)(i0 + lane) * kAbiU4 + 64] = t;
+  wave_put_rec8(out + (uint64_t)i0 * kAbiU4, s_rec[threadIdx.x >> 6], v, t, n - i0);
 }
 
 // single-process shards: OR of every shard's error word into each of them

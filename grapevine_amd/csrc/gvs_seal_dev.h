@@ -25,12 +25,6 @@ __device__ inline uint32_t stage_slot(int u, uint32_t lane) {
   return ((uint32_t)u * 4 + (lane >> 4)) * kSegU4 + (lane & 15);
 }
 
-// order the wave's LDS stores before its later LDS loads (and vice versa)
-__device__ inline void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // The AES table lives in LDS as 64 interleaved replicas: entry x of replica
 // r at byte x * 256 + 4 r.  Lane l reads replica l, so the 32 lanes of a

@@ -561,7 +561,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) st_row<NTS>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
+      for (int u = 0; u < U; ++u) {
+        if (NTS) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
+        else st_row<false>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
+      }
     }
     // The waves meet after every tile, expiry or not: without the barrier they
     // drift apart and the plain pass runs 4-5% slower.  A barrier after every
@@ -669,7 +672,7 @@ __device__ inline uint32_t stage_chunk(const R2Args& a, uint4 (&v)[U], uint32_t 
 
 // NW waves, chunks of U rows dealt round-robin (round r: wave w streams rows
 // (r NW + w) U ..): S must be a multiple of U NW, c at most kStageSlots.
-template <int U, int NW>
+template <int U, int NW, bool NTL = true>
 __global__ __launch_bounds__(64 * NW, 1) void k_rpass2s(R2Args a) {
   constexpr uint32_t kR = (uint32_t)U * NW;           // rows per round
   constexpr uint32_t kPer = kStageSlots / NW;          // slot lines per wave
@@ -745,12 +748,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_rpass2s(R2Args a) {
     const uint32_t rj = t * kR + wave * U;
     uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld_row<true>(&part[(uint64_t)(rj + u) * 64 + lane]);
+    for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rj + u) * 64 + lane]);
     const bool first = t == 0 && wave == 0;
     const uint32_t xc = stage_chunk<U>(a, v, rj, first, s_pk, s_sk, s_fin, s_snp, 0u,
                                        s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
 #pragma unroll
-    for (int u = 0; u < U; ++u) st_row<true>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
+    for (int u = 0; u < U; ++u) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
     if (lane == 0) s_xc[wave] = xc;
     __syncthreads();
     if (a.xon) {
@@ -983,7 +986,7 @@ struct Rr1Op {
     const bool r0_exists = nz4(in.r0[0]);
     const uint4 rid = g[1];
     // the pop of a next-message DELETE succeeds on a row that holds its id
-    const bool nd_ok = in.nd_valid && r0_exists && eq4(in.nd, in.r0[0]);
+    const bool nd_ok = (in.nd_valid != 0u) & r0_exists & eq4(in.nd, in.r0[0]);
     const bool is_next = kind == KIND_NEXT_READ || kind == KIND_NEXT_DEL;
     const bool is_create = kind == KIND_CREATE;
     // Every case is computed and the op's own one selected (no branch over op
@@ -993,23 +996,23 @@ struct Rr1Op {
     const bool c_next = !null && is_next, c_cr = !null && !is_next && is_create;
     const bool c_byid = !null && !is_next && !is_create;
     // next: M1 resolved it to this row, which must hold that id
-    const uint32_t st_next = (r0_exists && eq4(in.r0[0], rid)) ? 1u : 8u;
+    const uint32_t st_next = (r0_exists & eq4(in.r0[0], rid)) ? 1u : 8u;
     const uint32_t sk_next = (kind == KIND_NEXT_DEL && st_next == 1u) ? kSetZero : kSetNone;
     // create: the allocator hands out free rows, empty after the pops
-    const uint32_t st_cr = (r0_exists && !nd_ok) ? 8u : 1u;
+    const uint32_t st_cr = (r0_exists & !nd_ok) ? 8u : 1u;
     const uint32_t sk_cr = st_cr == 1u ? kSetRec : kSetNone;
     // by-id READ / UPDATE / DELETE: the row as the creates and pops of this
     // batch left it (class order: pops, creates, then these)
-    const bool cr_ok = in.cr_valid && !(r0_exists && !nd_ok);
+    const bool cr_ok = (in.cr_valid != 0u) & !(r0_exists & !nd_ok);
     uint4 idb[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) idb[i] = sel4(cr_ok, in.cr[i], sel4(nd_ok, make_uint4(0, 0, 0, 0), in.r0[i]));
     const bool exists1 = nz4(idb[0]);
-    const bool cand = exists1 && eq4(qid, idb[0]) &&
-                      ((eq4(q1, idb[1]) && eq4(q2, idb[2])) || (eq4(q1, idb[3]) && eq4(q2, idb[4])));
-    const bool rcpt_ok = eq4(q3, idb[3]) && eq4(q4, idb[4]);
+    const bool cand = exists1 & eq4(qid, idb[0]) &
+                      ((eq4(q1, idb[1]) & eq4(q2, idb[2])) | (eq4(q1, idb[3]) & eq4(q2, idb[4])));
+    const bool rcpt_ok = eq4(q3, idb[3]) & eq4(q4, idb[4]);
     const bool expiry = seq >= a.xbase;
-    const bool apply = cand && rcpt_ok && !expiry;
+    const bool apply = cand & rcpt_ok & !expiry;
     const uint32_t sk_b = selu32(apply && kind == KIND_UPDATE, kSetRec,
                                  selu32(apply && kind == KIND_DELETE, kFreeze, kSetNone));
     const uint32_t fl_b = kRsClass2 | (cand ? kRsCand : 0u) | (rcpt_ok ? kRsRcptOk : 0u) | (expiry ? kRsExpiry : 0u);

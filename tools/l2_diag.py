@@ -8,8 +8,8 @@ the seed-controlled measured batches of each mix, as a difference from main.
         [--variants base=,nt=build/diag_nt/libgvstore_test.so] \
         [--mixes main,main#2,all_miss_read,hot_next_rud] [--args "--log2n 20 --batch 65536"]
 
-A variant names a library (GVS_LIB_OVERRIDE); an empty path is the in-tree
-test library.  Test infrastructure only: nothing here is on the product path.
+A variant names a library (GVS_LIB_OVERRIDE; an empty path is the in-tree
+test library) and optionally, after "@", GVS_DIAG bits (name=lib@0x400).  Test infrastructure only: nothing here is on the product path.
 """
 import argparse
 import collections
@@ -50,7 +50,7 @@ def split(vals, first):
     return out
 
 
-def run(outdir, counters, mix, lib, args, timeout):
+def run(outdir, counters, mix, lib, args, timeout, diag=None):
     os.makedirs(outdir, exist_ok=True)
     cmd = (["rocprofv3", "--pmc"] + counters + ["-d", outdir, "-o", "run", "--output-format", "csv", "--",
                                                  sys.executable, PROBE, mix, "--fill-batches", "3",
@@ -59,6 +59,8 @@ def run(outdir, counters, mix, lib, args, timeout):
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"), GVS_TEST_HOOKS="1")
     if lib:
         env["GVS_LIB_OVERRIDE"] = os.path.join(ROOT, lib)
+    if diag:
+        env["GVS_DIAG"] = diag
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     if r.returncode != 0:
         sys.exit(f"probe failed ({mix}, {lib}):\n" + r.stdout[-3000:] + r.stderr[-3000:])
@@ -133,14 +135,15 @@ def main():
     p.add_argument("--timeout", type=int, default=300)
     a = p.parse_args()
     counters = a.counters.split()
-    variants = [v.split("=", 1) for v in a.variants.split(",")]
+    variants = [(v.split("=", 1) + [""])[:2] for v in a.variants.split(",")]
     mixes = a.mixes.split(",")
     lines = []
-    for vname, lib in variants:
+    for vname, spec in variants:
+        lib, _, diag = spec.partition("@")
         res = {}
         for mix in mixes:
             d = os.path.join(a.outdir, f"{vname}_{mix.replace('#', '_')}")
-            res[mix] = run(d, counters, mix.split("#")[0], lib, a.args.split(), a.timeout)
+            res[mix] = run(d, counters, mix.split("#")[0], lib, a.args.split(), a.timeout, diag)
             print(f"ran {vname} {mix}: {len(res[mix])} batches", flush=True)
         ref = res["main"][-1]
         lines.append(f"=== variant {vname} ({lib or 'in-tree'}); per kernel: main mean, then mix mean - main mean"
