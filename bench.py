@@ -647,7 +647,7 @@ def main():
             pass
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel": "k_rpass2 (fixed-slot message-table pass)",
+                    "kernel": "k_rpass2s (fixed-schedule message-table pass)",
                     "txn_slots": c, "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms}
         if a.auth:
             # sealed rows: the pass is bound by vector-ALU issue (AES + BLAKE2b),

@@ -46,20 +46,26 @@ constexpr uint32_t CF_MBOX_OK = 2u; // create passes the mailbox checks
 // Per-op records are 128 B (one L2 line) and written whole by one thread, so
 // no two ops ever share a line: scattered per-op traffic then touches a fixed
 // set of lines whatever order the data imposes (obliviousness).
-// 16-B store that drops the line from the XCD's L2 (buffer_store ... sc1:
+// 16-B store that drops the line from the XCD's L2 (buffer_store ... nt sc1:
 // the bytes are written through and the L2 drops the line,
-// MI355X_MICROARCH.md:174).  Every record or row that a LATER kernel reads in
+// MI355X_MICROARCH.md:174; with nt the line is not kept on the memory side
+// either: with sc1 alone, the readers of such records ran 4-7 us faster when
+// the batch had just written more of them, k_vscan_a<M1rOp> / k_m1r_c at C3,
+// profiles/r04j_timing_*).  Every record or row that a LATER kernel reads in
 // an order or pairing that depends on the data is stored this way, so that the
 // reader fetches it from HBM whatever the data, instead of hitting lines that
 // happen to still sit in some XCD's L2 (FETCH_SIZE would then depend on the
 // data; DESIGN.md §3 rule 3).  `base` is an array base (wave-uniform); the
 // byte offset 16 * i must be below 2^32.
+#ifndef GVS_DIAG_DROP_AUX
+#define GVS_DIAG_DROP_AUX (2 | 16)  // nt sc1 (diagnostic builds may change it)
+#endif
 __device__ inline void st_drop(const void* base, uint64_t i, uint4 x) {
   typedef unsigned int u4v __attribute__((ext_vector_type(4)));
   const u4v v = {x.x, x.y, x.z, x.w};
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(i * 16u), 0, 16 /* sc1 */);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(i * 16u), 0, GVS_DIAG_DROP_AUX);
 }
 
 // 16-B streaming store of a table or mailbox row (buffer_store ... nt sc1:

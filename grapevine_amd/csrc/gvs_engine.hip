@@ -132,7 +132,7 @@ struct Engine {
   uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
   uint4* msnap = nullptr;    // Q*cm x 1 KiB
   uint4* msnapp = nullptr;   // B x 1 KiB (group snapshots by head position)
-  uint4* mdry = nullptr;     // Q x 4 KiB (k_m1x / k_m2x: one 1 KiB per dry use)
+  uint4* mdry = nullptr;     // Q x 8 KiB (k_m1x / k_m2x: one 1 KiB per dry use)
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
   GtxV* gtx_carry = nullptr;
@@ -598,7 +598,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(gtx, (QC + B) * 8);
     A(msnap, QC * 64);
     A(msnapp, (uint64_t)B * 64);
-    A(mdry, (uint64_t)e.Q * 256);
+    A(mdry, (uint64_t)e.Q * kMDryU4);
     A(m2tx, (QC + B) * kVLineU4);
     A(gtx_agg, B / kScanT);
     A(gtx_carry, B / kScanT);
@@ -854,6 +854,14 @@ static MArgs margs2(const gvs_handle* h, const Engine& e) {
   a.mdry = e.mdry;
   a.stamp = e.stamp_run;
   a.cm = e.cm;
+  // a prime under 2^12 (slot x * it stays below 2^32) not dividing Q*cm
+  const uint32_t qc = e.Q * e.cm;
+  a.sink_mul = 1;
+  for (uint32_t m : {4093u, 4091u, 4079u})
+    if (qc % m != 0u) {
+      a.sink_mul = m;
+      break;
+    }
   return a;
 }
 

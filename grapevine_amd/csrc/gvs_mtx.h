@@ -225,6 +225,34 @@ __device__ inline uint32_t load_groups(const MArgs& a, uint32_t q, GroupM* g, ui
   return *s_ng;
 }
 
+// The row passes run one iteration of their per-group code for every row the
+// batch touches (in the row stream, by the wave that streams the row) and one
+// for every group slot no row takes.  Touched rows fall to the waves by the
+// data, so the slot iterations are dealt out by what each wave already has:
+// wave w takes T - t_w of them (T = ceil(cm / 4), t_w its touched rows) and
+// spreads them evenly over its chunks, so that every wave runs T iterations
+// in the stream, whatever the batch touched (fewer touched rows made k_m1x /
+// k_m2x 11-15 us faster at C3: profiles/r04g_timing_c3_store.txt).  A wave
+// with more than T touched rows (2^-20-rare under the keyed recipient hash)
+// runs them all.  Past the list of slots, iterations use the dry lines.
+constexpr uint32_t kRowWaves = 4;
+__device__ inline void slot_share(const uint32_t* s_tw, uint32_t cm, uint32_t wave, uint32_t* start,
+                                  uint32_t* cnt) {
+  const uint32_t T = (cm + kRowWaves - 1) / kRowWaves;
+  uint32_t s = 0, c = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < kRowWaves; ++v) {
+    const uint32_t cv = T > s_tw[v] ? T - s_tw[v] : 0u;
+    s += v < wave ? cv : 0u;
+    c = v == wave ? cv : c;
+  }
+  *start = s;
+  *cnt = c;
+}
+
+// chunk i of n: its share of the wave's d slot iterations (even spread)
+__device__ inline uint32_t spread_lo(uint32_t i, uint32_t n, uint32_t d) { return n ? (i * d) / n : 0u; }
+
 // --------------------------------------------------------------- k_m1x
 
 // mailbox read pass: snapshot of every group's row, with the verdict header
@@ -235,7 +263,10 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   __shared__ GroupM g[kGroupMax + 1];
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
-  __shared__ uint32_t s_ng, s_occ, s_empt;
+  __shared__ uint32_t s_ng, s_occ, s_empt, s_w[4], s_tw[kRowWaves];
+  __shared__ uint8_t s_tf[kGroupMax];     // tail: slots without a row
+  __shared__ uint16_t s_tp[kGroupMax + 1];
+  __shared__ int16_t s_tl[kGroupMax];
   GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
   __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id();
@@ -281,10 +312,47 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   __syncthreads();
   // group snapshots go to MSNAPP at the head's sorted position, so that every
   // op of k_m1r_c reads line p (an address stream that does not depend on the
-  // batch); unused slots write their own line of the MSNAP sink
-  uint4* snap = a.msnap + (uint64_t)q * a.cm * 64;
-  uint4* dry = a.mdry + (uint64_t)q * 256;  // lines 0..63: the row loop's, 64..127: the slot loop's
-  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+  // batch); slots without a row write a header-only line there, unused slots
+  // their own line of the MSNAP sink: every slot written once
+  uint4* dry = a.mdry + (uint64_t)q * kMDryU4;  // slot iterations past the list: 1 KiB line 1
+  // each wave's touched rows, and the slots without a row, listed
+  if (tid < kRowWaves) s_tw[tid] = 0;
+  __syncthreads();
+  for (uint32_t j = tid; j < a.Sr; j += 256) atomicAdd(&s_tw[(j / kMU) % kRowWaves], s_sg[j] >= 0 ? 1u : 0u);
+  for (uint32_t k = tid; k < a.cm; k += 256) s_tf[k] = (k < ng && g[k].slot >= 0) ? 0 : 1;
+  __syncthreads();
+  block_flag_scan(s_tf, a.cm, s_tp, s_w);
+  for (uint32_t k = tid; k < a.cm; k += 256)
+    if (s_tf[k]) s_tl[s_tp[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t nfree = s_tp[a.cm];
+  uint32_t d0, dn;
+  slot_share(s_tw, a.cm, wave, &d0, &dn);
+  const uint32_t nch = a.Sr > wave * kMU ? (a.Sr - wave * kMU + 4 * kMU - 1) / (4 * kMU) : 0u;
+  // one iteration: a touched row's snapshot (bit set) or a slot without a row
+  // (bit 0: header only), the same code and one 1-KiB line written either way
+  auto step = [&](const uint4 (&v)[kMU], uint32_t bit, uint32_t j0, uint32_t di) {
+    const bool slot_it = bit == 0u;
+    uint4 cur = v[0];
+#pragma unroll
+    for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+    const bool listed = slot_it && di < nfree;
+    const int k = slot_it ? (listed ? (int)s_tl[di] : 0) : s_sg[j0 + u0];
+    const GroupM& G = g[k >= 0 ? (uint32_t)k : 0u];
+    const bool real = !slot_it || (listed && (uint32_t)k < ng);
+    const uint4 hdr = sel4(real, make_uint4(slot_it ? 0u : G.len, G.fl, G.flags, (uint32_t)G.slot),
+                           make_uint4(0, 0, 0, 0));
+    cur = sel4(lane == 0, hdr, sel4(lane == 1 || slot_it, make_uint4(0, 0, 0, 0), cur));
+    // an unused slot's sink line is scattered over MSNAP like the heads'
+    // lines over MSNAPP: the partition's 1-KiB sink lines written in a row
+    // made a batch without groups 7-9 us faster (DRAM page locality)
+    const uint32_t sl = ((q * a.cm + (uint32_t)k) * a.sink_mul) % (a.Q * a.cm);
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : a.msnap + (uint64_t)sl * 64;
+    st_drop(dst, lane, cur);
+  };
+  uint32_t ci = 0;  // the wave's chunk index
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU, ++ci) {
     if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
     uint4 v[kMU];
     uint32_t mm = 0;
@@ -296,39 +364,23 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     }
     if (AUTH) m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
     mm = __builtin_amdgcn_readfirstlane(mm);
-    // wave 0's first chunk runs the loop once dry: an extra mask bit taken
-    // last by the same loop code (no peeled first iteration)
-    uint32_t mq = mm | (j0 == 0 ? (1u << kMU) : 0u);
-    while (mq) {
+    // the chunk's touched rows, then its share of the slot iterations
+    const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
+    const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
+    uint32_t mq = mm;
+    for (uint32_t r = 0; r < nr; ++r) {
       const uint32_t low = mq & (0u - mq);
       mq &= mq - 1u;
-      const bool dry_run = low == (1u << kMU);
-      const uint32_t bit = dry_run ? 0u : low;
-      uint4 cur = v[0];
-#pragma unroll
-      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
-      const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
-      const int k = dry_run ? 0 : s_sg[j0 + u0];
-      const GroupM& G = g[k];
-      const uint4 hdr = make_uint4(G.len, G.fl, G.flags, (uint32_t)G.slot);
-      cur = sel4(lane == 0, hdr, sel4(lane == 1, make_uint4(0, 0, 0, 0), cur));
-      uint4* dst = dry_run ? dry : a.msnapp + (uint64_t)G.head * 64;
-      st_drop(dst, lane, cur);
+      step(v, low, j0, d0 + dlo + (r - nt));
     }
 #pragma unroll
     for (int u = 0; u < kMU; ++u) va[u] = vb[u];
   }
-  // slots without a row (new recipients, misses, unused slots): header only;
-  // wave 0 also runs once dry, so every slot of MSNAP is written exactly once
-  for (uint32_t k = wave; k <= a.cm; k += 4) {
-    const bool dry_run = k == a.cm;
-    const GroupM& G = g[min(k, a.cm - 1u)];
-    const bool has_row = !dry_run && k < ng && G.slot >= 0;
-    if (has_row) continue;
-    const bool real = !dry_run && k < ng;
-    const uint4 hdr = sel4(real, make_uint4(0u, G.fl, G.flags, (uint32_t)G.slot), make_uint4(0, 0, 0, 0));
-    uint4* dst = dry_run ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : snap + (uint64_t)k * 64;
-    st_drop(dst, lane, sel4(lane == 0, hdr, make_uint4(0, 0, 0, 0)));
+  if (nch == 0) {  // a wave with no rows (partitions under 4 chunks): its slot iterations here
+    uint4 v[kMU];
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) v[u] = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < dn; ++r) step(v, 0u, 0u, d0 + r);
   }
 }
 
@@ -644,7 +696,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   __shared__ uint8_t s_gflag[kGroupMax + 1];
   __shared__ int16_t s_pend[kGroupMax + 1];
   __shared__ uint8_t s_ld[kGroupMax + 1];
-  __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta;
+  __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta, s_tw[kRowWaves];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
@@ -697,13 +749,67 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     atomicSub(&s_delta, (k >= 0 && g[k >= 0 ? k : 0].fl == 0) ? 1u : 0u);
   }
   if (tid == 0) atomicAdd(&s_delta, npend);
+  if (tid < kRowWaves) s_tw[tid] = 0;
   __syncthreads();
+  // the slot each touched row takes (a new recipient placed in it, else the
+  // row's own group), and each wave's touched rows (chunk j / kMU of the
+  // partition is streamed by wave (j / kMU) % 4)
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j], pl = s_place[j];
+    const int ge = pl >= 0 ? pl : k;
+    s_ld[ge >= 0 ? (uint32_t)ge : (uint32_t)kGroupMax] = 1;
+    atomicAdd(&s_tw[(j / kMU) % kRowWaves], ge >= 0 ? 1u : 0u);
+  }
+  __syncthreads();
+  // the slots no row takes, listed: each is read once, by a slot iteration
+  for (uint32_t k = tid; k < a.cm; k += 256) s_gflag[k] = s_ld[k] ? 0 : 1;
+  __syncthreads();
+  block_flag_scan(s_gflag, a.cm, s_gpfx, s_w);
+  for (uint32_t k = tid; k < a.cm; k += 256)
+    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t nfree = s_gpfx[a.cm];
+  uint32_t d0, dn;
+  slot_share(s_tw, a.cm, wave, &d0, &dn);
+  const uint32_t nch = a.Sr > wave * kMU ? (a.Sr - wave * kMU + 4 * kMU - 1) / (4 * kMU) : 0u;
   const uint4* res = a.m2tx + (uint64_t)q * a.cm * kVLineU4;
-  // k_m1x wrote lines 0..127 of the workgroup's dry block; the row loop reads
-  // 128..191 and the slot loop 192..255 (no line is read twice in a kernel)
-  const uint4* dry = a.mdry + (uint64_t)q * 256 + 128;
+  // the workgroup's dry block: k_m1x writes its first 4 KiB; slot iterations
+  // past the list read 1 KiB lines 4..7 (no line is read twice in a kernel)
+  const uint4* dry = a.mdry + (uint64_t)q * kMDryU4 + 256;
   uint4* wst = AUTH ? st : s_wst[AUTH ? 0 : wave];
-  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU) {
+  // one iteration: a touched row (bit set: its row in v is replaced) or a
+  // slot no row takes (bit 0: the same work, nothing kept)
+  auto step = [&](uint4 (&v)[kMU], uint4 (&sd)[kMU], uint32_t bit, uint32_t j0, uint32_t di) {
+    const bool slot_it = bit == 0u;
+    uint4 cur = v[0];
+#pragma unroll
+    for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+    const uint32_t j = j0 + ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u);
+    const bool listed = slot_it && di < nfree;
+    const int k = slot_it ? -1 : s_sg[j], pl = slot_it ? -1 : s_place[j];
+    const int ge = slot_it ? (listed ? (int)s_pend[di] : 0) : (pl >= 0 ? pl : k);
+    const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
+    const uint4* rs = (slot_it && !listed) ? dry + 64u * min(di - nfree, 3u)
+                                           : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
+    const uint4 app = ld_row<true>(&rs[lane]);
+    const bool matched = pl < 0;
+    const uint32_t len = matched ? G.len : 0u;
+    const uint32_t dp = min(G.n_del, len);
+    const uint64_t mask = ((uint64_t)G.mhi << 32) | G.mlo;
+    uint32_t fl;
+    const uint4 nv = m2_row(cur, matched, len, dp, mask, G.n_succ, app, wst, &fl);
+    const uint64_t w1 = (G.glo << 23) | ((uint64_t)fl << 1) | 1ull;
+    const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                                              (uint32_t)(w1 >> 32)),
+                           make_uint4(0, 0, 0, 0));
+#pragma unroll
+    for (int uu = 0; uu < kMU; ++uu) {  // a slot iteration has bit 0: no change
+      v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
+      sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
+    }
+  };
+  uint32_t ci = 0;  // the wave's chunk index
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU, ++ci) {
     if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
     uint4 v[kMU], sd[kMU];
     uint32_t mm = 0;
@@ -724,39 +830,14 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       for (int u = 0; u < kMU; ++u) sd[u] = shfl4(mine, u);
     }
     mm = __builtin_amdgcn_readfirstlane(mm);
-    uint32_t mq = mm | (j0 == 0 ? (1u << kMU) : 0u);  // the dry run: an extra bit, taken last
-    while (mq) {
+    // the chunk's touched rows, then its share of the slot iterations
+    const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
+    const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
+    uint32_t mq = mm;
+    for (uint32_t r = 0; r < nr; ++r) {
       const uint32_t low = mq & (0u - mq);
       mq &= mq - 1u;
-      const bool dry_run = low == (1u << kMU);
-      const uint32_t bit = dry_run ? 0u : low;
-      uint4 cur = v[0];
-#pragma unroll
-      for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
-      const uint32_t j = j0 + ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u);
-      const int k = dry_run ? -1 : s_sg[j], pl = dry_run ? -1 : s_place[j];
-      // the slot whose result this row takes: a new recipient placed in it,
-      // else the row's own group
-      const int ge = pl >= 0 ? pl : k;
-      const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
-      const uint4* rs = dry_run ? dry : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
-      const uint4 app = ld_row<true>(&rs[lane]);
-      if (lane == 0) s_ld[dry_run ? (uint32_t)kGroupMax : (uint32_t)ge] = 1;
-      const bool matched = pl < 0;
-      const uint32_t len = matched ? G.len : 0u;
-      const uint32_t dp = min(G.n_del, len);
-      const uint64_t mask = ((uint64_t)G.mhi << 32) | G.mlo;
-      uint32_t fl;
-      const uint4 nv = m2_row(cur, matched, len, dp, mask, G.n_succ, app, wst, &fl);
-      const uint64_t w1 = (G.glo << 23) | ((uint64_t)fl << 1) | 1ull;
-        const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
-                                                (uint32_t)(w1 >> 32)),
-                             make_uint4(0, 0, 0, 0));
-#pragma unroll
-      for (int uu = 0; uu < kMU; ++uu) {  // the dry run has bit 0: no change
-        v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
-        sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
-      }
+      step(v, sd, low, j0, d0 + dlo + (r - nt));
     }
     if (AUTH) {
       const uint64_t r0 = (uint64_t)q * a.Sr + j0;
@@ -784,14 +865,11 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       va[u] = vb[u];
     }
   }
-  __syncthreads();
-  // result slots no row took: every slot of M2TX is read once; the wave that
-  // reaches k = cm reads the dry line, so the code runs in every workgroup
-  for (uint32_t k = wave; k <= a.cm; k += 4) {
-    const bool dry_run = k == a.cm;
-    if (!dry_run && s_ld[k]) continue;
-    uint4 x = ld_row<true>(dry_run ? &dry[64 + lane] : &res[(uint64_t)k * kVLineU4 + 8 + lane]);
-    keep4(x);
+  if (nch == 0) {  // a wave with no rows (partitions under 4 chunks): its slot iterations here
+    uint4 v[kMU], sd[kMU];
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) v[u] = sd[u] = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < dn; ++r) step(v, sd, 0u, 0u, d0 + r);
   }
   // every workgroup adds, zero included: a fixed set of atomics
   if (tid == 0)

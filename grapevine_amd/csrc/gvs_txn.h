@@ -562,8 +562,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (NTS) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
-        else st_row<false>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
+        // plain rows written through (st_stream); sealed rows non-temporal:
+        // written through, the sealed pass's FETCH_SIZE spread 4x wider
+        // between identical batches (profiles/r04l_auth_store_policy.txt)
+        if (NTS && !AUTH) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
+        else st_row<NTS>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
       }
     }
     // The waves meet after every tile, expiry or not: without the barrier they
