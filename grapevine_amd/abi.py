@@ -104,6 +104,9 @@ RAW_MESSAGES, RAW_MAILBOXES, RAW_SIDE, RAW_MSG_TAGS, RAW_MBOX_TAGS = range(5)
 # the final row states the last batch left pending (by sorted position), their
 # side entries and tags, and that batch's slot descriptors (include/gvstore_test.h)
 RAW_PENDING, RAW_PENDING_SIDE, RAW_PENDING_TAGS, RAW_SLOTS = range(5, 9)
+# the key-value map's key directory (N x 32 B: key, hash) and, sealed, its
+# 1-KiB row tags (N/32 x 16 B)
+RAW_KEY_DIR, RAW_KEY_DIR_TAGS = 9, 10
 # header table field of a message row whose final state is pending in P
 TABLE_PENDING_STATE, TABLE_PENDING_ROW = 2, 0x100
 

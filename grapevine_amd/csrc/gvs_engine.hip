@@ -140,6 +140,7 @@ struct Engine {
   uint4* kvmeta = nullptr;   // B x 128-B op lines
   uint4* kvdummy = nullptr;  // B x 1 KiB
   uint4* kdir = nullptr;     // N x 32 B key directory (key, hash)
+  uint4* ktag = nullptr;     // sealed map: N/32 directory row tags
   Key128* okeys = nullptr;   // B (hash, seq) sort keys
   uint4* opr = nullptr;      // B x 128 B position records
   uint4* opos = nullptr;     // B
@@ -1330,6 +1331,9 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   e.S = (uint32_t)S;
   e.W = (uint32_t)(N / S);
   e.c = txn_slots(B, e.W, e.S);
+  // the sealed map's key pass holds the AES tables in LDS and a partition's
+  // directory entries in registers: fewer group slots and rows (gvs_omap.h)
+  if (h->kind == 2 && h->auth && (e.c > kOkeySealedSlots || e.S > kOkeySealedRows)) return GVS_ERR_INVALID_ARG;
   const uint64_t WC = (uint64_t)e.W * e.c;
 #define A(ptr, n)                                     \
   do {                                                \
@@ -1364,6 +1368,7 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   }
   if (h->kind == 2) {  // key-value map: key directory, key sort, group slots
     A(kdir, N * 2);
+    if (h->auth) A(ktag, N / 32);
     A(okeys, B);
     A(opr, (uint64_t)B * 8);
     A(opos, B);
@@ -1389,6 +1394,9 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
     e.epoch = 0;
     hipLaunchKernelGGL(k_seal_init, dim3(1024), dim3(256), 0, s, seal_of(h, e), (const uint32_t*)h->te,
                        e.table, e.mtag, (uint4*)nullptr, 0u, N);
+    if (h->kind == 2)  // the map's key directory: sealed rows of 32 entries
+      hipLaunchKernelGGL(k_kdir_seal_init, dim3(1024), dim3(256), 0, s, seal_of(h, e), (const uint32_t*)h->te,
+                         e.kdir, e.ktag, N / 32);
     GVS_HIP(h, hipGetLastError());
   }
   GVS_HIP(h, hipStreamSynchronize(s));
@@ -1477,8 +1485,17 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_scan_c<OgtOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
   mark(h, "groups");
-  hipLaunchKernelGGL(k_okey, dim3(e.W), dim3(256), 0, s,
-                     OkeyArgs{e.ogt, e.kdir, e.ogp, e.scal, e.W, e.S, e.c, B, e.stamp_run});
+  {
+    OkeyArgs a{e.ogt, e.kdir, e.ogp, e.scal, e.W, e.S, e.c, B, e.stamp_run};
+    if (h->auth) {
+      a.sc = seal_of(h, e);
+      a.te = h->te;
+      a.ktag = e.ktag;
+      hipLaunchKernelGGL(k_okey<true>, dim3(e.W), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(k_okey<false>, dim3(e.W), dim3(256), 0, s, a);
+    }
+  }
   mark(h, "keys");
   {
     OrowArgs a{e.opos, e.opr, e.ogp, e.rkeys, e.kvmeta, e.orow_agg, e.orow_carry, e.scal, B, B / kScanT};
@@ -1517,6 +1534,8 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     vscan_abc<KvOp>(s, a);
     hipLaunchKernelGGL(k_kv_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
+  if (h->auth)  // P at the epoch the pass wrote the rows at
+    hipLaunchKernelGGL(k_pseal<true>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch + 1));
   if (d_out && n)
     hipLaunchKernelGGL(k_out, dim3((n + 4 * kCopyPerWave - 1) / (4 * kCopyPerWave)), dim3(256), 0, s,
                        (const uint4*)e.resp, n, d_out);
@@ -2478,6 +2497,9 @@ static int raw_region(gvs_handle* h, uint32_t shard, uint32_t region, void** bas
     case 6: *base = e.psd; *size = (uint64_t)e.B * 128; break;
     case 7: *base = e.ptag; *size = e.ptag ? (uint64_t)e.B * 16 : 0; break;
     case 8: *base = e.tbuf[e.par ^ 1]; *size = (uint64_t)e.W * e.c * 128; break;
+    // the key-value map's key directory and, sealed, its row tags
+    case 9: *base = e.kdir; *size = e.kdir ? e.N * 32 : 0; break;
+    case 10: *base = e.ktag; *size = e.ktag ? e.N / 32 * 16 : 0; break;
     default: return GVS_ERR_INVALID_ARG;
   }
   return *base ? GVS_OK : GVS_ERR_INVALID_ARG;
@@ -2514,8 +2536,9 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
 }
 
 
-// the block store's engine handle, for the raw-region hooks above
+// the block store's and the map's engine handles, for the raw-region hooks above
 gvs_handle* gvs_oram_test_handle(gvs_oram* o) { return o ? o->h : nullptr; }
+gvs_handle* gvs_omap_test_handle(gvs_omap* m) { return m ? m->h : nullptr; }
 
 // The router's placement on the host, with the device's route_dest (see
 // include/gvstore_test.h): slot[i] = d * C + rank of request i among this
@@ -2585,7 +2608,6 @@ static int kv_create(const gvs_oram_config* cfg, int kind, gvs_handle** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GVS_ERR_NO_DEVICE;
   if ((int)cfg->device >= ndev) return GVS_ERR_INVALID_ARG;
-  if (kind == 2 && (cfg->flags & GVS_FLAG_AUTH_STORAGE)) return GVS_ERR_INVALID_ARG;
   gvs_handle* h = new (std::nothrow) gvs_handle();
   if (!h) return GVS_ERR_OUT_OF_MEMORY;
   h->kind = kind;

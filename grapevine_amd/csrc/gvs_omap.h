@@ -230,7 +230,17 @@ struct OkeyArgs {
   uint4* ogp;         // (B + W*c) x 128 B: group results by head position (dummies after B)
   Scal* scal;
   uint32_t W, S, c, B, stamp;
+  // sealed map (AUTH): the directory as N/32 rows of 1 KiB (32 entries each),
+  // sealed like the mailbox rows (AES-CTR, BLAKE2b tag over the row, its
+  // index, the epoch and table kDirTable), one 16-B tag per row
+  SealCtx sc;
+  const uint32_t* te;
+  uint4* ktag;
 };
+
+constexpr uint32_t kDirTable = 3;        // seal domain of the key directory rows
+constexpr uint32_t kOkeySealedSlots = 256;  // group slots per partition, sealed map (LDS: the AES tables)
+constexpr uint32_t kOkeySealedRows = 1024;  // rows per partition, sealed map (entries held in registers)
 
 struct GroupO {
   uint64_t hi, lo;  // hash (lo with the seq bits cleared)
@@ -254,17 +264,23 @@ __device__ inline int find_group_o(const GroupO* g, uint32_t ng, uint32_t c, uin
   return (pos < ng && G.hi == hi && G.lo == lo) ? (int)pos : -1;
 }
 
+template <bool AUTH>
 __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
-  __shared__ GroupO g[kSlotMax + 1];
+  constexpr uint32_t kG = AUTH ? kOkeySealedSlots : kSlotMax;  // group slots at most; g[kG]: the sink
+  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
+  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(2) : 1];
+  __shared__ GroupO g[kG + 1];
   __shared__ int16_t s_m[kRowsMax];    // row -> matched group, or -1
   __shared__ uint8_t s_free[kRowsMax];
   __shared__ uint16_t s_fpfx[kRowsMax + 1];
-  __shared__ uint8_t s_need[kSlotMax + 1];
-  __shared__ uint16_t s_npfx[kSlotMax + 1];
-  __shared__ int16_t s_pend[kSlotMax + 1];
+  __shared__ uint8_t s_need[kG + 1];
+  __shared__ uint16_t s_npfx[kG + 1];
+  __shared__ int16_t s_pend[kG + 1];
   __shared__ uint32_t s_w[4], s_ng;
   const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = lane_id(), wave = tid >> 6;
   if (a.scal->error) return;
+  if (AUTH) load_te(s_te, a.te);
+  uint4* st = s_st + (AUTH ? wave * stage_u4(2) : 0u);
   if (tid == 0) s_ng = 0;
   __syncthreads();
   // Global reads cover whole 128-B lines in one instruction (a line read in
@@ -303,14 +319,22 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   // on the traffic in between: FETCH_SIZE would depend on the keys)
   // Each wave reads its 64 entries (2 KiB) as two whole-line loads, entry
   // j = tid + 256 it to lane tid % 64 by shuffles (S >= 256, a power of two).
-  constexpr uint32_t kIt = kRowsMax / 256;
+  constexpr uint32_t kIt = AUTH ? kOkeySealedRows / 256 : kRowsMax / 256;
   uint4 dkey[kIt], dh[kIt];
   const int se = (int)((2u * lane) & 63u);
 #pragma unroll
   for (uint32_t it = 0; it < kIt; ++it) {
     const uint32_t j0 = it * 256 + wave * 64;
     if (j0 >= a.S) break;  // S only
-    const uint4 lo = kd[(uint64_t)j0 * 2 + lane], hi = kd[(uint64_t)j0 * 2 + 64 + lane];
+    uint4 lo = kd[(uint64_t)j0 * 2 + lane], hi = kd[(uint64_t)j0 * 2 + 64 + lane];
+    if (AUTH) {  // directory rows r0, r0 + 1: verified and decrypted at the epoch
+      uint4 v[2] = {lo, hi};
+      const uint64_t r0 = ((uint64_t)w * a.S + j0) / 32;
+      if (!wave_unseal<2>(a.sc, s_te, kDirTable, r0, v, a.ktag, false, st) && lane == 0)
+        atomicOr(&a.scal->error, 8u);
+      lo = v[0];
+      hi = v[1];
+    }
     const uint4 klo = shfl4(lo, se), khi = shfl4(hi, se), hlo = shfl4(lo, se + 1), hhi = shfl4(hi, se + 1);
     dkey[it] = sel4(lane < 32u, klo, khi);
     dh[it] = sel4(lane < 32u, hlo, hhi);
@@ -325,7 +349,7 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const GroupO& G = g[k >= 0 ? k : 0];
     const bool match = used && k >= 0 && key.x == G.key[0] && key.y == G.key[1] && key.z == G.key[2] &&
                        key.w == G.key[3];
-    const uint32_t kk = match ? (uint32_t)k : (uint32_t)kSlotMax;  // sink entry otherwise
+    const uint32_t kk = match ? (uint32_t)k : kG;  // sink entry otherwise
     g[kk].row = (int32_t)j;
     g[kk].e0 = 1u;
     s_m[j] = match ? (int16_t)k : (int16_t)-1;
@@ -342,13 +366,13 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   const uint32_t nfree = s_fpfx[a.S], nneed = s_npfx[a.c];
   const uint32_t nadm = min(nfree, nneed);
   for (uint32_t k = tid; k < a.c; k += 256)  // admitted groups in order; the rest write the sink
-    s_pend[(s_need[k] && s_npfx[k] < nadm) ? s_npfx[k] : (uint32_t)kSlotMax] = (int16_t)k;
+    s_pend[(s_need[k] && s_npfx[k] < nadm) ? s_npfx[k] : kG] = (int16_t)k;
   __syncthreads();
   // the r-th free row takes the r-th admitted group
   for (uint32_t j = tid; j < a.S; j += 256) {
     const bool take = s_free[j] && s_fpfx[j] < nadm;
-    const int16_t k = s_pend[min((uint32_t)s_fpfx[j], (uint32_t)kSlotMax)];
-    const uint32_t kk = take ? (uint32_t)k : (uint32_t)kSlotMax;
+    const int16_t k = s_pend[min((uint32_t)s_fpfx[j], kG)];
+    const uint32_t kk = take ? (uint32_t)k : kG;
     g[kk].row = (int32_t)j;
     s_m[j] = take ? (int16_t)(k | 0x4000) : s_m[j];  // placed: bit 14
   }
@@ -373,8 +397,11 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const int e = (int)(lane >> 1);
     const uint4 klo = shfl4(key, e), khi = shfl4(key, 32 + e), hlo = shfl4(h, e), hhi = shfl4(h, 32 + e);
     const uint64_t j0 = (uint64_t)j - lane;
-    kd[j0 * 2 + lane] = sel4(lane & 1u, hlo, klo);
-    kd[j0 * 2 + 64 + lane] = sel4(lane & 1u, hhi, khi);
+    uint4 v[2] = {sel4(lane & 1u, hlo, klo), sel4(lane & 1u, hhi, khi)};
+    if (AUTH)  // sealed at the next epoch, tags with them
+      wave_seal<2>(a.sc, s_te, kDirTable, ((uint64_t)w * a.S + j0) / 32, a.sc.epoch + 1u, v, a.ktag, false, st);
+    kd[j0 * 2 + lane] = v[0];
+    kd[j0 * 2 + 64 + lane] = v[1];
   }
   // each group's result to its head position (slots without a group:
   // dummies), a record by 8 lanes: one whole-line store
@@ -387,6 +414,24 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const uint64_t idx = real ? G.head : (uint64_t)a.B + (uint64_t)w * a.c + k;
     const uint4 rec0 = make_uint4((uint32_t)prow, (uint32_t)(prow >> 32), (G.e0 ? 1u : 0u) | (ovf ? 2u : 0u), 0u);
     if (k0 + (lane >> 3) < a.c) st_drop(a.ogp, idx * 8 + (lane & 7u), sel4((lane & 7u) == 0u, rec0, make_uint4(0, 0, 0, 0)));
+  }
+}
+
+// A sealed map's directory at creation: N/32 all-zero rows sealed at epoch 0,
+// one wave per two rows (grid-stride).
+__global__ __launch_bounds__(256) void k_kdir_seal_init(SealCtx c, const uint32_t* g_te, uint4* kdir,
+                                                        uint4* ktag, uint64_t n_rows) {
+  GVS_TE_LDS s_te[kTeWords];
+  __shared__ uint4 s_st[4 * stage_u4(2)];
+  load_te(s_te, g_te);
+  __syncthreads();
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint4* st = s_st + wave * stage_u4(2);
+  for (uint64_t r0 = ((uint64_t)blockIdx.x * 4 + wave) * 2; r0 < n_rows; r0 += (uint64_t)gridDim.x * 8) {
+    uint4 v[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    wave_seal<2>(c, s_te, kDirTable, r0, 0u, v, ktag, false, st);
+    kdir[r0 * 64 + lane] = v[0];
+    kdir[r0 * 64 + 64 + lane] = v[1];
   }
 }
 

@@ -36,7 +36,7 @@ EXPORTED = (
     "gvs_host_alloc", "gvs_host_free", "gvs_process_wire_batches",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
-                 "gvs_route_plan", "gvs_oram_test_handle")
+                 "gvs_route_plan", "gvs_oram_test_handle", "gvs_omap_test_handle")
 
 
 def test_hooks_enabled():
@@ -100,6 +100,8 @@ def load_library(path=None):
         lib.gvs_route_plan.argtypes = [ctypes.POINTER(abi.GvsConfig), vp, u32, vp, P32, P32, vp]
         lib.gvs_oram_test_handle.argtypes = [vp]
         lib.gvs_oram_test_handle.restype = vp
+        lib.gvs_omap_test_handle.argtypes = [vp]
+        lib.gvs_omap_test_handle.restype = vp
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p
@@ -124,7 +126,7 @@ def load_library(path=None):
     lib.gvs_omap_last_error.restype = ctypes.c_char_p
     for name in EXPORTED + (TEST_EXPORTED if hooks else ()):
         if name not in ("gvs_last_error", "gvs_version", "gvs_oram_last_error", "gvs_omap_last_error",
-                        "gvs_oram_test_handle"):
+                        "gvs_oram_test_handle", "gvs_omap_test_handle"):
             getattr(lib, name).restype = i32
     if path is None:
         _LIB = lib
@@ -502,6 +504,23 @@ class KeyValueMap:
 
     def access_device(self, d_ops, n, d_out):
         self._check(self.lib.gvs_omap_access_batch_device(self.h, d_ops, n, d_out))
+
+    def _raw_handle(self):
+        if not hasattr(self.lib, "gvs_omap_test_handle"):
+            raise RuntimeError("raw regions need the test library (GVS_TEST_HOOKS=1)")
+        return self.lib.gvs_omap_test_handle(self.h)
+
+    def dump_raw(self, region, offset, nbytes):
+        """Raw device bytes of the value table and its regions (as BlockStore),
+        the key directory (abi.RAW_KEY_DIR) or its tags (RAW_KEY_DIR_TAGS)."""
+        out = np.zeros(nbytes, dtype=np.uint8)
+        self._check(self.lib.gvs_dump_raw(self._raw_handle(), 0, region, offset, out.ctypes.data, nbytes))
+        return out
+
+    def store_raw(self, region, offset, data):
+        """Overwrite raw device bytes (tamper tests of the sealed map)."""
+        buf = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+        self._check(self.lib.gvs_store_raw(self._raw_handle(), 0, region, offset, buf.ctypes.data, len(buf)))
 
     def set_timing(self, on=True):
         self._check(self.lib.gvs_omap_set_timing(self.h, 1 if on else 0))

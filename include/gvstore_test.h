@@ -34,6 +34,11 @@ int gvs_store_raw(gvs_handle *h, uint32_t shard, uint32_t region, uint64_t offse
  * pending final states (5, 6, 7): tamper tests of the sealed block store. */
 gvs_handle *gvs_oram_test_handle(gvs_oram *o);
 
+/* The engine handle under a key-value map (gvs_omap_*): its key directory
+ * (region 9) and, sealed, the directory's row tags (10), besides the block
+ * table's regions: tamper tests of the sealed map. */
+gvs_handle *gvs_omap_test_handle(gvs_omap *m);
+
 /* The router's placement of one source's batch, computed on
  * the host by the device's own routing function: slot[i] = d * C + (rank of
  * request i among this batch's requests for shard d), or 0xFFFFFFFF when that
