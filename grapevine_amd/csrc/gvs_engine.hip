@@ -577,7 +577,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(pbuf, (uint64_t)B * 64);
     A(psd, (uint64_t)B * 8);
     if (h->auth) A(ptag, B);
-    A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
+    A(ps, (WC + B) * (h->auth ? 72 : 64));  // W*c slots + B sink lines (AUTH: then their side-entry lines)
     A(snapp, (uint64_t)B * 64);
     A(dryb, (uint64_t)e.W * 256);
     A(rtx_agg, B / kScanT);
@@ -888,7 +888,7 @@ static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
 
 static PsealArgs pargs(const gvs_handle* h, const Engine& e, uint32_t ep) {
   return PsealArgs{e.pbuf, e.psd, e.ptag, seal_of(h, e), h->te, e.scal, ep,
-                   e.ps, e.ps + (uint64_t)e.W * e.c * 64, e.W * e.c};
+                   e.ps, e.ps + ((uint64_t)e.W * e.c + e.B) * 64, e.W * e.c};
 }
 
 // Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
@@ -969,7 +969,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.stamp_cur = e.stamp_run;
   a.stamp_prev = e.stamp_prev;
   a.ps = e.ps;
-  a.psds = h->auth ? e.ps + (uint64_t)e.W * e.c * 64 : nullptr;
+  a.psds = h->auth ? e.ps + ((uint64_t)e.W * e.c + B) * 64 : nullptr;
   a.snap = e.snap;
   a.snapid = e.snapid;
   a.snapp = e.snapp;
@@ -1041,6 +1041,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     a.pbuf = e.pbuf;
     a.psd = e.psd;
     a.ps = h->auth ? nullptr : e.ps;  // AUTH: all by position, sealed, scattered by the unseal
+    a.psink = h->auth ? e.pbuf : e.ps + (uint64_t)e.W * e.c * 64;  // non-last states (plain: PS's sink lines)
     a.resp = e.resp;
     a.rres = e.rres;
     a.B = B;
@@ -1351,7 +1352,7 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   A(snapp, (uint64_t)B * 64);
   A(pbuf, (uint64_t)B * 64);
   A(psd, (uint64_t)B * 8);
-  A(ps, WC * (h->auth ? 72 : 64));  // AUTH: + W*c side-entry lines
+  A(ps, (WC + B) * (h->auth ? 72 : 64));  // W*c slots + B sink lines (AUTH: then their side-entry lines)
   A(snapid, WC * 8);
   A(snapidp, (uint64_t)B * 8);
   A(dryb, (uint64_t)e.W * 256);
@@ -1440,6 +1441,7 @@ static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     a.pbuf = e.pbuf;
     a.psd = e.psd;
     a.ps = h->auth ? nullptr : e.ps;
+    a.psink = h->auth ? e.pbuf : e.ps + (uint64_t)e.W * e.c * 64;  // non-last states (plain: PS's sink lines)
     a.out = d_out;
     a.outdummy = e.kvdummy;
     a.n = n;
@@ -1526,6 +1528,7 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     a.pbuf = e.pbuf;
     a.psd = e.psd;
     a.ps = h->auth ? nullptr : e.ps;
+    a.psink = h->auth ? e.pbuf : e.ps + (uint64_t)e.W * e.c * 64;  // non-last states (plain: PS's sink lines)
     a.out = e.resp;
     a.outdummy = e.kvdummy;
     a.n = n;

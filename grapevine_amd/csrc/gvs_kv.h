@@ -84,6 +84,7 @@ struct KvArgs {
   const uint4* snapp;      // B x 1 KiB: row snapshots at their first op's position
   uint4* pbuf;             // B x 1 KiB: final states of the positions that are not a row's last
   uint4* psd;              // B x 128 B side entries {row lo, row hi, valid, slot}
+  uint4* psink;            // the other positions' states, by position (plain: PS's B sink lines; AUTH: P)
   uint4* ps;               // plain: W*c x 1 KiB, each row's final state at its slot (the pass
                            // reads P by slot); AUTH: null (P by position, sealed)
   uint4* out;              // ORAM: n x 1 KiB (caller); OMAP: B x kRespSlot
@@ -269,10 +270,11 @@ __global__ __launch_bounds__(256) void k_kv_c(KvArgs a) {
       st_drop(null ? a.outdummy : a.out, (uint64_t)h.seq * 64 + lane, v);
     }
     // a row's final state to its slot (the next pass reads P by slot), the
-    // other positions' states to their own P line: one write per position
-    // (AUTH: all by position, sealed next; the unseal moves them to PS)
+    // other positions' states to their own sink line of PS after the slots:
+    // one write per position, B lines into PS whatever the batch (AUTH: all
+    // by position into P, sealed next; the unseal moves them to PS)
     const bool to_slot = a.ps && last;
-    st_drop(to_slot ? a.ps : a.pbuf, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, v2);
+    st_drop(to_slot ? a.ps : a.psink, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, v2);
     sd = sel4(lane == j, make_uint4((uint32_t)h.prow, (uint32_t)(h.prow >> 32), last ? 1u : 0u, h.slot), sd);
   }
   if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);

@@ -803,8 +803,8 @@ struct PsealArgs {
   const uint32_t* te;
   Scal* scal;
   uint32_t ep;   // epoch of the P rows (seal: written; unseal: read)
-  uint4* ps;     // unseal: W*c x 1 KiB final states by slot (the pass reads every slot)
-  uint4* psds;   // unseal: W*c x 128 B their side entries
+  uint4* ps;     // unseal: (W*c + B) x 1 KiB final states by slot (the pass reads every slot), then sinks
+  uint4* psds;   // unseal: (W*c + B) x 128 B their side entries
   uint32_t nslots;  // W*c
 };
 
@@ -845,18 +845,19 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
     if (lane < (uint32_t)U) st_drop(a.psd, (p0 + lane) * 8, sct);
   } else {
     // a row's last op's state goes to its slot's line of PS (the pass reads
-    // PS by slot), every other position's back to its own P line: one 1 KiB
-    // write per position either way
+    // PS by slot), every other position's to its own sink line of PS, after
+    // the slots: one 1-KiB line and one side line of PS per position, so the
+    // lines each array takes do not depend on the batch
     const uint4 pt = xor4(sd, ks);  // lane u < U: position p0 + u's side entry
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint4 e = uni4(shfl4(pt, u));
       // only an authenticated side entry names a slot (a forged or replayed
-      // one fails the batch and is written back in place)
+      // one fails the batch and goes to its sink)
       const bool last = ok && e.z != 0u && e.w < a.nslots;
-      st_drop(last ? a.ps : a.pbuf, (last ? (uint64_t)e.w : p0 + u) * 64 + lane, v[u]);
-      if (lane < 8) st_drop(last ? a.psds : a.psd, (last ? (uint64_t)e.w : p0 + u) * 8 + lane,
-                            lane == 0 ? e : make_uint4(0, 0, 0, 0));
+      const uint64_t d = last ? (uint64_t)e.w : (uint64_t)a.nslots + p0 + u;
+      st_drop(a.ps, d * 64 + lane, v[u]);
+      if (lane < 8) st_drop(a.psds, d * 8 + lane, lane == 0 ? e : make_uint4(0, 0, 0, 0));
     }
   }
 }
@@ -1317,6 +1318,7 @@ struct Rr2Args {
   uint4* pbuf;            // B final states, by sorted position (AUTH: all of them,
                           // sealed next; plain: the positions that are not a row's last)
   uint4* psd;             // B x 128 B: {physical row lo, hi, valid (the row's last op), slot}
+  uint4* psink;           // the other positions' states, by position (plain: PS's B sink lines; AUTH: P)
   uint4* ps;              // plain: W*c x 1 KiB, each row's final state at its slot
   uint4* resp;            // B internal response slots (kRespSlot)
   RRes* rres;
@@ -1503,10 +1505,11 @@ __global__ __launch_bounds__(256) void k_rr2_c(Rr2Args a) {
       st_drop(a.rres, (uint64_t)h.seq * 8 + lane, t);
     }
     // the row's final state: plain stores put it at the row's slot (the next
-    // pass reads P by slot), every other position's state in its own P line;
-    // AUTH keeps all of them by position (sealed next, k_pseal)
+    // pass reads P by slot), every other position's state in its own sink
+    // line after the slots (so PS takes B lines whatever the batch); AUTH
+    // keeps all of them by position (sealed next, k_pseal)
     const bool to_slot = a.ps && (h.flags & kRsLast);
-    st_drop(to_slot ? a.ps : a.pbuf, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, fin);
+    st_drop(to_slot ? a.ps : a.psink, (to_slot ? (uint64_t)h.slot : p) * 64 + lane, fin);
     sd = sel4(lane == j, make_uint4(h.prow_lo, h.prow_hi, (h.flags & kRsLast) ? 1u : 0u, h.slot), sd);
   }
   if (lane < 16) st_drop(a.psd, (uint64_t)(p0 + lane) * 8, sd);
