@@ -54,8 +54,6 @@ def parse():
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=8, choices=(4, 8),
                    help="--auth: waves per workgroup of the sealed message pass")
-    p.add_argument("--sealed-fused", type=int, default=0, choices=(0, 1),
-                   help="--auth: AES and BLAKE2b interleaved in the sealed message pass (1) or phased (0)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
@@ -502,7 +500,6 @@ def main():
                                       store.get_option("txn_slots")], device=dev)
     if a.auth:
         store.set_option("sealed_pass_waves", a.sealed_waves)
-        store.set_option("sealed_pass_fused", a.sealed_fused)
     g = torch.Generator(device=dev)
     g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)
@@ -665,8 +662,7 @@ def main():
             roofline = {"bound": "valu", "achieved": v_ach, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                         "frac": v_ach / VALU_PEAK_GINST if v_ach else None, "traffic": None,
                         "kernel": f"k_rpass2 AUTH (fixed-slot message-table pass, sealed rows; "
-                                  f"{a.sealed_waves} waves per workgroup"
-                                  f"{', AES and BLAKE2b interleaved' if a.sealed_fused else ''})",
+                                  f"{a.sealed_waves} waves per workgroup)",
                         "valu_insts_per_launch": insts, "kernel_ms": rpass_ms,
                         "hbm_achieved": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
                         "alg_bytes_per_launch": alg_bytes}

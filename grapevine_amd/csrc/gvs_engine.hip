@@ -256,8 +256,6 @@ struct gvs_handle {
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   int sealed_nw = 8;         // waves per workgroup of the sealed message pass (4 or 8; option)
-  int sealed_fused = 0;      // sealed message pass with AES and BLAKE2b interleaved (option; it
-                             // spills 33 VGPRs to scratch and is no faster: off by default)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -997,9 +995,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     if (e.stamp_prev != kNone)
       hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
     mark(h, "punseal");
-    if (h->sealed_fused && e.S % 512 == 0)  // two waves per SIMD, crypto interleaved (gvs_seal_fused.h)
-      hipLaunchKernelGGL((k_rpass2<8, true, true, 1, true, 8, true>), dim3(e.W), dim3(512), 0, s, a);
-    else if (h->sealed_nw == 8 && e.S % 512 == 0)  // two waves per SIMD (gvs_txn.h)
+    if (h->sealed_nw == 8 && e.S % 512 == 0)  // two waves per SIMD (gvs_txn.h)
       hipLaunchKernelGGL((k_rpass2<8, true, true, 1, true, 8>), dim3(e.W), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
@@ -2372,10 +2368,6 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
   if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 4 || value == 8)) {
     h->sealed_nw = (int)value;
-    return GVS_OK;
-  }
-  if (std::strcmp(key, "sealed_pass_fused") == 0 && (value == 0 || value == 1)) {
-    h->sealed_fused = (int)value;
     return GVS_OK;
   }
   return GVS_ERR_INVALID_ARG;

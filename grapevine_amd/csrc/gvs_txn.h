@@ -30,7 +30,6 @@
 // per-position record is written by whole-line stores (DESIGN.md §3 rules).
 #pragma once
 #include "gvs_kernels.h"
-#include "gvs_seal_fused.h"
 
 namespace gvs {
 
@@ -407,16 +406,9 @@ constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose fi
 // S must be a multiple).  The sealed pass runs 8 waves of U = 8 rows: they
 // share one AES table, so two waves per SIMD fit the CU's LDS (its VALU work
 // needs both to issue at full rate); the plain pass runs 4 waves of 16 rows.
-//
-// FUSED (AUTH, U = 8, NW = 8): the chunk's crypto runs as two fused
-// iterations (gvs_seal_fused.h), each the 8 keystream blocks of one epoch with
-// one leaf compression interleaved: (A) the read-epoch keystream with the
-// write tag of the chunk before (its ciphertext still in the stage), (B) the
-// write-epoch keystream with the read tag of this chunk.  The write tag of a
-// chunk is therefore stored one chunk later (the last one after the loop).
-template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4, bool FUSED = false>
+
+template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
-  static_assert(!FUSED || (AUTH && U == 8), "the fused pass is the sealed one, 8 rows per chunk");
   constexpr uint32_t kT = 64u * NW;  // rows per tile
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
   __shared__ uint32_t s_sh[kSlotMax];  // this batch's slot -> position of the row's first op
@@ -483,11 +475,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   uint4* sslot = a.snap + sbase * 64;
   uint4* dry = a.dry + (uint64_t)w * 256;
   const uint32_t tiles = a.S / kT;
-  // FUSED: the lane's leaf key, and the chunk whose write tag is pending
-  B2State lk{};
-  if constexpr (FUSED) lk = leaf_key128(a.sc, lane & 7u);
-  uint64_t hpend[2] = {0, 0}, prev_r0 = 0;
-  bool have_prev = false;
   for (uint32_t t = 0; t < tiles; ++t) {
     uint32_t xc = 0;
     const uint32_t rb = t * kT + wave * 64;
@@ -509,56 +496,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       const uint64_t r0 = rowbase + rj;  // physical row of v[0]
       const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
       const bool first = t == 0 && j == 0 && wave == 0;
-      if constexpr (FUSED) {
-        const LdsTe te = lds_te(s_te);
-        // one copy of the fused code: phase 0 = (A), phase 1 = (B)
-#pragma unroll 1
-        for (uint32_t ph = 0; ph < 2; ++ph) {
-          uint64_t m[16], dig[2], tg[2];
-          uint4 ks[8];
-          // the leaf to hash, then the chunk (ciphertext in (A), plaintext in
-          // (B)) waits in the stage instead of registers while the fused code runs
-          stage_leaf8(st, m);
-          wave_lds_sync();
-          stage_rows<U>(v, st);
-          fused_ks8_leaf(a.sc, te, 0u, r0, a.sc.epoch + ph, lk, m, ks, dig);
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] = xor4(st[stage_slot(u, lane)], ks[u]);
-          const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
-          const uint64_t hh[2] = {ph ? hvr[0] : hpend[0], ph ? hvr[1] : hpend[1]};
-          tag_finish8(dig, hh, tg);
-          const uint32_t ur = (lane >> 2) & 7u;
-          if (ph == 0) {
-            if (have_prev && (lane & 3u) == 0u && lane < 32u)
-              a.mtag[prev_r0 + ur] = make_uint4((uint32_t)tg[0], (uint32_t)(tg[0] >> 32), (uint32_t)tg[1],
-                                                (uint32_t)(tg[1] >> 32));
-            xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
-                                            s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
-          } else {
-            const uint4 want = a.mtag[r0 + ur];
-            if (__ballot(lane < 32u && (u4lo(want) != tg[0] || u4hi(want) != tg[1])) != 0ull && lane == 0)
-              atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-            wave_lds_sync();
-            stage_rows<U>(v, st);  // the new ciphertext: its tag is taken by the next (A)
-            const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
-            hpend[0] = hsr[0];
-            hpend[1] = hsr[1];
-            prev_r0 = r0;
-            have_prev = true;
-          }
-        }
-      } else {
-        if (AUTH) {
-          const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
-          if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
-            atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-        }
-        xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
-                                        s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
-        if (AUTH) {
-          const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
-          wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
-        }
+      if (AUTH) {
+        const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
+        if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
+          atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
+      }
+      xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+                                      s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
+      if (AUTH) {
+        const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
+        wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -580,15 +527,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
       __syncthreads();
       if (tid == 0) s_xt = tot;
     }
-  }
-  if constexpr (FUSED) {  // the write tag of the wave's last chunk
-    uint64_t m[16], dig[2], tg[2];
-    stage_leaf8(st, m);
-    leaf_prf128(lk, m, dig);
-    tag_finish8(dig, hpend, tg);
-    if ((lane & 3u) == 0u && lane < 32u)
-      a.mtag[prev_r0 + ((lane >> 2) & 7u)] =
-          make_uint4((uint32_t)tg[0], (uint32_t)(tg[0] >> 32), (uint32_t)tg[1], (uint32_t)(tg[1] >> 32));
   }
   // unused slots (slots are dense from 0: [np, c) were not used by the
   // previous batch): every slot's final-state line is read once per pass
