@@ -512,6 +512,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
         // plain rows written through (st_stream); sealed rows non-temporal:
         // written through, the sealed pass's FETCH_SIZE spread 4x wider
         // between identical batches (profiles/r04l_auth_store_policy.txt)
+#ifdef GVS_DIAG_AUTH_ROW_AUX  // diagnostic builds only: the sealed rows' store cache bits
+        if (AUTH) {
+          const v4u x = {v[u].x, v[u].y, v[u].z, v[u].w};
+          __builtin_amdgcn_raw_buffer_store_b128(x, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, -1, 0x00020000),
+                                                 ((rj + u) * 64 + lane) * 16u, 0, GVS_DIAG_AUTH_ROW_AUX);
+        } else
+#endif
         if (NTS && !AUTH) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
         else st_row<NTS>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
       }
