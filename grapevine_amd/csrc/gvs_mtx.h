@@ -146,16 +146,17 @@ struct GroupM {  // 64 B
 };
 
 // group of (hi, glo) among g[0, ng) (sorted), or -1: a fixed-step search
-__device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint64_t hi, uint64_t glo) {
+// (g holds cm + 1 entries: the slots and the sink g[cm])
+__device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, uint64_t hi, uint64_t glo) {
   uint32_t pos = 0;
 #pragma unroll
   for (uint32_t step = kGroupMax; step > 0; step >>= 1) {
     const uint32_t c = pos + step;
-    const GroupM& G = g[min(c - 1, (uint32_t)kGroupMax)];
+    const GroupM& G = g[min(c - 1, cm)];
     const bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
     pos = (c <= ng && less) ? c : pos;
   }
-  const GroupM& G = g[min(pos, (uint32_t)kGroupMax)];
+  const GroupM& G = g[min(pos, cm)];
   return (pos < ng && G.hi == hi && G.glo == glo) ? (int)pos : -1;
 }
 
@@ -171,12 +172,12 @@ __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uin
     if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
-    const int kf = find_group_m(g, ng, hi, w1 >> 23);  // every row: no code skipped
+    const int kf = find_group_m(g, ng, a.cm, hi, w1 >> 23);  // every row: no code skipped
     const int k = occ ? kf : -1;
     atomicAdd(s_occ, occ ? 1u : 0u);
-    // rows without a group write the sink entry g[kGroupMax]: the same code
-    // runs whatever the batch holds (instruction fetch shows in FETCH_SIZE)
-    const uint32_t kk = k >= 0 ? (uint32_t)k : (uint32_t)kGroupMax;
+    // rows without a group write the sink entry g[cm]: the same code runs
+    // whatever the batch holds (instruction fetch shows in FETCH_SIZE)
+    const uint32_t kk = k >= 0 ? (uint32_t)k : a.cm;
     g[kk].slot = (int32_t)j;
     g[kk].len = (uint32_t)(w1 >> 1) & 63u;
     s_sg[j] = (int16_t)k;
@@ -260,7 +261,10 @@ __device__ inline uint32_t spread_lo(uint32_t i, uint32_t n, uint32_t d) { retur
 // pops, 2 admitted as a new mailbox), row}; lanes 2.. = the 62 ids
 template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
-  __shared__ GroupM g[kGroupMax + 1];
+  // the group slots and the sink, cm + 1 entries in dynamic LDS sized at
+  // launch (9 KiB at C3 instead of 33): more workgroups per CU
+  extern __shared__ uint4 s_dyn[];
+  GroupM* g = reinterpret_cast<GroupM*>(s_dyn);
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
   __shared__ uint32_t s_ng, s_occ, s_empt, s_w[4], s_tw[kRowWaves];
@@ -683,7 +687,10 @@ __device__ inline uint4 m2_row(uint4 v, bool matched, uint32_t len, uint32_t dp,
 
 template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
-  __shared__ GroupM g[kGroupMax + 1];
+  // the group slots and the sink, cm + 1 entries in dynamic LDS sized at
+  // launch (9 KiB at C3 instead of 33): more workgroups per CU
+  extern __shared__ uint4 s_dyn[];
+  GroupM* g = reinterpret_cast<GroupM*>(s_dyn);
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
   GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
@@ -779,7 +786,8 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   uint4* wst = AUTH ? st : s_wst[AUTH ? 0 : wave];
   // one iteration: a touched row (bit set: its row in v is replaced) or a
   // slot no row takes (bit 0: the same work, nothing kept)
-  auto step = [&](uint4 (&v)[kMU], uint4 (&sd)[kMU], uint32_t bit, uint32_t j0, uint32_t di) {
+  // mine: lane u < kMU holds row u's side entry
+  auto step = [&](uint4 (&v)[kMU], uint4& mine, uint32_t bit, uint32_t j0, uint32_t di) {
     const bool slot_it = bit == 0u;
     uint4 cur = v[0];
 #pragma unroll
@@ -803,31 +811,27 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
                                               (uint32_t)(w1 >> 32)),
                            make_uint4(0, 0, 0, 0));
 #pragma unroll
-    for (int uu = 0; uu < kMU; ++uu) {  // a slot iteration has bit 0: no change
-      v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
-      sd[uu] = sel4((bit >> uu) & 1u, nsd, sd[uu]);
-    }
+    for (int uu = 0; uu < kMU; ++uu) v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);  // a slot iteration has bit 0
+    mine = sel4(bit != 0u && lane == ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u), nsd, mine);
   };
   uint32_t ci = 0;  // the wave's chunk index
   for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU, ++ci) {
     if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
-    uint4 v[kMU], sd[kMU];
+    uint4 v[kMU];
     uint32_t mm = 0;
 #pragma unroll
     for (int u = 0; u < kMU; ++u) {
       const bool in = j0 + u < a.Sr;  // wave-uniform
       v[u] = va[u];
-      sd[u] = in ? side[j0 + u] : make_uint4(0, 0, 0, 0);
       mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
     }
+    // the chunk's side entries, one per lane u < kMU: one whole-line load
+    uint4 mine = (!AUTH && lane < (uint32_t)kMU && j0 + lane < a.Sr) ? side[j0 + lane] : make_uint4(0, 0, 0, 0);
     if (AUTH) {
       m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
       const uint64_t r0 = (uint64_t)q * a.Sr + j0;
-      uint4 mine = make_uint4(0, 0, 0, 0);
       if (lane < (uint32_t)kMU)
         mine = xor4(st[kMU * 4 * kSegU4 + lane], side_keystream(a.sc, s_te, r0 + lane, a.sc.epoch));
-#pragma unroll
-      for (int u = 0; u < kMU; ++u) sd[u] = shfl4(mine, u);
     }
     mm = __builtin_amdgcn_readfirstlane(mm);
     // the chunk's touched rows, then its share of the slot iterations
@@ -837,14 +841,11 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     for (uint32_t r = 0; r < nr; ++r) {
       const uint32_t low = mq & (0u - mq);
       mq &= mq - 1u;
-      step(v, sd, low, j0, d0 + dlo + (r - nt));
+      step(v, mine, low, j0, d0 + dlo + (r - nt));
     }
     if (AUTH) {
       const uint64_t r0 = (uint64_t)q * a.Sr + j0;
       const uint32_t ep = a.sc.epoch + 1u;
-      uint4 mine = sd[0];
-#pragma unroll
-      for (int u = 1; u < kMU; ++u) mine = sel4(lane == (uint32_t)u, sd[u], mine);
       if (lane < (uint32_t)kMU) {
         const uint4 ct = xor4(mine, side_keystream(a.sc, s_te, r0 + lane, ep));
         st[kMU * 4 * kSegU4 + lane] = ct;
@@ -854,9 +855,6 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     }
     if (!AUTH) {  // the chunk's side entries: one store, kMU lanes (one whole line at kMU = 8;
                   // eight 16-B stores of one line from one lane left partial lines behind)
-      uint4 mine = sd[0];
-#pragma unroll
-      for (int u = 1; u < kMU; ++u) mine = sel4(lane == (uint32_t)u, sd[u], mine);
       if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
     }
 #pragma unroll
@@ -866,10 +864,10 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     }
   }
   if (nch == 0) {  // a wave with no rows (partitions under 4 chunks): its slot iterations here
-    uint4 v[kMU], sd[kMU];
+    uint4 v[kMU], mine = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kMU; ++u) v[u] = sd[u] = make_uint4(0, 0, 0, 0);
-    for (uint32_t r = 0; r < dn; ++r) step(v, sd, 0u, 0u, d0 + r);
+    for (int u = 0; u < kMU; ++u) v[u] = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < dn; ++r) step(v, mine, 0u, 0u, d0 + r);
   }
   // every workgroup adds, zero included: a fixed set of atomics
   if (tid == 0)
