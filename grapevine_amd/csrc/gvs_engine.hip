@@ -1076,7 +1076,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   if (h->auth)
     hipLaunchKernelGGL(k_m2x<true>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
   else
-    hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+    hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + e.Sr * sizeof(uint4), s,
+                       margs2(h, e));
   if (d_out && n)
     hipLaunchKernelGGL(k_out, dim3((n + 4 * kCopyPerWave - 1) / (4 * kCopyPerWave)), dim3(256), 0, s,
                        (const uint4*)e.resp, n, d_out);

@@ -161,14 +161,16 @@ __device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, ui
 }
 
 // occupied rows of the partition -> groups, every side entry read (AUTH:
-// decrypted here, authenticated with its row later)
+// decrypted here, authenticated with its row later); s_keep (LDS, or null)
+// keeps the entries as read, so that a later use does not read them again
 template <bool AUTH>
 __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uint32_t ng,
                                       int16_t* s_sg, uint8_t* s_occb, uint32_t* s_occ,
-                                      const uint32_t* s_te) {
+                                      const uint32_t* s_te, uint4* s_keep = nullptr) {
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
     const uint64_t row = (uint64_t)q * a.Sr + j;
     uint4 sd = a.side[row];
+    if (s_keep) s_keep[j] = sd;
     if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
@@ -687,10 +689,16 @@ __device__ inline uint4 m2_row(uint4 v, bool matched, uint32_t len, uint32_t dp,
 
 template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
-  // the group slots and the sink, cm + 1 entries in dynamic LDS sized at
-  // launch (9 KiB at C3 instead of 33): more workgroups per CU
+  // dynamic LDS sized at launch: (plain) the partition's Sr side entries as
+  // the prepass read them, then the group slots and the sink, cm + 1 entries
+  // (9 KiB at C3 instead of 33): more workgroups per CU.  The side entries are
+  // read from HBM once: read again in the row stream, their lines were
+  // fetched twice or once depending on what the stream had evicted meanwhile,
+  // i.e. on the batch's timing (FETCH_SIZE -16 KiB under hot and all-miss
+  // mixes, profiles/r04x_m2x_read_counters.txt)
   extern __shared__ uint4 s_dyn[];
-  GroupM* g = reinterpret_cast<GroupM*>(s_dyn);
+  uint4* s_side = s_dyn;
+  GroupM* g = reinterpret_cast<GroupM*>(s_dyn + (AUTH ? 0u : a.Sr));
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
   GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
@@ -720,7 +728,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     s_delta = 0;
   }
   __syncthreads();
-  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te, AUTH ? nullptr : s_side);
   __syncthreads();
   // final lengths; pending = groups with no row that end non-empty
   for (uint32_t k = tid; k < a.cm; k += 256) {
@@ -825,8 +833,8 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       v[u] = va[u];
       mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
     }
-    // the chunk's side entries, one per lane u < kMU: one whole-line load
-    uint4 mine = (!AUTH && lane < (uint32_t)kMU && j0 + lane < a.Sr) ? side[j0 + lane] : make_uint4(0, 0, 0, 0);
+    // the chunk's side entries, one per lane u < kMU, as the prepass read them
+    uint4 mine = (!AUTH && lane < (uint32_t)kMU && j0 + lane < a.Sr) ? s_side[j0 + lane] : make_uint4(0, 0, 0, 0);
     if (AUTH) {
       m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
       const uint64_t r0 = (uint64_t)q * a.Sr + j0;
