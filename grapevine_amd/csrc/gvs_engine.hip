@@ -132,6 +132,7 @@ struct Engine {
   uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
   uint4* msnap = nullptr;    // Q*cm x 1 KiB
   uint4* msnapp = nullptr;   // B x 1 KiB (group snapshots by head position)
+  uint4* mpid = nullptr;     // B x 16 B: each sorted position's message id (k_gtx, for k_m1r_c)
   uint4* mdry = nullptr;     // Q x 8 KiB (k_m1x / k_m2x: one 1 KiB per dry use)
   uint4* m2tx = nullptr;     // (Q*cm + B) x 1152 B
   GtxV* gtx_agg = nullptr;
@@ -597,6 +598,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(gtx, (QC + B) * 8);
     A(msnap, QC * 64);
     A(msnapp, (uint64_t)B * 64);
+    A(mpid, B);
     A(mdry, (uint64_t)e.Q * kMDryU4);
     A(m2tx, (QC + B) * kVLineU4);
     A(gtx_agg, B / kScanT);
@@ -911,6 +913,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   {
     GtxArgs a{e.s1keys, e.ops, e.mpos, e.gtx, e.gtx_agg, e.gtx_carry, e.scal,
               B,        e.Q,   e.logQ, e.cm,  B / kScanT, e.stamp_run};
+    a.mpid = e.mpid;
     hipLaunchKernelGGL(k_scan_a<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_b<GtxOp>, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_c<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
@@ -926,6 +929,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     a.mpos = e.mpos;
     a.ops = e.ops;
     a.msnapp = e.msnapp;
+    a.mpid = e.mpid;
     a.m1out = e.m1out;
     a.N = e.N;
     a.kc = e.kc;

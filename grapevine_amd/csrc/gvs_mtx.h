@@ -50,6 +50,7 @@ struct GtxArgs {
   GtxV* carry;
   Scal* scal;
   uint32_t B, Q, logQ, cm, nblk, stamp;
+  uint4* mpid;         // B: each position's message id (OpState words 10..13), for k_m1r_c
 };
 
 struct GtxOp {
@@ -122,6 +123,7 @@ struct GtxOp {
     wave_load128(stage, reinterpret_cast<const uint4*>(a.ops + seq), ol);
     const uint32_t* ow = reinterpret_cast<const uint32_t*>(ol);
     const uint64_t glo = s1_group(k.lo);
+    a.mpid[p] = make_uint4(ow[10], ow[11], ow[12], ow[13]);
     uint4 rec[8];
     rec[0] = make_uint4(a.stamp, in.n_next, in.n_del, in.n_create);
     rec[1] = make_uint4(in.n_x, in.fcs, in.g0, in.c1);
@@ -398,6 +400,7 @@ struct M1rArgs {
   const uint4* mpos;
   const OpState* ops;
   const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions
+  const uint4* mpid;    // B x 16 B: each position's message id (k_gtx)
   M1Out* m1out;
   uint64_t N;
   KeyCtx kc;
@@ -449,6 +452,11 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
   // the wave's 16 MPOS records in one load (two whole lines), op j's to every
   // lane by a shuffle; each op's own MSNAPP line, read once
   const uint4 mp_l = a.mpos[p0 + (lane & 15u)];
+  // the 16 ops' ids by position (k_gtx copied them there from the OpStates it
+  // reads anyway): read by seq here, the OpState lines came in the sort's
+  // order, and runs of ascending seqs under the hot and all-miss mixes made
+  // the kernel 3 us faster (profiles/r04z_timing_c3_store.txt)
+  const uint4 id_l = a.mpid[p0 + (lane & 15u)];
   uint4 As[16];
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
@@ -477,8 +485,7 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
     const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
     const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;
     const uint4 A = As[j];
-    const uint4 ol = line_load(a.ops + ((a.diag & 2u) ? p : seq));  // OpState: id is 32-bit words 10..13
-    const uint4 myid = make_uint4(line_u32(ol, 10), line_u32(ol, 11), line_u32(ol, 12), line_u32(ol, 13));
+    const uint4 myid = uni4(shfl4(id_l, (int)j));
     const uint4 pf = sel4(head, make_uint4(1u, 0u, 0u, 0u), cf);
     const uint4 pv = sel4(head, A, cv);
     const uint4 hdr = uni4(shfl4(pv, 0));
