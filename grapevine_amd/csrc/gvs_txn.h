@@ -196,27 +196,42 @@ struct RtxOp {
   // 32-bit arithmetic and selects only: a 64-bit division expands to a branch
   // on the dividend's high word, and a branch around it for null rows would
   // skip code by the data (instruction fetch shows in FETCH_SIZE)
-  __device__ static void row_of(const Args& a, uint32_t p, uint64_t& row, uint32_t& w) {
-    const uint64_t k = a.rkeys[p];
+  __device__ static void row_of_key(const Args& a, uint64_t k, uint64_t& row, uint32_t& w) {
     const uint64_t n = (uint64_t)a.W * a.S;
     const bool valid = (k >> 22) < n;  // never index past the table
     const uint32_t r32 = valid ? (uint32_t)(k >> 22) : 0u;
     row = valid ? (uint64_t)r32 : kRNullRow;
     w = valid ? r32 / a.S : a.W;
   }
-  __device__ static V local(const Args& a, uint32_t p, uint4*) {
+  // Every key this kernel needs is read from HBM once, in local() (before
+  // any record is written): each lane its own, lane 0 the one before the
+  // wave's and lane 63 the one after, the neighbours' by shuffles.  emit()
+  // takes them from the wave's stage.  Read again in emit, after the slot
+  // records (data-dependent destinations) had started to land, the key lines
+  // hit or missed L2 by the batch (FETCH_SIZE +3-8 KiB under the hot mixes,
+  // profiles/r04zd_oblivious_FETCH_SIZE_plain.txt).
+  __device__ static V local(const Args& a, uint32_t p, uint4* st) {
+    const uint32_t lane = lane_id();
+    const uint64_t k = a.rkeys[p];
+    uint64_t pk = shfl_u64(k, (int)(lane ? lane - 1u : 0u));
+    uint64_t nk = shfl_u64(k, (int)min(lane + 1u, 63u));
+    if (lane == 0u) pk = p ? a.rkeys[p - 1] : 0ull;
+    if (lane == 63u) nk = p + 1 < a.B ? a.rkeys[p + 1] : 0ull;
+    st[lane] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)nk, (uint32_t)(nk >> 32));
     uint64_t row, prow = ~0ull;
     uint32_t w, pw = ~0u;
-    row_of(a, p, row, w);
-    if (p) row_of(a, p - 1, prow, pw);
+    row_of_key(a, k, row, w);
+    if (p) row_of_key(a, pk, prow, pw);
     const bool head = row != kRNullRow && (p == 0 || row != prow);
     return V{(uint32_t)(p == 0 || w != pw), head ? 1u : 0u, head ? p : kNone, 0u};
   }
   __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
+    const uint4 kk4 = stage[lane_id()];
+    const uint64_t key = ((uint64_t)kk4.y << 32) | kk4.x, nkey = ((uint64_t)kk4.w << 32) | kk4.z;
     uint64_t row, nrow = ~0ull;
     uint32_t w, nw;
-    row_of(a, p, row, w);
-    if (p + 1 < a.B) row_of(a, p + 1, nrow, nw);
+    row_of_key(a, key, row, w);
+    if (p + 1 < a.B) row_of_key(a, nkey, nrow, nw);
     const bool null = row == kRNullRow;
     const bool head = loc.cnt != 0u;
     const bool last = !null && (p + 1 == a.B || nrow != row);
@@ -227,7 +242,7 @@ struct RtxOp {
     if (head && k >= a.c) atomicOr(&a.scal->error, kRErr);
     const uint32_t kk = min(k, a.c - 1u);
     const uint32_t o = null ? 0u : (uint32_t)(row - (uint64_t)w * a.S);
-    const uint32_t seq = (uint32_t)a.rkeys[p] & kSeqMask;
+    const uint32_t seq = (uint32_t)key & kSeqMask;
     a.rpos[p] = make_uint4(seq | (head ? kPosHead : 0u) | (last ? kPosLast : 0u) | (null ? kPosNull : 0u),
                            null ? kNone : w * a.c + kk, w, o);
     // the row's LAST op writes the slot descriptor: the row, the stamp, the
