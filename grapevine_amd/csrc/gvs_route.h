@@ -237,9 +237,17 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
     const uint32_t i = min(i0 + r, n - 1u);
     const uint32_t p = pos[i];
     // an overflowed batch (p == kNone) fails as a whole; out is then undefined
+    // the status word's and the time word's 128-B lines are each read whole,
+    // by 8 lanes in one instruction, and the word taken by a shuffle: a 16-B
+    // read of a line was fetched as 32 or 64 B depending on the requests in
+    // flight, which follow the batch's routing (FETCH_SIZE -6..-28 KiB under
+    // the hot mixes, profiles/r04ze_oblivious_FETCH_SIZE_routed.txt)
     v[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + lane] : make_uint4(0, 0, 0, 0);
-    tw[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + 64] : make_uint4(0, 0, 0, 0);
-    uint4 ts = in[(uint64_t)i * kAbiU4 + 5];  // the request's server time (record word 5)
+    const uint4 tl = p != kNone ? back[(uint64_t)p * kSlotU4 + 64 + (lane & 7u)] : make_uint4(0, 0, 0, 0);
+    tw[r] = shfl4(tl, 0);
+    const uint64_t tsa = (uint64_t)i * kAbiU4 + 5;  // the request's server time (record word 5)
+    const uint4 tsl = in[(tsa & ~7ull) + (lane & 7u)];
+    uint4 ts = shfl4(tsl, (int)(tsa & 7u));
     // pinned: only shed requests use ts and only the others the slot, and the
     // compiler would otherwise load each under its condition (the time word's
     // line was then read once per shed request: FETCH_SIZE followed the mix)
