@@ -31,6 +31,7 @@
 #include "gvs_omap.h"
 #include "gvs_wire.h"
 #include "gvs_sr25519.h"
+#include "gvs_spass.h"
 
 using namespace gvs;
 
@@ -230,6 +231,9 @@ struct Bounce {
     size_t bytes;
   };
   std::vector<Out> pend;  // device -> pinned copies enqueued, to hand to the caller after the sync
+  // a DMA from or into a slot may still be in flight: a call that failed after
+  // enqueuing returns without the stream sync of finish()
+  bool inflight = false;
 };
 
 struct gvs_handle {
@@ -573,7 +577,7 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(rpos, B);
     A(rsb, (uint64_t)B * 8);
     A(snap, WC * 64);
-    A(pbuf, (uint64_t)B * 64);
+    if (h->auth) A(pbuf, (uint64_t)B * 64);  // sealed P (plain final states go to PS)
     A(psd, (uint64_t)B * 8);
     if (h->auth) A(ptag, B);
     A(ps, (WC + B) * (h->auth ? 72 : 64));  // W*c slots + B sink lines (AUTH: then their side-entry lines)
@@ -826,24 +830,6 @@ static AllocArgs aargs(const Engine& e) {
   return a;
 }
 
-// Diagnostic kernel variants (GVS_DIAG bits; honoured by the test library only,
-// results are then wrong by design: tools/gpu_pmc_mix.sh attribution runs).
-#ifndef GVS_DIAG_RP_NTL
-#define GVS_DIAG_RP_NTL true  // diagnostic builds only: the plain pass's load / store policy
-#define GVS_DIAG_RP_NTS true
-#endif
-#ifdef GVS_TEST_HOOKS
-static uint32_t diag_bits() {
-  static const uint32_t d = [] {
-    const char* v = std::getenv("GVS_DIAG");
-    return v ? (uint32_t)std::strtoul(v, nullptr, 0) : 0u;
-  }();
-  return d;
-}
-#else
-static uint32_t diag_bits() { return 0u; }
-#endif
-
 // ------------------------------------------- pipeline 2: fixed-slot transactions
 
 static MArgs margs2(const gvs_handle* h, const Engine& e) {
@@ -855,11 +841,14 @@ static MArgs margs2(const gvs_handle* h, const Engine& e) {
   a.mdry = e.mdry;
   a.stamp = e.stamp_run;
   a.cm = e.cm;
-  // a prime under 2^12 (slot x * it stays below 2^32) not dividing Q*cm
-  const uint32_t qc = e.Q * e.cm;
+  // a prime not dividing Q*cm (so x -> x * m mod Q*cm is a permutation) with
+  // Q*cm * m below 2^32 (gvs_mtx.h computes slot x * m in 32 bits): the
+  // largest such prime of the list, 1 when none is
+  const uint64_t qc = (uint64_t)e.Q * e.cm;
   a.sink_mul = 1;
-  for (uint32_t m : {4093u, 4091u, 4079u})
-    if (qc % m != 0u) {
+  for (uint32_t m : {4093u, 4091u, 4079u, 2039u, 2029u, 1021u, 1019u, 509u, 503u, 251u, 241u, 127u, 113u,
+                     61u, 59u, 31u, 29u, 13u, 11u, 7u, 5u, 3u})
+    if (qc % m != 0u && qc * m < (1ull << 32)) {
       a.sink_mul = m;
       break;
     }
@@ -889,6 +878,17 @@ static void vscan_abc(hipStream_t s, const typename Op::Args& a) {
 static PsealArgs pargs(const gvs_handle* h, const Engine& e, uint32_t ep) {
   return PsealArgs{e.pbuf, e.psd, e.ptag, seal_of(h, e), h->te, e.scal, ep,
                    e.ps, e.ps + ((uint64_t)e.W * e.c + e.B) * 64, e.W * e.c};
+}
+
+// Sealed stores stage every slot line of a partition in LDS when c fits
+// (gvs_spass.h); the two batches' slots then share kSpBufs buffers, which
+// k_sjoint checks before any state changes.
+static bool sealed_staged(const Engine& e) { return e.c <= kSpSlots; }
+
+static void launch_sjoint(gvs_handle* h, Engine& e) {
+  if (!h->auth || !sealed_staged(e)) return;
+  hipLaunchKernelGGL(k_sjoint, dim3((e.W + 3) / 4), dim3(256), 0, h->stream, (const uint4*)e.tbuf[e.par ^ 1],
+                     (const uint4*)e.tbuf[e.par], e.stamp_prev, e.stamp_run, e.W, e.S, e.c, kSpBufs, e.scal);
 }
 
 // Phase A of pipeline 2: phase_a's kernels, then allocation, the message-pass
@@ -933,7 +933,6 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     a.m1out = e.m1out;
     a.N = e.N;
     a.kc = e.kc;
-    a.diag = diag_bits();
     vscan_abc<M1rOp>(s, a);
     hipLaunchKernelGGL(k_m1r_c, dim3(a.nvb), dim3(256), 0, s, a);
   }
@@ -954,6 +953,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
+  launch_sjoint(h, e);
   mark(h, "rtx");
   GVS_HIP(h, hipGetLastError());
   return GVS_OK;
@@ -989,7 +989,6 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   a.cutoff = h->cutoff;
   a.xbuf = e.X ? e.xb2[e.par] : nullptr;
   a.xprev = e.X ? e.xb2[e.par ^ 1] : nullptr;
-  a.diag = diag_bits();
   if (h->auth) {
     a.sc = seal_of(h, e);
     a.te = h->te;
@@ -999,22 +998,17 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     if (e.stamp_prev != kNone)
       hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
     mark(h, "punseal");
-    if (h->sealed_nw == 8 && e.S % 512 == 0)  // two waves per SIMD (gvs_txn.h)
-      hipLaunchKernelGGL((k_rpass2<8, true, true, 1, true, 8>), dim3(e.W), dim3(512), 0, s, a);
+    if (!sealed_staged(e))  // more slots than LDS stages: slot lines in the stream
+      hipLaunchKernelGGL((k_spass<8, false>), dim3(e.W), dim3(512), 0, s, a);
+    else if (h->sealed_nw == 4)
+      hipLaunchKernelGGL((k_spass<4, true>), dim3(e.W), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((k_rpass2<16, true, true, 1, true>), dim3(e.W), dim3(256), 0, s, a);
-  } else if (e.c <= kStageSlots && e.S % (16 * 8) == 0 && !(a.diag & 1024u)) {
+      hipLaunchKernelGGL((k_spass<8, true>), dim3(e.W), dim3(512), 0, s, a);
+  } else if (e.c <= kStageSlots && e.S % (16 * 8) == 0) {
     // the fixed-schedule pass: slot lines staged in LDS (gvs_txn.h k_rpass2s)
-    hipLaunchKernelGGL((k_rpass2s<16, 8, GVS_DIAG_RP_NTL>), dim3(e.W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_rpass2s<16, 8>), dim3(e.W), dim3(512), 0, s, a);
   } else {
-    hipLaunchKernelGGL((k_rpass2<16, GVS_DIAG_RP_NTL, GVS_DIAG_RP_NTS, 2>), dim3(e.W), dim3(256), 0, s, a);
-    if (a.diag & 32u)  // diagnostic: the pass again on the same inputs (results wrong)
-      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
-    if (a.diag & 64u) {  // diagnostic: again as a pure stream (no slot work: idempotent)
-      R2Args b = a;
-      b.diag |= 16u;
-      hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, b);
-    }
+    hipLaunchKernelGGL((k_rpass2<16, true, true, 2>), dim3(e.W), dim3(256), 0, s, a);
   }
 }
 
@@ -1351,7 +1345,7 @@ static int kv_engine_init(gvs_handle* h, Engine& e, uint64_t N, uint32_t B) {
   for (int k = 0; k < 2; ++k) A(tbuf[k], (WC + B) * 8);
   A(snap, WC * 64);
   A(snapp, (uint64_t)B * 64);
-  A(pbuf, (uint64_t)B * 64);
+  if (h->auth) A(pbuf, (uint64_t)B * 64);  // sealed P (plain final states go to PS)
   A(psd, (uint64_t)B * 8);
   A(ps, (WC + B) * (h->auth ? 72 : 64));  // W*c slots + B sink lines (AUTH: then their side-entry lines)
   A(snapid, WC * 8);
@@ -1429,6 +1423,7 @@ static int oram_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
+  launch_sjoint(h, e);
   mark(h, "rtx");
   launch_rpass2(h, e);
   mark(h, "rpass");
@@ -1516,6 +1511,7 @@ static int omap_batch(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t n, u
     hipLaunchKernelGGL(k_scan_b<RtxOp>, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(k_scan_c<RtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
+  launch_sjoint(h, e);
   mark(h, "rtx");
   launch_rpass2(h, e);
   mark(h, "rpass");
@@ -1675,8 +1671,18 @@ static bool is_pinned(const void* p) {
   return at.type == hipMemoryTypeHost;
 }
 
+// wait for the copies of an earlier call that ended on an error path before a
+// slot is rewritten or freed
+static int bounce_quiesce(gvs_handle* h) {
+  if (!h->bounce.inflight) return GVS_OK;
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  h->bounce.inflight = false;
+  return GVS_OK;
+}
+
 static int bounce_grow(gvs_handle* h, int slot, size_t bytes) {
   Bounce& b = h->bounce;
+  if (int r = bounce_quiesce(h)) return r;
   if (b.cap[slot] >= bytes) return GVS_OK;
   if (b.buf[slot]) GVS_HIP(h, hipHostFree(b.buf[slot]));
   b.buf[slot] = nullptr;
@@ -1695,6 +1701,7 @@ static int h2d(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes
     if (int r = bounce_grow(h, slot, bytes)) return r;
     par_memcpy(h->bounce.buf[slot], src, bytes);
     src = h->bounce.buf[slot];
+    h->bounce.inflight = true;
   }
   GVS_HIP(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
   return GVS_OK;
@@ -1710,12 +1717,14 @@ static int d2h(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes
   }
   if (int r = bounce_grow(h, slot, bytes)) return r;
   GVS_HIP(h, hipMemcpyAsync(h->bounce.buf[slot], src, bytes, hipMemcpyDeviceToHost, h->stream));
+  h->bounce.inflight = true;
   h->bounce.pend.push_back(Bounce::Out{dst, slot, bytes});
   return GVS_OK;
 }
 
 // after the call's stream sync (finish): the pageable outputs, on success
 static int bounce_done(gvs_handle* h, int rc) {
+  if (rc == GVS_OK) h->bounce.inflight = false;  // finish() synchronised the stream
   if (rc == GVS_OK)
     for (const auto& o : h->bounce.pend) par_memcpy(o.dst, h->bounce.buf[o.slot], o.bytes);
   h->bounce.pend.clear();
@@ -2452,8 +2461,12 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
         for (int b = 0; b < 16; ++b) d[16 * j + b] ^= (uint8_t)(kw[b / 4] >> (8 * (b % 4)));
       }
     };
-    if (h->auth)
+    if (h->auth) {  // sealed rows in the tile layout (gvs_seal_dev.h tile_unit)
+      std::vector<uint8_t> t(phys);
+      for (uint64_t row = 0; row < N; ++row)
+        for (uint32_t b = 0; b < 64; ++b) std::memcpy(&phys[row * 1024 + b * 16], &t[tile_unit(row, b) * 16], 16);
       for (uint64_t row = 0; row < N; ++row) unseal(phys.data() + row * 1024, 0u, row);
+    }
     if (e.stamp_prev != kNone) {
       // rows the last batch changed are pending in P (applied by the next pass):
       // slot descriptor {row in partition, stamp, P position, first position};
@@ -2511,6 +2524,22 @@ int gvs_raw_size(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t* size)
   return raw_region(h, shard, region, &base, size);
 }
 
+// A sealed message / block table is stored in 8-row tiles (gvs_seal_dev.h
+// tile_unit); the raw hooks show and take it as rows (row r at r * 1024), the
+// layout of the storage format (oracle/gvs_seal.c), converting the tiles the
+// byte range covers.
+static bool tiled(const gvs_handle* h, uint32_t region) { return region == 0 && h->auth; }
+
+static int tiles_in(gvs_handle* h, const void* base, uint64_t t0, uint64_t nt, std::vector<uint8_t>& rows) {
+  std::vector<uint8_t> t(nt * 8192);
+  GVS_HIP(h, hipMemcpyAsync(t.data(), (const uint8_t*)base + t0 * 8192, t.size(), hipMemcpyDeviceToHost, h->stream));
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  rows.resize(t.size());
+  for (uint64_t r = 0; r < nt * 8; ++r)
+    for (uint32_t b = 0; b < 64; ++b) std::memcpy(&rows[r * 1024 + b * 16], &t[tile_unit(r, b) * 16], 16);
+  return GVS_OK;
+}
+
 int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset, void* dst,
                  uint64_t bytes) {
   if (!h || !dst) return GVS_ERR_INVALID_ARG;
@@ -2518,6 +2547,13 @@ int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;
   if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
+  if (tiled(h, region) && bytes) {
+    const uint64_t t0 = offset / 8192, t1 = (offset + bytes + 8191) / 8192;
+    std::vector<uint8_t> rows;
+    if (int r = tiles_in(h, base, t0, t1 - t0, rows)) return r;
+    std::memcpy(dst, &rows[offset - t0 * 8192], bytes);
+    return GVS_OK;
+  }
   GVS_HIP(h, hipMemcpyAsync(dst, (uint8_t*)base + offset, bytes, hipMemcpyDeviceToHost, h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   return GVS_OK;
@@ -2530,11 +2566,32 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;
   if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
+  if (tiled(h, region) && bytes) {
+    const uint64_t t0 = offset / 8192, t1 = (offset + bytes + 8191) / 8192;
+    std::vector<uint8_t> rows;
+    if (int r = tiles_in(h, base, t0, t1 - t0, rows)) return r;
+    std::memcpy(&rows[offset - t0 * 8192], src, bytes);
+    std::vector<uint8_t> t(rows.size());
+    for (uint64_t r = 0; r < (t1 - t0) * 8; ++r)
+      for (uint32_t b = 0; b < 64; ++b) std::memcpy(&t[tile_unit(r, b) * 16], &rows[r * 1024 + b * 16], 16);
+    GVS_HIP(h, hipMemcpyAsync((uint8_t*)base + t0 * 8192, t.data(), t.size(), hipMemcpyHostToDevice, h->stream));
+    GVS_HIP(h, hipStreamSynchronize(h->stream));
+    return GVS_OK;
+  }
   GVS_HIP(h, hipMemcpyAsync((uint8_t*)base + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   return GVS_OK;
 }
 
+
+// Set every shard's epoch (authenticated mode): tests of the epoch limit.  No
+// row is re-sealed, so a batch at the new epoch fails its tags, unless the
+// call is refused first (GVS_ERR_EPOCH_EXHAUSTED) as it must be at the limit.
+int gvs_test_set_epoch(gvs_handle* h, uint32_t epoch) {
+  if (!h || !h->auth) return GVS_ERR_INVALID_ARG;
+  for (auto& e : h->eng) e.epoch = epoch;
+  return GVS_OK;
+}
 
 // the block store's and the map's engine handles, for the raw-region hooks above
 gvs_handle* gvs_oram_test_handle(gvs_oram* o) { return o ? o->h : nullptr; }
@@ -2730,6 +2787,7 @@ int gvs_omap_access_batch(gvs_omap* o, const gvs_omap_op* ops, uint32_t n, gvs_o
   if (!o || (!ops && n) || (!out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
   gvs_handle* h = o->h;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   h->bounce.pend.clear();
   if (int r = h2d(h, 0, h->in_stage, ops, (size_t)n * sizeof(gvs_omap_op))) return r;
@@ -2742,6 +2800,7 @@ int gvs_omap_access_batch_device(gvs_omap* o, const void* d_ops, uint32_t n, voi
   if (!o || (!d_ops && n) || (!d_out && n) || n > o->h->Bsub) return GVS_ERR_INVALID_ARG;
   gvs_handle* h = o->h;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
+  if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
   const uint4* in = n ? (const uint4*)d_ops : h->in_stage;
   if (int r = omap_batch(h, h->eng[0], in, n, (uint4*)d_out)) return r;

@@ -404,7 +404,6 @@ struct M1rArgs {
   M1Out* m1out;
   uint64_t N;
   KeyCtx kc;
-  uint32_t diag;  // diagnostic variants (test library only, GVS_DIAG)
 };
 
 struct M1rOp {
@@ -480,7 +479,6 @@ __global__ __launch_bounds__(256) void k_m1r_c(M1rArgs a) {
   uint32_t my_need = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    const uint32_t p = p0 + j;
     const uint4 mp = uni4(shfl4(mp_l, (int)j));
     const uint32_t seq = mp.x & kSeqMask, cls = mpos_cls(mp.x);
     const bool head = mp.x & kMPosHead, null = mp.x & kMPosNull;

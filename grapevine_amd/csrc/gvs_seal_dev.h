@@ -26,27 +26,32 @@ __device__ inline uint32_t stage_slot(int u, uint32_t lane) {
 }
 
 
-// The AES table lives in LDS as 64 interleaved replicas: entry x of replica
-// r at byte x * 256 + 4 r.  Lane l reads replica l, so the 32 lanes of a
-// ds_read_b32 half-wave always hit 32 distinct banks whatever the (secret,
-// data-dependent) indices are: no bank conflicts, and no timing that depends
-// on the key or the plaintext through conflicts.  The table is 64 KiB-aligned,
+// The AES table lives in LDS as 32 interleaved replicas: entry x of replica
+// r at byte x * 256 + 4 r (r < 32).  Lane l reads replica l mod 32: a
+// ds_read_b32 is serviced in two half-waves {0-31}, {32-63}, banked by
+// (address / 4) mod 32 (MI355X_MICROARCH.md "LDS"), so the 32 lanes of a half
+// always hit 32 distinct banks whatever the (secret, data-dependent) indices
+// are: no bank conflicts, and no timing that depends on the key or the
+// plaintext through conflicts.  The table's 64-KiB window is 64 KiB-aligned,
 // which puts it at LDS address 0, so a lookup address is a single v_perm_b32:
-// byte 1 = the state byte, byte 0 = 4 l.
-constexpr uint32_t kTeRep = 64;
-constexpr uint32_t kTeWords = 256 * kTeRep;  // 64 KiB
+// byte 1 = the state byte, byte 0 = 4 (l mod 32).  Bytes [128, 256) of every
+// 256-B entry row are not part of the table: 256 holes of 128 B (32 KiB) that
+// the sealed message pass uses as staging space (gvs_spass.h).
+constexpr uint32_t kTeRep = 32;
+constexpr uint32_t kTeWords = 256 * 64;  // the 64-KiB window (table + holes)
 #define GVS_TE_LDS __shared__ __attribute__((aligned(65536))) uint32_t
 
 __device__ inline void load_te(uint32_t* s_te, const uint32_t* g_te) {
-  for (uint32_t i = threadIdx.x; i < kTeWords; i += blockDim.x) s_te[i] = g_te[i / kTeRep];
+  for (uint32_t i = threadIdx.x; i < 256 * kTeRep; i += blockDim.x)
+    s_te[(i / kTeRep) * 64 + (i % kTeRep)] = g_te[i / kTeRep];
 }
 
 struct LdsTe {
   const uint32_t* base;  // s_te (at LDS address 0)
-  uint32_t lane4;        // 4 * lane
+  uint32_t lane4;        // 4 * (lane mod 32)
 };
 
-__device__ inline LdsTe lds_te(const uint32_t* s_te) { return LdsTe{s_te, lane_id() * 4u}; }
+__device__ inline LdsTe lds_te(const uint32_t* s_te) { return LdsTe{s_te, (lane_id() & 31u) * 4u}; }
 
 __device__ inline uint32_t te_at(const LdsTe& t, uint32_t s, int k) {
   const uint32_t off = __builtin_amdgcn_perm(s, t.lane4, 0x0c0c0400u | ((uint32_t)(4 + k) << 8));
@@ -157,6 +162,58 @@ __device__ inline void ctr_keystream2(const AesRk& rk, const LdsTe& te, const Ct
   aes128_rounds2<2>(rk, te, a, b);
   ka = make_uint4(bswap32(a[0]), bswap32(a[1]), bswap32(a[2]), bswap32(a[3]));
   kb = make_uint4(bswap32(b[0]), bswap32(b[1]), bswap32(b[2]), bswap32(b[3]));
+}
+
+// Counter blocks j = j0 + i (i < 8, j0 a multiple of 8) of one row: they
+// differ only in byte 0 of the last word, which round 1 reads once (the
+// byte-0 lookup of word 3, into t[0]).  Round 1 once per row without that
+// term; per block one lookup (the leaf-major message pass, gvs_spass.h: lane L
+// holds blocks 8 (L & 7) .. + 7 of one row).
+struct CtrRound1J {
+  uint32_t t[4];  // round-1 output, t[0] still missing T0[x3.b0] >>> 24
+  uint32_t x3b0;  // byte 0 of x3 for j0 (x3 = (table << 24 | j) ^ rk3)
+};
+
+__device__ inline CtrRound1J ctr_round1_row(const AesRk& rk, const LdsTe& te, uint32_t table,
+                                            uint64_t row, uint32_t epoch, uint32_t j0) {
+  const uint32_t x0 = bswap32((uint32_t)row) ^ rk.w[0];
+  const uint32_t x1 = bswap32((uint32_t)(row >> 32)) ^ rk.w[1];
+  const uint32_t x2 = bswap32(epoch) ^ rk.w[2];
+  const uint32_t x3 = ((table << 24) | j0) ^ rk.w[3];
+  const uint32_t x[4] = {x0, x1, x2, x3};
+  uint32_t l[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) l[4 * i + k] = (i == 0 && k == 3) ? 0u : te_at(te, x[(i + k) & 3], 3 - k);
+  CtrRound1J c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    c.t[i] = xor3(xor3(l[4 * i], ror32(l[4 * i + 1], 8), ror32(l[4 * i + 2], 16)),
+                  ror32(l[4 * i + 3], 24), rk.w[4 + i]);
+  c.x3b0 = x3 & 0xffu;
+  return c;
+}
+
+// keystream blocks j0 + i and j0 + i + 1 of the row as little-endian words
+__device__ inline void ctr_keystream2_j(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1,
+                                        uint32_t i, uint4& ka, uint4& kb) {
+  const uint32_t ta = te_at(te, c1.x3b0 ^ i, 0);
+  const uint32_t tb = te_at(te, c1.x3b0 ^ (i + 1), 0);
+  uint32_t a[4] = {c1.t[0] ^ ror32(ta, 24), c1.t[1], c1.t[2], c1.t[3]};
+  uint32_t b[4] = {c1.t[0] ^ ror32(tb, 24), c1.t[1], c1.t[2], c1.t[3]};
+  aes128_rounds2<2>(rk, te, a, b);
+  ka = make_uint4(bswap32(a[0]), bswap32(a[1]), bswap32(a[2]), bswap32(a[3]));
+  kb = make_uint4(bswap32(b[0]), bswap32(b[1]), bswap32(b[2]), bswap32(b[3]));
+}
+
+// The tile layout of a sealed message (or block) table: rows in tiles of 8
+// (8 KiB); inside a tile, 16-B unit i * 64 + L holds block 8 (L & 7) + i of
+// row L >> 3.  A wave's coalesced load of unit i into lane L (8 whole-KiB
+// instructions) then leaves leaf L & 7 (128 B) of row L >> 3 in lane L's
+// registers: the leaf hashes need no transposition through LDS.
+__host__ __device__ constexpr uint64_t tile_unit(uint64_t row, uint32_t block) {
+  return (row >> 3) * 512 + (uint64_t)(block & 7u) * 64 + (row & 7) * 8 + (block >> 3);
 }
 
 template <int U>
@@ -401,7 +458,12 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
     else  // message tables: 8 leaves of 128 B
       wave_seal<U, 8>(c, s_te, table, r0, 0u, v, tags, false, st, hdr);
 #pragma unroll
-    for (int u = 0; u < U; ++u) rows[(r0 + u) * 64 + lane] = v[u];
+    for (int u = 0; u < U; ++u) {
+      if (side)
+        rows[(r0 + u) * 64 + lane] = v[u];
+      else  // message and block tables: the tile layout (tile_unit)
+        rows[tile_unit(r0 + u, lane)] = v[u];
+    }
   }
 }
 

@@ -292,7 +292,6 @@ struct R2Args {
   uint64_t cutoff;
   uint4* xbuf;         // records written by this pass
   const uint4* xprev;  // records being deleted by this batch (exclusion)
-  uint32_t diag;       // diagnostic variants (test library only, GVS_DIAG bits 4, 8, 16)
 };
 
 // Expiry detection on a chunk (v1 x_detect plus the exclusion of rows whose
@@ -345,9 +344,10 @@ __device__ inline uint4 ld_line(const uint4* p) { return ld_row<NTL>(p); }
 
 constexpr uint32_t kSlotMax = 1024;      // transaction slots per partition (c) at most
 
-// One chunk of U rows (partition row rj, physical row r0) of the message
-// pass, plaintext in v: apply the previous batch's final states, snapshot the
-// rows this batch touches, expiry selection.  Returns the expiry count.
+// One chunk of U rows (partition row rj) of the plain message pass's
+// fallback (more slots than k_rpass2s stages): apply the previous batch's
+// final states, snapshot the rows this batch touches, expiry selection.
+// Returns the expiry count.
 //
 // The first chunk of wave 0 (`first`) runs each loop once "dry" on the
 // workgroup's own dry line, so every workgroup executes the same code whatever
@@ -355,11 +355,11 @@ constexpr uint32_t kSlotMax = 1024;      // transaction slots per partition (c) 
 // The dry iteration is an extra mask bit (1 << U), taken last by the same loop
 // code: a loop whose first iteration were special could be peeled by the
 // compiler, and then not every workgroup would fetch the loop's code.
-template <int U, bool AUTH>
-__device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uint32_t rj, uint64_t r0,
-                                             bool first, const int16_t* s_pk, const int16_t* s_sk,
-                                             const uint32_t* s_sh, uint64_t sbase, uint4* dry,
-                                             uint32_t xc, uint4* s_xw_w, const uint4* s_xx, uint32_t nx) {
+template <int U>
+__device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uint32_t rj, bool first,
+                                             const int16_t* s_pk, const int16_t* s_sk, const uint32_t* s_sh,
+                                             uint64_t sbase, uint4* dry, uint32_t xc, uint4* s_xw_w,
+                                             const uint4* s_xx, uint32_t nx) {
   const uint32_t lane = lane_id();
   uint32_t mp = 0, ms = 0;
 #pragma unroll
@@ -369,9 +369,6 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
   }
   mp = __builtin_amdgcn_readfirstlane(mp);
   ms = __builtin_amdgcn_readfirstlane(ms);
-  if (a.diag & (16u | 128u)) mp = ms = 0u;  // diagnostic: no slot work inside the stream
-  if (a.diag & 256u) ms = 0u;                // diagnostic: no snapshot writes inside it
-  if (a.diag & 512u) mp = 0u;                // diagnostic: no final-state reads inside it
   uint32_t mq = mp | (first ? (1u << U) : 0u);
   while (mq) {  // rows the previous batch changed: its final state
     const uint32_t low = mq & (0u - mq);
@@ -380,12 +377,8 @@ __device__ inline uint32_t rpass_chunk_merge(const R2Args& a, uint4 (&v)[U], uin
     const uint32_t bit = dry_p ? 0u : low;
     const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
     const int16_t k = dry_p ? (int16_t)0 : s_pk[rj + u0];
-    const uint4* src = (dry_p || (a.diag & 12u)) ? dry : a.ps + (sbase + (uint64_t)k) * 64;
+    const uint4* src = dry_p ? dry : a.ps + (sbase + (uint64_t)k) * 64;
     const uint4 x = ld_row<true>(&src[lane]);
-    if (AUTH) {  // the final state must be the one sealed for this row
-      const uint4 sd = uni4(shfl4(line_load(dry_p ? dry + 3 * 64 : a.psds + (sbase + (uint64_t)k) * 8), 0));
-      if (!dry_p && lane == 0 && (sd.z == 0u || u4lo(sd) != r0 + u0)) atomicOr(&a.scal->error, 8u);
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
   }
@@ -416,13 +409,13 @@ constexpr uint32_t kPendTable = 0x100u;  // header table field of a row whose fi
 // flag in its header, so the next pass must find its final state in P (a
 // hidden P slot fails that row's tag); P rows are sealed as table 2, bound to
 // their position and, through their side entry, to the row they replace.
-//
-// NW waves per workgroup, 64 rows per wave per tile (tiles of 64 * NW rows;
-// S must be a multiple).  The sealed pass runs 8 waves of U = 8 rows: they
-// share one AES table, so two waves per SIMD fit the CU's LDS (its VALU work
-// needs both to issue at full rate); the plain pass runs 4 waves of 16 rows.
+// The sealed pass is k_spass (gvs_spass.h).
 
-template <int U, bool NTL, bool NTS, int MINW, bool AUTH = false, int NW = 4>
+// The plain pass's fallback (c > kStageSlots or S not a multiple of the
+// staged pass's rounds): NW waves per workgroup, 64 rows per wave per tile
+// (tiles of 64 * NW rows; S must be a multiple), U rows per chunk, the slot
+// lines read and written in the stream.
+template <int U, bool NTL, bool NTS, int MINW, int NW = 4>
 __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   constexpr uint32_t kT = 64u * NW;  // rows per tile
   __shared__ int16_t s_pk[kRowsMax], s_sk[kRowsMax];
@@ -432,13 +425,9 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
   __shared__ uint32_t s_xc[NW], s_xt;
-  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
-  __shared__ uint4 s_st[AUTH ? NW * stage_u4(U) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
-  if (AUTH) load_te(s_te, a.te);
-  uint4* st = s_st + (AUTH ? wave * stage_u4(U) : 0u);
   for (uint32_t o = tid; o < a.S; o += kT) {
     s_pk[o] = -1;
     s_sk[o] = -1;
@@ -493,48 +482,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   for (uint32_t t = 0; t < tiles; ++t) {
     uint32_t xc = 0;
     const uint32_t rb = t * kT + wave * 64;
-    // AUTH: the header PRF of the wave's 64 rows at both epochs, one row per
-    // lane; the pending flag comes from the slots of each batch
-    uint64_t hv[2] = {0, 0}, hs[2] = {0, 0};
-    if (AUTH) {
-      const uint64_t z[2] = {0, 0};
-      const uint32_t tv = s_pk[rb + lane] >= 0 ? kPendTable : 0u;
-      const uint32_t ts = s_sk[rb + lane] >= 0 ? kPendTable : 0u;
-      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch, tv, z, hv);
-      header_prf(a.sc.headk, rowbase + rb + lane, a.sc.epoch + 1u, ts, z, hs);
-    }
     for (uint32_t j = 0; j < 64; j += U) {
       uint4 v[U];
       const uint32_t rj = rb + j;
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rj + u) * 64 + lane]);
-      const uint64_t r0 = rowbase + rj;  // physical row of v[0]
-      const uint32_t hsrc = j + ((lane >> 2) & (uint32_t)(U - 1));
       const bool first = t == 0 && j == 0 && wave == 0;
-      if (AUTH) {
-        const uint64_t hvr[2] = {shfl_u64(hv[0], (int)hsrc), shfl_u64(hv[1], (int)hsrc)};
-        if (!wave_unseal<U, 8>(a.sc, s_te, 0u, r0, v, a.mtag, false, st, hvr) && lane == 0)
-          atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-      }
-      xc = rpass_chunk_merge<U, AUTH>(a, v, rj, r0, first, s_pk, s_sk, s_sh, sbase, dry, xc,
-                                      s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
-      if (AUTH) {
-        const uint64_t hsr[2] = {shfl_u64(hs[0], (int)hsrc), shfl_u64(hs[1], (int)hsrc)};
-        wave_seal<U, 8>(a.sc, s_te, 0u, r0, a.sc.epoch + 1u, v, a.mtag, false, st, hsr);
-      }
+      xc = rpass_chunk_merge<U>(a, v, rj, first, s_pk, s_sk, s_sh, sbase, dry, xc,
+                                s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // plain rows written through (st_stream); sealed rows non-temporal:
-        // written through, the sealed pass's FETCH_SIZE spread 4x wider
-        // between identical batches (profiles/r04l_auth_store_policy.txt)
-#ifdef GVS_DIAG_AUTH_ROW_AUX  // diagnostic builds only: the sealed rows' store cache bits
-        if (AUTH) {
-          const v4u x = {v[u].x, v[u].y, v[u].z, v[u].w};
-          __builtin_amdgcn_raw_buffer_store_b128(x, __builtin_amdgcn_make_buffer_rsrc(part, (short)0, -1, 0x00020000),
-                                                 ((rj + u) * 64 + lane) * 16u, 0, GVS_DIAG_AUTH_ROW_AUX);
-        } else
-#endif
-        if (NTS && !AUTH) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
+        if (NTS) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
         else st_row<NTS>(&part[(uint64_t)(rj + u) * 64 + lane], v[u]);
       }
     }
@@ -552,12 +510,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
   }
   // unused slots (slots are dense from 0: [np, c) were not used by the
   // previous batch): every slot's final-state line is read once per pass
-  for (uint32_t k = ((a.diag & (8u | 128u | 512u)) ? 0u : (a.diag & 4u) ? a.c : np) + wave; k < a.c; k += NW) {
+  for (uint32_t k = np + wave; k < a.c; k += NW) {
     uint4 x = ld_row<true>(&a.ps[(sbase + k) * 64 + lane]);
-    if (AUTH) x = xor4(x, uni4(shfl4(line_load(a.psds + (sbase + k) * 8), 0)));  // as a used slot's read
     keep4(x);
   }
-  for (uint32_t k = ((a.diag & (128u | 256u)) ? 0u : ns) + wave; k < a.c; k += NW) {
+  for (uint32_t k = ns + wave; k < a.c; k += NW) {
     st_drop(sslot, (uint64_t)k * 64 + lane, make_uint4(0, 0, 0, 0));
     if (lane < 8) st_drop(a.snapid, (sbase + k) * 8 + lane, make_uint4(0, 0, 0, 0));
   }

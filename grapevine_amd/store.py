@@ -36,7 +36,7 @@ EXPORTED = (
     "gvs_host_alloc", "gvs_host_free", "gvs_process_wire_batches",
 )
 TEST_EXPORTED = ("gvs_dump_messages", "gvs_raw_size", "gvs_dump_raw", "gvs_store_raw",
-                 "gvs_route_plan", "gvs_oram_test_handle", "gvs_omap_test_handle")
+                 "gvs_route_plan", "gvs_oram_test_handle", "gvs_omap_test_handle", "gvs_test_set_epoch")
 
 
 def test_hooks_enabled():
@@ -102,6 +102,7 @@ def load_library(path=None):
         lib.gvs_oram_test_handle.restype = vp
         lib.gvs_omap_test_handle.argtypes = [vp]
         lib.gvs_omap_test_handle.restype = vp
+        lib.gvs_test_set_epoch.argtypes = [vp, u32]
     lib.gvs_last_error.argtypes = [vp]
     lib.gvs_set_expiry_cutoff.argtypes = [vp, ctypes.c_uint64]
     lib.gvs_last_error.restype = ctypes.c_char_p

@@ -39,6 +39,11 @@ gvs_handle *gvs_oram_test_handle(gvs_oram *o);
  * table's regions: tamper tests of the sealed map. */
 gvs_handle *gvs_omap_test_handle(gvs_omap *m);
 
+/* Set the storage epoch of every shard (authenticated mode only), without
+ * re-sealing anything: tests that a store at the epoch limit refuses work
+ * with GVS_ERR_EPOCH_EXHAUSTED on every entry point. */
+int gvs_test_set_epoch(gvs_handle *h, uint32_t epoch);
+
 /* The router's placement of one source's batch, computed on
  * the host by the device's own routing function: slot[i] = d * C + (rank of
  * request i among this batch's requests for shard d), or 0xFFFFFFFF when that

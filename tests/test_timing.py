@@ -32,7 +32,7 @@ import sys
 
 import pytest
 
-from test_oblivious import PROBE, short, split_batches
+from test_oblivious import PROBE, quiesce, short, split_batches
 
 pytestmark = pytest.mark.gpu
 
@@ -42,6 +42,16 @@ SHAPES = {
     "store": dict(args=ARGS, ref="rud",
                   mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
     "expiry": dict(args=ARGS + ["--expiry", "1024"], ref="main", mixes=["main", "x_all", "x_few"]),
+    # sealed storage (BASELINE config 5 mode) at the counter
+    # test's sealed shape: 2^21 messages, 512-row partitions, the production
+    # 8-wave sealed pass
+    "auth": dict(args=["--log2n", "21", "--batch", "65536", "--identities", "200000", "--fill-batches", "3",
+                       "--auth"], ref="rud",
+                 mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
+    # the 2-shard router and the padded all-to-all in one process
+    "routed": dict(args=["--log2n", "20", "--batch", "32768", "--shards", "2", "--identities", "100000",
+                         "--fill-batches", "3"], ref="rud",
+                   mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
 }
 SEEDS = (1234, 99, 5)
 PER_SEED = 2
@@ -55,6 +65,7 @@ def kernel_trace(mix, outdir, args):
     if shutil.which("rocprofv3") is None:
         pytest.skip("rocprofv3 not available")
     os.makedirs(outdir, exist_ok=True)
+    quiesce(f"timing/{os.path.basename(outdir)}")
     cmd = (["rocprofv3", "--kernel-trace", "-d", outdir, "-o", "run", "--output-format", "csv", "--",
             sys.executable, PROBE, mix, "--seeds", ",".join(map(str, SEEDS)), "--batches", str(PER_SEED)]
            + args)
@@ -127,3 +138,11 @@ def test_kernel_durations_independent_of_mix(tmp_path):
 
 def test_kernel_durations_independent_of_expiry(tmp_path):
     check_durations("expiry", tmp_path)
+
+
+def test_kernel_durations_independent_of_mix_sealed(tmp_path):
+    check_durations("auth", tmp_path)
+
+
+def test_kernel_durations_independent_of_mix_routed(tmp_path):
+    check_durations("routed", tmp_path)

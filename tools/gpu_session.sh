@@ -5,6 +5,9 @@
 #   bench    bench.py (default workload)
 #   obl      the obliviousness counter tests (plain shapes)
 #   all      tests, bench, timing
+#   seal     the sealed-storage GPU tests (message store, block store, map, epoch limit)
+#   sealobl  seal, then the sealed shape's counter tests and a sealed bench line
+#   driver   the driver's round-end command (pytest tests/ -x -q -m gpu)
 # Each GPU step runs under its own time limit.  A pytest exit status of 1
 # means failed tests (recorded, the session goes on); anything else (time
 # limit, abort, crash) ends the session.
@@ -26,7 +29,13 @@ PT="python3 -u -m pytest -v --timeout 600 --timeout-method thread -p no:cachepro
 tests() { step gpu_tests 600 $PT tests -m gpu --ignore=tests/test_oblivious.py --ignore=tests/test_timing.py "$@"; }
 timing() { step timing_c3 300 $PT tests/test_timing.py; cp gpurun_out/timing_c3.txt "$O/" 2>/dev/null; }
 bench() { step bench 300 python3 bench.py; }
+SEALT="tests/test_gpu_seal.py tests/test_gpu_oram.py tests/test_gpu_omap.py tests/test_gpu_epoch.py"
 case "$2" in
+  seal) step seal_tests 600 $PT $SEALT ;;
+  sealobl) step seal_tests 600 $PT $SEALT && \
+    step oblivious_auth 900 $PT tests/test_oblivious.py -k "auth and not oram_auth and not omap_auth" && \
+    step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 ;;
+  driver) step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread ;;
   tests) tests ;;
   timing) timing ;;
   bench) bench ;;

@@ -97,7 +97,7 @@ def run_kv(a, kind):
     from grapevine_amd.store import BlockStore, KeyValueMap
     assert a.mix in KV_MIXES[kind], f"{kind} mixes: {sorted(KV_MIXES[kind])}"
     cap, B = 1 << a.log2n, a.batch
-    cfg = abi.make_oram_config(cap, max_batch=B, secret_key=KV_SECRET)
+    cfg = abi.make_oram_config(cap, max_batch=B, secret_key=KV_SECRET, auth_storage=a.auth)
     if kind == "oram":
         store, model = BlockStore(cfg), ffi.OramModel(cap)
     else:
