@@ -107,12 +107,14 @@ __device__ inline void leaf_words(const uint4 (&v)[8], uint64_t (&m)[16]) {
 }
 
 // Tag of the lane's row (leaf-major: lane L holds leaf L & 7 of row L >> 3):
-// its leaf PRF, the XOR over the row's 8 lanes, then the header H
-__device__ inline void lm_tag(const SealCtx& c, const uint4 (&v)[8], const uint64_t hdr[2], uint64_t out[2]) {
+// its leaf PRF, the XOR over the row's 8 lanes, then the header H.  The 8
+// leaf keys' states sit in LDS (s_lk, 8 x 128 B): each lane reads its own
+// instead of selecting among all eight, which held them in registers.
+__device__ inline void lm_tag(const uint64_t* s_lk, const uint4 (&v)[8], const uint64_t hdr[2], uint64_t out[2]) {
   const uint32_t leaf = lane_id() & 7u;
-  B2State k = c.leafk0[0];
+  B2State k;
 #pragma unroll
-  for (uint32_t i = 1; i < 8; ++i) k = b2_sel(leaf == i, c.leafk0[i], k);
+  for (int i = 0; i < 8; ++i) k.h[i] = s_lk[leaf * 8 + i];
   uint64_t m[16];
   leaf_words(v, m);
   uint64_t r[2];
@@ -154,10 +156,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
   __shared__ uint32_t s_xc[NW];
+  __shared__ uint64_t s_lk[8 * 8];              // the message leaves' key states (leafk0)
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
   load_te(s_lds, a.te);
+  if (tid < 64) s_lk[tid] = a.sc.leafk0[tid >> 3].h[tid & 7u];
   const uint32_t nwd = a.S / 32u;
   for (uint32_t o = tid; o < nwd; o += 64 * NW) {
     s_pbm[o] = 0u;
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         {
           const uint64_t hr[2] = {shfl_u64(hh[0], (int)rr), shfl_u64(hh[1], (int)rr)};
           uint64_t tg[2];
-          lm_tag(a.sc, v, hr, tg);
+          lm_tag(s_lk, v, hr, tg);
           const uint4 want = shfl4(tl, (int)u);
           if (__ballot((u4lo(want) != tg[0]) | (u4hi(want) != tg[1])) && lane == 0)
             atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
           lm_ctr(a.sc, te, row, a.sc.epoch + 1u, v);
           const uint64_t hw[2] = {shfl_u64(hh[0], (int)(32u + rr)), shfl_u64(hh[1], (int)(32u + rr))};
           uint64_t tg[2];
-          lm_tag(a.sc, v, hw, tg);
+          lm_tag(s_lk, v, hw, tg);
           // lane r < 8 writes row r's tag: the 8 rows' tags are one whole line
           const uint64_t t0 = shfl_u64(tg[0], (int)(8u * (lane & 7u))), t1 = shfl_u64(tg[1], (int)(8u * (lane & 7u)));
           if (lane < 8u)

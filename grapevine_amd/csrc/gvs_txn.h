@@ -546,45 +546,29 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_rpass2(R2Args a) {
 // kStageSlots slots (2 x 65 KiB of LDS: one workgroup of NW waves per CU).
 constexpr uint32_t kStageSlots = 64;
 
+// Every row of every chunk does the same LDS work, used or not (DESIGN.md §3
+// rule 10): it reads a final state (its slot's, or the dry slot's, kept only
+// for a row the previous batch changed) and writes its snapshot (to its
+// slot, or to the dry slot).  Round 4 merged and snapshot only the touched
+// rows, one LDS loop iteration each, and the pass's duration followed how
+// many rows the batch touched (hot and all-miss mixes up to 19 us faster,
+// profiles/r04zf_timing_c3_store.txt).
 template <int U>
-__device__ inline uint32_t stage_chunk(const R2Args& a, uint4 (&v)[U], uint32_t rj, bool first,
+__device__ inline uint32_t stage_chunk(const R2Args& a, uint4 (&v)[U], uint32_t rj,
                                        const int16_t* s_pk, const int16_t* s_sk, const uint4* s_fin,
                                        uint4* s_snp, uint32_t xc, uint4* s_xw_w, const uint4* s_xx,
                                        uint32_t nx) {
   const uint32_t lane = lane_id();
-  uint32_t mp = 0, ms = 0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    mp |= s_pk[rj + u] >= 0 ? (1u << u) : 0u;
-    ms |= s_sk[rj + u] >= 0 ? (1u << u) : 0u;
+  for (int u = 0; u < U; ++u) {  // rows the previous batch changed: their final state
+    const int16_t k = s_pk[rj + u];
+    const uint32_t b = selu32(k >= 0, (uint32_t)k, kStageSlots);
+    v[u] = sel4(k >= 0, s_fin[b * 64 + lane], v[u]);
   }
-  mp = __builtin_amdgcn_readfirstlane(mp);
-  ms = __builtin_amdgcn_readfirstlane(ms);
-  // the dry iteration (an extra mask bit, taken last) uses LDS slot kStageSlots
-  uint32_t mq = mp | (first ? (1u << U) : 0u);
-  while (mq) {  // rows the previous batch changed: their final state
-    const uint32_t low = mq & (0u - mq);
-    mq &= mq - 1u;
-    const bool dry_p = low == (1u << U);
-    const uint32_t bit = dry_p ? 0u : low;
-    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
-    const uint32_t k = dry_p ? kStageSlots : (uint32_t)s_pk[rj + u0];
-    const uint4 x = s_fin[k * 64 + lane];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = sel4((bit >> u) & 1u, x, v[u]);
-  }
-  uint32_t sq = ms | (first ? (1u << U) : 0u);
-  while (sq) {  // rows this batch touches: their snapshot
-    const uint32_t low = sq & (0u - sq);
-    sq &= sq - 1u;
-    const bool dry_s = low == (1u << U);
-    const uint32_t bit = dry_s ? 0u : low;
-    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
-    const uint32_t k = dry_s ? kStageSlots : (uint32_t)s_sk[rj + u0];
-    uint4 cur = v[0];
-#pragma unroll
-    for (int u = 1; u < U; ++u) cur = sel4((bit >> u) & 1u, v[u], cur);
-    s_snp[k * 64 + lane] = cur;
+  for (int u = 0; u < U; ++u) {  // rows this batch touches: their snapshot
+    const int16_t k = s_sk[rj + u];
+    s_snp[selu32(k >= 0, (uint32_t)k, kStageSlots) * 64 + lane] = v[u];
   }
   if (a.xon) xc = x_detect2<U>(a, v, s_xw_w, xc, s_xx, nx);
   return xc;
@@ -669,8 +653,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_rpass2s(R2Args a) {
     uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = ld_row<NTL>(&part[(uint64_t)(rj + u) * 64 + lane]);
-    const bool first = t == 0 && wave == 0;
-    const uint32_t xc = stage_chunk<U>(a, v, rj, first, s_pk, s_sk, s_fin, s_snp, 0u,
+    const uint32_t xc = stage_chunk<U>(a, v, rj, s_pk, s_sk, s_fin, s_snp, 0u,
                                        s_xw + wave * (kXepMax + 1) * 3, s_xx, nx);
 #pragma unroll
     for (int u = 0; u < U; ++u) st_stream(part, (uint64_t)(rj + u) * 64 + lane, v[u]);
