@@ -52,8 +52,8 @@ def parse():
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
-    p.add_argument("--sealed-waves", type=int, default=8, choices=(4, 8),
-                   help="--auth: waves per workgroup of the sealed message pass")
+    p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12),
+                   help="--auth: waves per workgroup of the sealed message pass (0: the store's choice)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
@@ -661,8 +661,8 @@ def main():
             v_ach = insts / (rpass_ms * 1e-3) / 1e9 if insts else None
             roofline = {"bound": "valu", "achieved": v_ach, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                         "frac": v_ach / VALU_PEAK_GINST if v_ach else None, "traffic": None,
-                        "kernel": f"k_rpass2 AUTH (fixed-slot message-table pass, sealed rows; "
-                                  f"{a.sealed_waves} waves per workgroup)",
+                        "kernel": f"k_spass (fixed-schedule sealed message-table pass; "
+                                  f"{a.sealed_waves or 'default'} waves per workgroup)",
                         "valu_insts_per_launch": insts, "kernel_ms": rpass_ms,
                         "hbm_achieved": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
                         "alg_bytes_per_launch": alg_bytes}

@@ -260,7 +260,7 @@ struct gvs_handle {
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
-  int sealed_nw = 8;         // waves per workgroup of the sealed message pass (4 or 8; option)
+  int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12; 0: by S)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -998,9 +998,14 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     if (e.stamp_prev != kNone)
       hipLaunchKernelGGL(k_pseal<false>, dim3(B / 64), dim3(256), 0, s, pargs(h, e, e.epoch));
     mark(h, "punseal");
+    // waves per workgroup: 12 (three per SIMD) once a partition has rounds
+    // enough to keep them busy (S >= 1024: 32 groups of 32 rows), else 8
+    const int nw = h->sealed_nw ? h->sealed_nw : (e.S >= 1024 ? 12 : 8);
     if (!sealed_staged(e))  // more slots than LDS stages: slot lines in the stream
       hipLaunchKernelGGL((k_spass<8, false>), dim3(e.W), dim3(512), 0, s, a);
-    else if (h->sealed_nw == 4)
+    else if (nw == 12)
+      hipLaunchKernelGGL((k_spass<12, true>), dim3(e.W), dim3(768), 0, s, a);
+    else if (nw == 4)
       hipLaunchKernelGGL((k_spass<4, true>), dim3(e.W), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((k_spass<8, true>), dim3(e.W), dim3(512), 0, s, a);
@@ -2380,7 +2385,7 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
-  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 4 || value == 8)) {
+  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12)) {
     h->sealed_nw = (int)value;
     return GVS_OK;
   }

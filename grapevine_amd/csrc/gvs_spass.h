@@ -141,6 +141,26 @@ __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
   }
 }
 
+// A value the compiler must treat as unknown where this is called: the loop
+// bodies below recompute what depends on it instead of hoisting invariant
+// pieces (round-1 AES lookups of the fixed counter words, the header PRF's
+// first G functions over its zero words) out of the loop into registers, which
+// cost the sealed pass more registers than waves per SIMD allow.
+__device__ inline uint32_t opaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ inline B2State opaque(const B2State& k) {
+  B2State r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t lo = (uint32_t)k.h[i], hi = (uint32_t)(k.h[i] >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    r.h[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+  return r;
+}
+
 // NW waves; every slot line of the partition staged in LDS (LB) or read and
 // written in the stream (LB = false).
 template <int NW, bool LB>
@@ -248,7 +268,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         const uint32_t bits = wr ? cbits : pbits;
         const uint32_t tab = ((bits >> r) & 1u) ? kPendTable : 0u;
         const uint64_t z[2] = {0, 0};
-        header_prf(a.sc.headk, rowbase + g * 32u + r, a.sc.epoch + (wr ? 1u : 0u), tab, z, hh);
+        header_prf(opaque(a.sc.headk), rowbase + g * 32u + r, opaque(a.sc.epoch + (wr ? 1u : 0u)), tab, z, hh);
       }
 #pragma unroll 1
       for (uint32_t jj = 0; jj < 4; ++jj) {
@@ -268,7 +288,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
           const uint4 want = shfl4(tl, (int)u);
           if (__ballot((u4lo(want) != tg[0]) | (u4hi(want) != tg[1])) && lane == 0)
             atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-          lm_ctr(a.sc, te, row, a.sc.epoch, v);
+          lm_ctr(a.sc, te, row, opaque(a.sc.epoch), v);
         }
         // (3) the previous batch's final state, this batch's snapshot
         const bool app = (pbits >> rr) & 1u, tch = (cbits >> rr) & 1u;
@@ -299,7 +319,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         if (a.xon) xc = x_detect_lm(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
         // (4) encrypt and tag at the write epoch, store
         {
-          lm_ctr(a.sc, te, row, a.sc.epoch + 1u, v);
+          lm_ctr(a.sc, te, row, opaque(a.sc.epoch + 1u), v);
           const uint64_t hw[2] = {shfl_u64(hh[0], (int)(32u + rr)), shfl_u64(hh[1], (int)(32u + rr))};
           uint64_t tg[2];
           lm_tag(s_lk, v, hw, tg);

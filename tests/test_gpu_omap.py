@@ -136,6 +136,20 @@ def test_sealed_map_matches_the_oracle():
         model.close()
 
 
+def test_sealed_map_staged_pass():
+    """A 65536-row map (256-row partitions, 40 transaction slots): the value
+    table's sealed pass stages every slot line in LDS (gvs_spass.h)."""
+    store, model, rng, pool = sealed_pair(74, batches=5, cap=65536, nkeys=3000)
+    try:
+        for n in (1024, 7, 512):
+            ops = random_map_ops(rng, n, pool)
+            same(store.access(ops), model.access(ops), f"staged sealed {n}")
+        read_back(store, model, pool, 1024)
+    finally:
+        store.close()
+        model.close()
+
+
 def test_sealed_map_directory_is_not_plaintext():
     """No stored key appears in the sealed directory's bytes."""
     store, model, rng, pool = sealed_pair(71)

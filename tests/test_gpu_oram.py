@@ -151,6 +151,25 @@ def test_sealed_block_replay_and_swap_are_detected():
             model.close()
 
 
+def test_sealed_block_store_staged_pass():
+    """65536 blocks in 256-row partitions: 40 transaction slots, so the sealed
+    pass stages every slot line in LDS (gvs_spass.h); hot and uniform batches
+    bit-exact, then every block read back, then a tampered row detected."""
+    cap, B = 65536, 1024
+    store, model, rng = sealed_pair(63, batches=4, cap=cap, B=B)
+    try:
+        for _ in range(3):
+            ops = random_ops(rng, B, cap, hot=64)
+            assert (store.access(ops) == model.access(ops)).all()
+        read_all(store, model, cap, B)
+        b = store.dump_raw(abi.RAW_MESSAGES, 4321 * 1024 + 100, 1)
+        store.store_raw(abi.RAW_MESSAGES, 4321 * 1024 + 100, bytes([int(b[0]) ^ 0x01]))
+        expect_integrity(store, rng, cap=cap, B=B)
+    finally:
+        store.close()
+        model.close()
+
+
 def test_sealed_block_rows_are_the_storage_format():
     """Rows that the last batch did not touch hold the message table's format
     (table 0) at the epoch = batches applied: the oracle's seal of the model's

@@ -25,9 +25,12 @@ SECRET = bytes((0x67 + 31 * i) & 0xFF for i in range(32))
 
 
 def make_pair(n_msgs=4096, Q=16, Sr=32, B=1024, rpp=0):
-    """rpp = 512 (rows per partition) runs the 8-wave sealed message pass
-    (gvs_txn.h k_rpass2 NW = 8, U = 8); the default small-table partitions of
-    256 rows run the 4-wave one."""
+    """The sealed message pass (gvs_spass.h k_spass) stages a partition's slot
+    lines in LDS when it has at most 64 transaction slots: with 1024-request
+    batches that needs 64 partitions or more (n_msgs = 65536 and rpp <= 1024
+    here, the staged pass; 12 waves per workgroup from 1024-row partitions).
+    The small default tables (4096 messages, 16 partitions of 256 rows, 144
+    slots) run the fallback that keeps slot lines in HBM."""
     cfg = abi.make_config(n_msgs, mailbox_partitions=Q, mailbox_partition_slots=Sr,
                           max_batch=B, secret_key=SECRET, auth_storage=True, rows_per_partition=rpp)
     return ObliviousStore(cfg), ffi.Model(cfg)
@@ -46,9 +49,13 @@ def unseal(table, row, epoch, ct, side_ct=None):
     return pt, spt
 
 
-@pytest.mark.parametrize("rpp,waves", [(0, 8), (512, 8), (512, 4)])
-def test_auth_mode_parity_stream(rpp, waves):
-    store, model = make_pair(rpp=rpp)
+STAGED = dict(n_msgs=65536, rpp=256)  # the staged pass, 8 waves
+
+
+@pytest.mark.parametrize("n_msgs,rpp,waves", [(4096, 0, 8), (4096, 512, 4), (65536, 256, 8), (65536, 512, 4),
+                                              (65536, 1024, 12), (65536, 1024, 0)])
+def test_auth_mode_parity_stream(n_msgs, rpp, waves):
+    store, model = make_pair(n_msgs=n_msgs, rpp=rpp)
     store.set_option("sealed_pass_waves", waves)
     model.seed(31)
     seen = run_stream(store, model, ffi.gen_params(n_identities=300), batches=8, n=1024)
@@ -84,9 +91,9 @@ def pending_states(store, ep):
     return out
 
 
-@pytest.mark.parametrize("rpp", [0, 512])
-def test_stored_bytes_are_the_oracle_format(rpp):
-    store, model = make_pair(rpp=rpp)
+@pytest.mark.parametrize("n_msgs,rpp", [(4096, 0), (4096, 512), (65536, 256)])
+def test_stored_bytes_are_the_oracle_format(n_msgs, rpp):
+    store, model = make_pair(n_msgs=n_msgs, rpp=rpp)
     model.seed(33)
     run_stream(store, model, ffi.gen_params(n_identities=200), batches=3, n=1024)
     st = store.stats()
@@ -146,8 +153,9 @@ def run_one(store, model, params, n=1024):
     (abi.RAW_PENDING_SIDE, 17 * 128 + 12),  # its side entry (the slot its state goes to)
     (abi.RAW_PENDING_TAGS, 900 * 16),     # its tag
 ])
-def test_tamper_is_detected(region, offset):
-    store, model = make_pair()
+@pytest.mark.parametrize("staged", [False, True])
+def test_tamper_is_detected(region, offset, staged):
+    store, model = make_pair(**(STAGED if staged else {}))
     model.seed(34)
     params = ffi.gen_params(n_identities=200)
     run_stream(store, model, params, batches=2, n=1024)
@@ -161,8 +169,9 @@ def test_tamper_is_detected(region, offset):
     assert ei.value.code == abi.ERR_INTEGRITY
 
 
-def test_replayed_row_is_detected():
-    store, model = make_pair()
+@pytest.mark.parametrize("staged", [False, True])
+def test_replayed_row_is_detected(staged):
+    store, model = make_pair(**(STAGED if staged else {}))
     model.seed(35)
     params = ffi.gen_params(n_identities=200)
     run_stream(store, model, params, batches=2, n=1024)
@@ -177,8 +186,9 @@ def test_replayed_row_is_detected():
     assert ei.value.code == abi.ERR_INTEGRITY
 
 
-def test_swapped_rows_are_detected():
-    store, model = make_pair()
+@pytest.mark.parametrize("staged", [False, True])
+def test_swapped_rows_are_detected(staged):
+    store, model = make_pair(**(STAGED if staged else {}))
     model.seed(36)
     params = ffi.gen_params(n_identities=200)
     run_stream(store, model, params, batches=2, n=1024)
@@ -223,8 +233,9 @@ def live_slot_descriptors(store):
     (1, 1),   # the stamp: the row's pending final state is hidden
     (0, 1),   # the row: the final state is applied to another row
 ])
-def test_tampered_slot_descriptor_is_detected(word, delta):
-    store, model = make_pair()
+@pytest.mark.parametrize("staged", [False, True])
+def test_tampered_slot_descriptor_is_detected(word, delta, staged):
+    store, model = make_pair(**(STAGED if staged else {}))
     model.seed(38)
     params = ffi.gen_params(n_identities=200)
     run_stream(store, model, params, batches=2, n=1024)

@@ -20,7 +20,9 @@ Two checks per kernel (the counter test's, in microseconds):
 
 Shapes: the store under seven mixes, including adversarial ones (every request
 aimed at one recipient, every read missing, only deletes); the expiry sweep
-(README.md:92-97) with nothing, everything or a few old rows expired."""
+(README.md:92-97) with nothing, everything or a few old rows expired; sealed
+storage (2^22 messages, the production sealed pass, README.md:49-50); the
+2-shard router and padded all-to-all."""
 import csv
 import glob
 import math
@@ -43,9 +45,9 @@ SHAPES = {
                   mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
     "expiry": dict(args=ARGS + ["--expiry", "1024"], ref="main", mixes=["main", "x_all", "x_few"]),
     # sealed storage (BASELINE config 5 mode) at the counter
-    # test's sealed shape: 2^21 messages, 512-row partitions, the production
-    # 8-wave sealed pass
-    "auth": dict(args=["--log2n", "21", "--batch", "65536", "--identities", "200000", "--fill-batches", "3",
+    # test's sealed shape: 2^22 messages, 1024-row partitions, the production
+    # sealed pass (staged slot lines, 12 waves per workgroup)
+    "auth": dict(args=["--log2n", "22", "--batch", "65536", "--identities", "200000", "--fill-batches", "3",
                        "--auth"], ref="rud",
                  mixes=["rud", "main", "hot_next", "hot_next_rud", "all_miss_read", "deletes", "all_create"]),
     # the 2-shard router and the padded all-to-all in one process

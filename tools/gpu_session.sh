@@ -35,6 +35,19 @@ case "$2" in
   sealobl) step seal_tests 600 $PT $SEALT && \
     step oblivious_auth 900 $PT tests/test_oblivious.py -k "auth and not oram_auth and not omap_auth" && \
     step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 ;;
+  plaintime)  # the plain pass's timing and counters, then the C3 bench line
+    step timing_store 600 $PT tests/test_timing.py -k "independent_of_mix and not sealed and not routed"
+    cp gpurun_out/timing_c3_store.txt "$O/" 2>/dev/null
+    step oblivious_plain 600 $PT tests/test_oblivious.py -k "plain"
+    step bench 400 python3 bench.py --no-cpu ;;
+  sealperf)  # the sealed tests, the sealed bench at 12 and 8 waves
+    step seal_tests 600 $PT $SEALT
+    step bench_auth12 400 python3 bench.py --auth --no-cpu --steps 5 --sealed-waves 12
+    step bench_auth8 400 python3 bench.py --auth --no-cpu --steps 5 --sealed-waves 8 ;;
+  contract)  # every counter and timing shape
+    step oblivious_all 1200 $PT tests/test_oblivious.py
+    step timing_all 900 $PT tests/test_timing.py
+    cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
   driver) step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread ;;
   tests) tests ;;
   timing) timing ;;
