@@ -207,6 +207,61 @@ __device__ inline void ctr_keystream2_j(const AesRk& rk, const LdsTe& te, const 
   kb = make_uint4(bswap32(b[0]), bswap32(b[1]), bswap32(b[2]), bswap32(b[3]));
 }
 
+// The same for NB independent blocks at once: each round issues all 16 NB
+// lookups before combining them, so a lane waits for NB / 2 times fewer LDS
+// round trips per block (the sealed pass is bound by that latency).
+template <int R0, int NB>
+__device__ inline void aes128_rounds_n(const AesRk& rk, const LdsTe& te, uint32_t (&s)[NB][4]) {
+#pragma unroll
+  for (int r = R0; r < 10; ++r) {
+    uint32_t l[NB][16];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) l[b][4 * i + k] = te_at(te, s[b][(i + k) & 3], 3 - k);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        s[b][i] = xor3(xor3(l[b][4 * i], ror32(l[b][4 * i + 1], 8), ror32(l[b][4 * i + 2], 16)),
+                       ror32(l[b][4 * i + 3], 24), rk.w[4 * r + i]);
+  }
+  uint32_t l[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) l[b][4 * i + k] = te_at(te, s[b][(i + k) & 3], 3 - k);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      s[b][i] = sbox_pack(l[b][4 * i], l[b][4 * i + 1], l[b][4 * i + 2], l[b][4 * i + 3]) ^ rk.w[40 + i];
+}
+
+// keystream blocks j0 + i0 .. j0 + i0 + NB - 1 of the row (ctr_round1_row)
+template <int NB>
+__device__ inline void ctr_keystream_jn(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1, uint32_t i0,
+                                        uint4 (&ks)[NB]) {
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint32_t t = te_at(te, c1.x3b0 ^ (i0 + (uint32_t)b), 0);
+    s[b][0] = c1.t[0] ^ ror32(t, 24);
+    s[b][1] = c1.t[1];
+    s[b][2] = c1.t[2];
+    s[b][3] = c1.t[3];
+  }
+  aes128_rounds_n<2, NB>(rk, te, s);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
+}
+
 // The tile layout of a sealed message (or block) table: rows in tiles of 8
 // (8 KiB); inside a tile, 16-B unit i * 64 + L holds block 8 (L & 7) + i of
 // row L >> 3.  A wave's coalesced load of unit i into lane L (8 whole-KiB

@@ -129,15 +129,20 @@ __device__ inline void lm_tag(const uint64_t* s_lk, const uint4 (&v)[8], const u
 }
 
 // XOR the keystream of (message table, row, epoch) blocks 8 (L & 7) .. + 7
-// into the lane's registers (the row is the lane's own, L >> 3 of the chunk)
+// into the lane's registers (the row is the lane's own, L >> 3 of the chunk),
+// NB blocks in flight at a time
+#ifndef GVS_SP_NB
+#define GVS_SP_NB 2
+#endif
 __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
+  constexpr int NB = GVS_SP_NB;
   const CtrRound1J c1 = ctr_round1_row(c.rk, te, 0u, row, epoch, (lane_id() & 7u) * 8u);
 #pragma unroll
-  for (uint32_t i = 0; i < 8; i += 2) {
-    uint4 k0, k1;
-    ctr_keystream2_j(c.rk, te, c1, i, k0, k1);
-    v[i] = xor4(v[i], k0);
-    v[i + 1] = xor4(v[i + 1], k1);
+  for (uint32_t i = 0; i < 8; i += NB) {
+    uint4 ks[NB];
+    ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) v[i + b] = xor4(v[i + b], ks[b]);
   }
 }
 

@@ -48,6 +48,11 @@ case "$2" in
     step oblivious_all 1200 $PT tests/test_oblivious.py
     step timing_all 900 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
+  sealab)  # sealed pass A/B: AES blocks in flight (library builds ab/libgvstore_nb*.so) x waves
+    for nb in 2 4 8; do for nw in 8 12; do
+      GVS_LIB_OVERRIDE=ab/libgvstore_nb$nb.so step bench_auth_nb${nb}_nw$nw 300 \
+        python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
+    done; done ;;
   driver) step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread ;;
   tests) tests ;;
   timing) timing ;;
