@@ -25,6 +25,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from srcsha import source_sha  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md:36
 # vector-ALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per SIMD per
@@ -442,6 +444,7 @@ def predict_shards(a, torch, dev, json_out):
     st = store.stats()
     line = {"metric": "predicted per-GPU step of an S-GPU sharded run, measured on one GPU",
             "shards": S, "log2n_per_shard": a.log2n, "batch_per_source": B, "route_capacity": C,
+            "source_sha": source_sha(),
             "shard_batch": st["shard_batch"], "steps": a.steps, "warmup": a.warmup,
             "inproc_ms_per_call": T * 1e3, "per_rank_compute_ms": T / S * 1e3,
             "xgmi_bytes_per_direction_per_rank": xbytes, "xgmi_gbs_assumed": a.xgmi_gbs,
@@ -629,6 +632,9 @@ def main():
         W = st["msg_partitions"]
         c = store.get_option("txn_slots")
         alg_bytes = 2 * N * 1024 + 2 * W * c * 1024
+        # side figures from other runs are attached only when they were measured
+        # on these kernel sources (tools/srcsha.py)
+        src_sha = source_sha()
         achieved = alg_bytes / (rpass_ms * 1e-3) / 1e9
         traffic = None
         try:
@@ -637,7 +643,8 @@ def main():
             # the pass's bytes depend on N, W and c only: attach
             # the file's figure when it was measured at the same N and slot
             # count, whatever the rank count
-            if (tj.get("kernel") == "k_rpass2" and tj.get("log2n") == a.log2n and not a.auth
+            if (tj.get("kernel") == "k_rpass2s" and tj.get("log2n") == a.log2n and not a.auth
+                    and tj.get("expiry_per_batch", 0) == a.expiry and tj.get("source_sha") == src_sha
                     and tj.get("txn_slots", c if tj.get("batch") == B else None) == c):
                 traffic = tj.get("rpass_bytes_per_launch")
         except (OSError, ValueError):
@@ -654,7 +661,8 @@ def main():
             try:
                 with open(a.valu_json) as f:
                     vj = json.load(f)
-                if vj.get("log2n") == a.log2n and vj.get("batch") == B:
+                if (vj.get("log2n") == a.log2n and vj.get("batch") == B and vj.get("kernel") == "k_spass"
+                        and vj.get("source_sha") == src_sha and not a.sealed_waves):
                     insts = vj.get("valu_insts_per_launch")
             except (OSError, ValueError):
                 pass
@@ -673,7 +681,8 @@ def main():
         try:
             with open(a.prediction_json) as f:
                 pj = json.load(f)
-            if pj.get("log2n_per_shard") == a.log2n and pj.get("batch_per_source") == B:
+            if (pj.get("log2n_per_shard") == a.log2n and pj.get("batch_per_source") == B
+                    and pj.get("source_sha") == src_sha and not a.auth and not a.expiry):
                 prediction = {k: pj[k] for k in ("shards", "predicted_per_gpu_step_ms", "predicted_req_s_at_S",
                                                  "per_rank_compute_ms", "xgmi_ms_out_and_back",
                                                  "xgmi_gbs_assumed", "route_capacity", "shard_batch")}

@@ -77,14 +77,17 @@ case "$2" in
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines
     step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
-    python3 tools/traffic_from_pmc.py "$O/pmc_fetch" "$O/pmc_write" 24 65536 > "$O/traffic_latest.json" && cp "$O/traffic_latest.json" profiles/traffic_latest.json
+    python3 tools/traffic_from_pmc.py "$O/pmc_fetch" "$O/pmc_write" 24 65536 k_rpass2s > "$O/traffic_latest.json" && cp "$O/traffic_latest.json" profiles/traffic_latest.json
     rm -rf "$O/pmc_fetch" "$O/pmc_write"
     step kstats 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 bench.py --no-cpu
     find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
     find "$O/prof" -name "*kernel_trace.csv" -delete
     step bench_full 300 python3 bench.py
     step pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU -d "$O/pmc_valu" -o run --output-format csv -- python3 bench.py --auth --no-cpu --steps 5 --warmup 1
-    python3 tools/valu_from_pmc.py "$O/pmc_valu" 24 65536 > "$O/valu_auth_latest.json" && cp "$O/valu_auth_latest.json" profiles/
+    python3 tools/valu_from_pmc.py "$O/pmc_valu" 24 65536 k_spass > "$O/valu_auth_latest.json" && cp "$O/valu_auth_latest.json" profiles/
+    step predict 600 python3 bench.py --predict-shards 8 --steps 3 --warmup 1
+    grep '^{"metric": "predicted' "$O/predict.log" | tail -1 > "$O/scale_prediction.json" && \
+      python3 -c "import json; d=json.load(open('$O/scale_prediction.json')); json.dump(d, open('profiles/scale_prediction.json','w'), indent=1)"
     rm -rf "$O/pmc_valu"
     step bench_auth 600 python3 bench.py --auth --no-cpu --steps 5
     step bench_expiry 300 python3 bench.py --expiry 1024 --no-cpu ;;

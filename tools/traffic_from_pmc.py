@@ -8,7 +8,7 @@ coalesced reads, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The
 message pass streams every row with 16-B-per-lane loads and stores, the case
 that calibration covers.
 
-    python tools/traffic_from_pmc.py FETCH_DIR WRITE_DIR LOG2N BATCH [KERNEL]
+    python tools/traffic_from_pmc.py FETCH_DIR WRITE_DIR LOG2N BATCH [KERNEL [EXPIRY]]
 """
 import csv
 import glob
@@ -16,6 +16,8 @@ import json
 import os
 import statistics
 import sys
+
+from srcsha import source_sha
 
 
 def per_launch(d, counter, kernel):
@@ -33,7 +35,8 @@ def per_launch(d, counter, kernel):
 
 def main():
     fdir, wdir, log2n, batch = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-    kernel = sys.argv[5] if len(sys.argv) > 5 else "k_rpass2"
+    kernel = sys.argv[5] if len(sys.argv) > 5 else "k_rpass2s"
+    expiry = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     f = per_launch(fdir, "FETCH_SIZE", kernel)
     w = per_launch(wdir, "WRITE_SIZE", kernel)
     # the last launches are the timed C3 batches (the prefill batches run on a
@@ -41,7 +44,8 @@ def main():
     fm = statistics.median(f[-5:])
     wm = statistics.median(w[-5:])
     out = {
-        "kernel": kernel, "log2n": log2n, "batch": batch,
+        "kernel": kernel, "log2n": log2n, "batch": batch, "expiry_per_batch": expiry,
+        "source_sha": source_sha(),
         "fetch_kib": fm, "write_kib": wm,
         "read_bytes": 2 * fm * 1024, "write_bytes": wm * 1024,
         "rpass_bytes_per_launch": (2 * fm + wm) * 1024,

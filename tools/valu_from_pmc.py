@@ -12,16 +12,17 @@ import json
 import statistics
 import sys
 
+from srcsha import source_sha
 from traffic_from_pmc import per_launch
 
 
 def main():
     d, log2n, batch = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_rpass2"
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_spass"
     v = per_launch(d, "SQ_INSTS_VALU", kernel)
     print(json.dumps({"kernel": kernel, "log2n": log2n, "batch": batch,
                       "valu_insts_per_launch": statistics.median(v[-5:]),
-                      "launches_seen": len(v)}, indent=1))
+                      "launches_seen": len(v), "source_sha": source_sha()}, indent=1))
 
 
 if __name__ == "__main__":
