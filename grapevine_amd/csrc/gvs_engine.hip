@@ -32,6 +32,7 @@
 #include "gvs_wire.h"
 #include "gvs_sr25519.h"
 #include "gvs_spass.h"
+#include "gvs_mauth.h"
 
 using namespace gvs;
 
@@ -260,7 +261,7 @@ struct gvs_handle {
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
-  int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12; 0: by S)
+  int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12, 16; 0: by S)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -325,6 +326,9 @@ static int validate(const gvs_config* c) {
   if (!is_pow2(c->max_batch) || c->max_batch < 1024 || c->max_batch > (1u << (kSeqBits - 1)))
     return GVS_ERR_INVALID_ARG;
   if (c->flags & ~GVS_FLAG_AUTH_STORAGE) return GVS_ERR_INVALID_ARG;
+  // sealed mailbox partitions: the per-row values of k_m1a / k_m2a live in the
+  // AES window's holes (gvs_mauth.h)
+  if ((c->flags & GVS_FLAG_AUTH_STORAGE) && c->mailbox_partition_slots > kSrAuth) return GVS_ERR_INVALID_ARG;
   if (c->rows_per_partition && (!is_pow2(c->rows_per_partition) ||
                                 c->rows_per_partition < (uint32_t)kTile ||
                                 c->rows_per_partition > (uint32_t)kRowsMax))
@@ -920,7 +924,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   }
   mark(h, "gtx");
   if (h->auth)
-    hipLaunchKernelGGL(k_m1x<true>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+    hipLaunchKernelGGL(k_m1a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
   else
     hipLaunchKernelGGL(k_m1x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
   {
@@ -1005,6 +1009,8 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
       hipLaunchKernelGGL((k_spass<8, false>), dim3(e.W), dim3(512), 0, s, a);
     else if (nw == 12)
       hipLaunchKernelGGL((k_spass<12, true>), dim3(e.W), dim3(768), 0, s, a);
+    else if (nw == 16)
+      hipLaunchKernelGGL((k_spass<16, true>), dim3(e.W), dim3(1024), 0, s, a);
     else if (nw == 4)
       hipLaunchKernelGGL((k_spass<4, true>), dim3(e.W), dim3(256), 0, s, a);
     else
@@ -1077,7 +1083,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   }
   mark(h, "m2r");
   if (h->auth)
-    hipLaunchKernelGGL(k_m2x<true>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+    hipLaunchKernelGGL(k_m2a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
   else
     hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + e.Sr * sizeof(uint4), s,
                        margs2(h, e));
@@ -2385,7 +2391,7 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
-  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12)) {
+  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12 || value == 16)) {
     h->sealed_nw = (int)value;
     return GVS_OK;
   }
@@ -2530,18 +2536,23 @@ int gvs_raw_size(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t* size)
 }
 
 // A sealed message / block table is stored in 8-row tiles (gvs_seal_dev.h
-// tile_unit); the raw hooks show and take it as rows (row r at r * 1024), the
-// layout of the storage format (oracle/gvs_seal.c), converting the tiles the
-// byte range covers.
-static bool tiled(const gvs_handle* h, uint32_t region) { return region == 0 && h->auth; }
+// tile_unit), a sealed mailbox table in 16-row tiles (mtile_unit); the raw
+// hooks show and take them as rows (row r at r * 1024), the layout of the
+// storage format (oracle/gvs_seal.c), converting the tiles the byte range
+// covers.  Rows per tile, 0 for a region stored as rows.
+static uint32_t tiled(const gvs_handle* h, uint32_t region) {
+  return !h->auth ? 0u : region == 0 ? 8u : region == 1 && h->kind == 0 ? 16u : 0u;
+}
+static uint64_t tile_u(uint32_t tr, uint64_t r, uint32_t b) { return tr == 8 ? tile_unit(r, b) : mtile_unit(r, b); }
 
-static int tiles_in(gvs_handle* h, const void* base, uint64_t t0, uint64_t nt, std::vector<uint8_t>& rows) {
-  std::vector<uint8_t> t(nt * 8192);
-  GVS_HIP(h, hipMemcpyAsync(t.data(), (const uint8_t*)base + t0 * 8192, t.size(), hipMemcpyDeviceToHost, h->stream));
+static int tiles_in(gvs_handle* h, const void* base, uint32_t tr, uint64_t t0, uint64_t nt, std::vector<uint8_t>& rows) {
+  const uint64_t tb = (uint64_t)tr * 1024;
+  std::vector<uint8_t> t(nt * tb);
+  GVS_HIP(h, hipMemcpyAsync(t.data(), (const uint8_t*)base + t0 * tb, t.size(), hipMemcpyDeviceToHost, h->stream));
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   rows.resize(t.size());
-  for (uint64_t r = 0; r < nt * 8; ++r)
-    for (uint32_t b = 0; b < 64; ++b) std::memcpy(&rows[r * 1024 + b * 16], &t[tile_unit(r, b) * 16], 16);
+  for (uint64_t r = 0; r < nt * tr; ++r)
+    for (uint32_t b = 0; b < 64; ++b) std::memcpy(&rows[r * 1024 + b * 16], &t[tile_u(tr, r, b) * 16], 16);
   return GVS_OK;
 }
 
@@ -2552,11 +2563,11 @@ int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;
   if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
-  if (tiled(h, region) && bytes) {
-    const uint64_t t0 = offset / 8192, t1 = (offset + bytes + 8191) / 8192;
+  if (const uint32_t tr = tiled(h, region); tr && bytes) {
+    const uint64_t tb = (uint64_t)tr * 1024, t0 = offset / tb, t1 = (offset + bytes + tb - 1) / tb;
     std::vector<uint8_t> rows;
-    if (int r = tiles_in(h, base, t0, t1 - t0, rows)) return r;
-    std::memcpy(dst, &rows[offset - t0 * 8192], bytes);
+    if (int r = tiles_in(h, base, tr, t0, t1 - t0, rows)) return r;
+    std::memcpy(dst, &rows[offset - t0 * tb], bytes);
     return GVS_OK;
   }
   GVS_HIP(h, hipMemcpyAsync(dst, (uint8_t*)base + offset, bytes, hipMemcpyDeviceToHost, h->stream));
@@ -2571,15 +2582,15 @@ int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offse
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;
   if (offset > size || bytes > size - offset) return GVS_ERR_INVALID_ARG;
-  if (tiled(h, region) && bytes) {
-    const uint64_t t0 = offset / 8192, t1 = (offset + bytes + 8191) / 8192;
+  if (const uint32_t tr = tiled(h, region); tr && bytes) {
+    const uint64_t tb = (uint64_t)tr * 1024, t0 = offset / tb, t1 = (offset + bytes + tb - 1) / tb;
     std::vector<uint8_t> rows;
-    if (int r = tiles_in(h, base, t0, t1 - t0, rows)) return r;
-    std::memcpy(&rows[offset - t0 * 8192], src, bytes);
+    if (int r = tiles_in(h, base, tr, t0, t1 - t0, rows)) return r;
+    std::memcpy(&rows[offset - t0 * tb], src, bytes);
     std::vector<uint8_t> t(rows.size());
-    for (uint64_t r = 0; r < (t1 - t0) * 8; ++r)
-      for (uint32_t b = 0; b < 64; ++b) std::memcpy(&t[tile_unit(r, b) * 16], &rows[r * 1024 + b * 16], 16);
-    GVS_HIP(h, hipMemcpyAsync((uint8_t*)base + t0 * 8192, t.data(), t.size(), hipMemcpyHostToDevice, h->stream));
+    for (uint64_t r = 0; r < (t1 - t0) * tr; ++r)
+      for (uint32_t b = 0; b < 64; ++b) std::memcpy(&t[tile_u(tr, r, b) * 16], &rows[r * 1024 + b * 16], 16);
+    GVS_HIP(h, hipMemcpyAsync((uint8_t*)base + t0 * tb, t.data(), t.size(), hipMemcpyHostToDevice, h->stream));
     GVS_HIP(h, hipStreamSynchronize(h->stream));
     return GVS_OK;
   }

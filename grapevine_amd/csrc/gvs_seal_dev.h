@@ -271,6 +271,14 @@ __host__ __device__ constexpr uint64_t tile_unit(uint64_t row, uint32_t block) {
   return (row >> 3) * 512 + (uint64_t)(block & 7u) * 64 + (row & 7) * 8 + (block >> 3);
 }
 
+// The tile layout of a sealed mailbox table: rows in tiles of 16 (16 KiB);
+// inside a tile, 16-B unit i * 64 + L holds block 16 (L & 3) + i of row L >> 2.
+// A wave's 16 coalesced 1-KiB loads leave leaf L & 3 (256 B) of row L >> 2 in
+// lane L's registers (gvs_mauth.h).
+__host__ __device__ constexpr uint64_t mtile_unit(uint64_t row, uint32_t block) {
+  return (row >> 4) * 1024 + (uint64_t)(block & 15u) * 64 + (row & 15) * 4 + (block >> 4);
+}
+
 template <int U>
 __device__ inline void stage_rows(const uint4 (&v)[U], uint4* st) {
   const uint32_t lane = lane_id();
@@ -514,8 +522,8 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
       wave_seal<U, 8>(c, s_te, table, r0, 0u, v, tags, false, st, hdr);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (side)
-        rows[(r0 + u) * 64 + lane] = v[u];
+      if (side)  // the mailbox table: 16-row tiles (mtile_unit)
+        rows[mtile_unit(r0 + u, lane)] = v[u];
       else  // message and block tables: the tile layout (tile_unit)
         rows[tile_unit(r0 + u, lane)] = v[u];
     }

@@ -134,6 +134,9 @@ __device__ inline void lm_tag(const uint64_t* s_lk, const uint4 (&v)[8], const u
 #ifndef GVS_SP_NB
 #define GVS_SP_NB 2
 #endif
+#ifndef GVS_SP_ROUNDSYNC
+#define GVS_SP_ROUNDSYNC 1  // A/B builds: 0 = no barrier between rounds without expiry
+#endif
 __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
   constexpr int NB = GVS_SP_NB;
   const CtrRound1J c1 = ctr_round1_row(c.rk, te, 0u, row, epoch, (lane_id() & 7u) * 8u);
@@ -142,7 +145,10 @@ __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
     uint4 ks[NB];
     ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
 #pragma unroll
-    for (int b = 0; b < NB; ++b) v[i + b] = xor4(v[i + b], ks[b]);
+    for (int b = 0; b < NB; ++b) {
+      v[i + b] = xor4(v[i + b], ks[b]);
+      keep4(v[i + b]);  // XORed here, not sunk to the re-encryption with both keystreams held
+    }
   }
 }
 
@@ -339,8 +345,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
       }
     }
     // the waves meet after every round: the expiry lists merge in row order
+    // (without expiry they do not meet in the stream, so waves drift apart
+    // and one's AES rounds overlap another's BLAKE2b; a.xon is kernel-uniform)
     if (lane == 0) s_xc[wave] = xc;
-    __syncthreads();
+    if (GVS_SP_ROUNDSYNC || a.xon) __syncthreads();
     if (a.xon) {
       const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
       __syncthreads();

@@ -129,7 +129,8 @@ typedef struct gvs_response {
 typedef struct gvs_config {
   uint64_t msg_capacity;        /* N message slots per shard; power of two, >= 256 */
   uint32_t mailbox_partitions;  /* Q per shard; power of two */
-  uint32_t mailbox_partition_slots; /* S_r mailboxes per partition; R = Q*S_r */
+  uint32_t mailbox_partition_slots; /* S_r mailboxes per partition; R = Q*S_r; a multiple of 16,
+                                       at most 1024 (256 with GVS_FLAG_AUTH_STORAGE) */
   uint32_t max_batch;           /* B: requests per gvs_process_batch call (per rank
                                    when sharded); power of two, 1024 .. 2^19 */
   uint32_t device;              /* HIP device ordinal */

@@ -48,11 +48,23 @@ case "$2" in
     step oblivious_all 1200 $PT tests/test_oblivious.py
     step timing_all 900 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
-  sealab)  # sealed pass A/B: AES blocks in flight (library builds ab/libgvstore_nb*.so) x waves
-    for nb in 2 4 8; do for nw in 8 12; do
-      GVS_LIB_OVERRIDE=ab/libgvstore_nb$nb.so step bench_auth_nb${nb}_nw$nw 300 \
+  sealab)  # sealed pass A/B: library builds ab/libgvstore_VAR.so x waves (SEALAB="VAR:WAVES ...")
+    for v in ${SEALAB:-nb2:12 nb4:12 nb8:12 nosync_nb2:12 nosync_nb4:12 nb2:8 nb4:8}; do
+      lib=${v%%:*}; nw=${v##*:}
+      GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
         python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
-    done; done ;;
+    done ;;
+  kplain)  # per-kernel stats of the device-buffer C3 batches alone (no host or wire paths)
+    step kstats_plain 400 rocprofv3 --kernel-trace --stats -d "$O/kp" -o run --output-format csv -- \
+      python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10 --warmup 2
+    find "$O/kp" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_plain.csv" \;
+    rm -rf "$O/kp" ;;
+  kauth)  # the same for the sealed store
+    step kstats_auth 400 rocprofv3 --kernel-trace --stats -d "$O/ka" -o run --output-format csv -- \
+      python3 bench.py --auth --no-cpu --host-steps 0 --wire-steps 0 --steps 5 --warmup 2
+    find "$O/ka" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_auth.csv" \;
+    rm -rf "$O/ka" ;;
+  authsq) step auth_sq 900 bash tools/gpu_auth_sq.sh "$1/sq" ;;
   driver) step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread ;;
   tests) tests ;;
   timing) timing ;;
