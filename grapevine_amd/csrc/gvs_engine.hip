@@ -262,6 +262,7 @@ struct gvs_handle {
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12, 16; 0: by S)
+  uint32_t sealed_skew = 0;  // its per-SIMD-slot start offset, x 64 cycles (gvs_spass.h)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -997,6 +998,7 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     a.sc = seal_of(h, e);
     a.te = h->te;
     a.mtag = e.mtag;
+    a.skew = h->sealed_skew;
     // the previous batch's P (sealed at this epoch, by position) is unsealed
     // first, each row's final state to its slot's line of PS
     if (e.stamp_prev != kNone)
@@ -2393,6 +2395,10 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
   if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12 || value == 16)) {
     h->sealed_nw = (int)value;
+    return GVS_OK;
+  }
+  if (std::strcmp(key, "sealed_pass_skew") == 0 && value >= 0 && value <= 65536) {
+    h->sealed_skew = (uint32_t)value;
     return GVS_OK;
   }
   return GVS_ERR_INVALID_ARG;

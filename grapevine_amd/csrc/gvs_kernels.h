@@ -496,18 +496,6 @@ struct MArgs {
   uint32_t sink_mul;   // MSNAP sink line of global slot x: x * sink_mul mod Q*cm (a permutation)
 };
 
-// AUTH, phase C: stage the side ciphertexts of rows j0 .. j0+kMU-1 and verify
-// and decrypt the chunk's rows; a mismatch fails the batch for good.
-template <int U>
-__device__ inline void m_unseal_chunk(const MArgs& a, const uint32_t* s_te, uint32_t q,
-                                      uint32_t j0, uint4 (&v)[U], uint4* st) {
-  const uint32_t lane = lane_id();
-  const uint64_t r0 = (uint64_t)q * a.Sr + j0;
-  if (lane < (uint32_t)U) st[U * 4 * kSegU4 + lane] = a.side[r0 + lane];
-  if (!wave_unseal<U>(a.sc, s_te, 1u, r0, v, a.btag, true, st) && lane == 0)
-    atomicOr(&a.scal->error, 8u);
-}
-
 // ---------------------------------------------------------- allocation
 
 struct AllocArgs {

@@ -162,18 +162,16 @@ __device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, ui
   return (pos < ng && G.hi == hi && G.glo == glo) ? (int)pos : -1;
 }
 
-// occupied rows of the partition -> groups, every side entry read (AUTH:
-// decrypted here, authenticated with its row later); s_keep (LDS, or null)
-// keeps the entries as read, so that a later use does not read them again
-template <bool AUTH>
+// occupied rows of the partition -> groups, every side entry read; s_keep
+// (LDS, or null) keeps the entries as read, so that a later use does not read
+// them again (sealed stores: ma_prepass, gvs_mauth.h)
 __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uint32_t ng,
                                       int16_t* s_sg, uint8_t* s_occb, uint32_t* s_occ,
-                                      const uint32_t* s_te, uint4* s_keep = nullptr) {
+                                      uint4* s_keep = nullptr) {
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
     const uint64_t row = (uint64_t)q * a.Sr + j;
     uint4 sd = a.side[row];
     if (s_keep) s_keep[j] = sd;
-    if (AUTH) sd = xor4(sd, side_keystream(a.sc, s_te, row, a.sc.epoch));
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
     const int kf = find_group_m(g, ng, a.cm, hi, w1 >> 23);  // every row: no code skipped
@@ -265,6 +263,7 @@ __device__ inline uint32_t spread_lo(uint32_t i, uint32_t n, uint32_t d) { retur
 // pops, 2 admitted as a new mailbox), row}; lanes 2.. = the 62 ids
 template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
+  static_assert(!AUTH, "sealed stores run k_m1a (gvs_mauth.h)");
   // the group slots and the sink, cm + 1 entries in dynamic LDS sized at
   // launch (9 KiB at C3 instead of 33): more workgroups per CU
   extern __shared__ uint4 s_dyn[];
@@ -275,14 +274,10 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   __shared__ uint8_t s_tf[kGroupMax];     // tail: slots without a row
   __shared__ uint16_t s_tp[kGroupMax + 1];
   __shared__ int16_t s_tl[kGroupMax];
-  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
-  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
-  if (AUTH) load_te(s_te, a.te);
-  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
   const uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
   uint4 va[kMU], vb[kMU];
   load_rows(va, part, wave * kMU, a.Sr);
@@ -292,7 +287,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     s_empt = 0;
   }
   __syncthreads();
-  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  side_prepass_m(a, q, g, ng, s_sg, s_occb, &s_occ);
   __syncthreads();
   // admission (grapevine.proto:74): rows that empty after the pops are free
   // again; new recipients are admitted by the seq of their first create
@@ -370,7 +365,6 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
       keep4(v[u]);  // every row is read, used or not
       mm |= (j0 + u < a.Sr && s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
     }
-    if (AUTH) m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
     mm = __builtin_amdgcn_readfirstlane(mm);
     // the chunk's touched rows, then its share of the slot iterations
     const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
@@ -694,6 +688,7 @@ __device__ inline uint4 m2_row(uint4 v, bool matched, uint32_t len, uint32_t dp,
 
 template <bool AUTH>
 __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
+  static_assert(!AUTH, "sealed stores run k_m2a (gvs_mauth.h)");
   // dynamic LDS sized at launch: (plain) the partition's Sr side entries as
   // the prepass read them, then the group slots and the sink, cm + 1 entries
   // (9 KiB at C3 instead of 33): more workgroups per CU.  The side entries are
@@ -703,12 +698,10 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   // mixes, profiles/r04x_m2x_read_counters.txt)
   extern __shared__ uint4 s_dyn[];
   uint4* s_side = s_dyn;
-  GroupM* g = reinterpret_cast<GroupM*>(s_dyn + (AUTH ? 0u : a.Sr));
+  GroupM* g = reinterpret_cast<GroupM*>(s_dyn + a.Sr);
   __shared__ int16_t s_sg[kSrMax];
   __shared__ uint8_t s_occb[kSrMax];
-  GVS_TE_LDS s_te[AUTH ? kTeWords : 1];
-  __shared__ uint4 s_st[AUTH ? 4 * stage_u4(kMU) : 1];
-  __shared__ uint4 s_wst[AUTH ? 1 : 4][64];  // AUTH: the seal stage doubles as it
+  __shared__ uint4 s_wst[4][64];
   __shared__ int16_t s_place[kSrMax];
   __shared__ uint8_t s_flag[kSrMax];
   __shared__ uint16_t s_pfx[kSrMax + 1];
@@ -721,8 +714,6 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
-  if (AUTH) load_te(s_te, a.te);
-  uint4* st = s_st + (AUTH ? wave * stage_u4(kMU) : 0u);
   uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
   uint4* side = a.side + (uint64_t)q * a.Sr;
   uint4 va[kMU], vb[kMU];
@@ -733,7 +724,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
     s_delta = 0;
   }
   __syncthreads();
-  side_prepass_m<AUTH>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te, AUTH ? nullptr : s_side);
+  side_prepass_m(a, q, g, ng, s_sg, s_occb, &s_occ, s_side);
   __syncthreads();
   // final lengths; pending = groups with no row that end non-empty
   for (uint32_t k = tid; k < a.cm; k += 256) {
@@ -796,7 +787,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   // the workgroup's dry block: k_m1x writes its first 4 KiB; slot iterations
   // past the list read 1 KiB lines 4..7 (no line is read twice in a kernel)
   const uint4* dry = a.mdry + (uint64_t)q * kMDryU4 + 256;
-  uint4* wst = AUTH ? st : s_wst[AUTH ? 0 : wave];
+  uint4* wst = s_wst[wave];
   // one iteration: a touched row (bit set: its row in v is replaced) or a
   // slot no row takes (bit 0: the same work, nothing kept)
   // mine: lane u < kMU holds row u's side entry
@@ -839,13 +830,7 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
     }
     // the chunk's side entries, one per lane u < kMU, as the prepass read them
-    uint4 mine = (!AUTH && lane < (uint32_t)kMU && j0 + lane < a.Sr) ? s_side[j0 + lane] : make_uint4(0, 0, 0, 0);
-    if (AUTH) {
-      m_unseal_chunk<kMU>(a, s_te, q, j0, v, st);
-      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
-      if (lane < (uint32_t)kMU)
-        mine = xor4(st[kMU * 4 * kSegU4 + lane], side_keystream(a.sc, s_te, r0 + lane, a.sc.epoch));
-    }
+    uint4 mine = (lane < (uint32_t)kMU && j0 + lane < a.Sr) ? s_side[j0 + lane] : make_uint4(0, 0, 0, 0);
     mm = __builtin_amdgcn_readfirstlane(mm);
     // the chunk's touched rows, then its share of the slot iterations
     const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
@@ -856,20 +841,9 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
       mq &= mq - 1u;
       step(v, mine, low, j0, d0 + dlo + (r - nt));
     }
-    if (AUTH) {
-      const uint64_t r0 = (uint64_t)q * a.Sr + j0;
-      const uint32_t ep = a.sc.epoch + 1u;
-      if (lane < (uint32_t)kMU) {
-        const uint4 ct = xor4(mine, side_keystream(a.sc, s_te, r0 + lane, ep));
-        st[kMU * 4 * kSegU4 + lane] = ct;
-        side[j0 + lane] = ct;
-      }
-      wave_seal<kMU>(a.sc, s_te, 1u, r0, ep, v, a.btag, true, st);
-    }
-    if (!AUTH) {  // the chunk's side entries: one store, kMU lanes (one whole line at kMU = 8;
-                  // eight 16-B stores of one line from one lane left partial lines behind)
-      if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
-    }
+    // the chunk's side entries: one store, kMU lanes (one whole line at kMU = 8;
+    // eight 16-B stores of one line from one lane left partial lines behind)
+    if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
 #pragma unroll
     for (int u = 0; u < kMU; ++u) {
       if (j0 + u < a.Sr) st_stream(part, (uint64_t)(j0 + u) * 64 + lane, v[u]);

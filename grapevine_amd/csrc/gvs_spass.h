@@ -48,10 +48,13 @@
 
 namespace gvs {
 
-constexpr uint32_t kSpBufs = 96;              // LDS staging buffers (1 KiB each)
+#ifndef GVS_SP_DUAL
+#define GVS_SP_DUAL 0  // A/B builds: 1 = T0 and T1 in the AES window (load_te2), every buffer after it
+#endif
+constexpr uint32_t kSpBufs = GVS_SP_DUAL ? 88 : 96;  // LDS staging buffers (1 KiB each)
 constexpr uint32_t kSpSlots = 64;             // transaction slots per partition (c) with LDS staging
 constexpr uint32_t kSpDry = kSpBufs;          // the dry buffer
-constexpr uint32_t kSpHoles = 32;             // buffers 0..31 live in the AES window's holes
+constexpr uint32_t kSpHoles = GVS_SP_DUAL ? 0 : 32;  // buffers 0..31 live in the AES window's holes
 constexpr uint32_t kSpWords = kRowsMax / 32;  // bitmap words per partition
 
 // byte address (from the 64-KiB-aligned window at LDS 0) of 16-B block i of
@@ -61,7 +64,7 @@ __device__ inline uint32_t sp_addr(uint32_t b, uint32_t q, uint32_t i) {
   const uint32_t rot = ((i + q) & 7u) * 16u;
   const uint32_t hole = (8u * b + q) * 256u + 128u + rot;
   const uint32_t buf = 65536u + (b - kSpHoles) * 1024u + q * 128u + rot;
-  return selu32(b < kSpHoles, hole, buf);
+  return kSpHoles ? selu32(b < kSpHoles, hole, buf) : buf;
 }
 
 template <bool LB>
@@ -128,30 +131,6 @@ __device__ inline void lm_tag(const uint64_t* s_lk, const uint4 (&v)[8], const u
   }
 }
 
-// XOR the keystream of (message table, row, epoch) blocks 8 (L & 7) .. + 7
-// into the lane's registers (the row is the lane's own, L >> 3 of the chunk),
-// NB blocks in flight at a time
-#ifndef GVS_SP_NB
-#define GVS_SP_NB 2
-#endif
-#ifndef GVS_SP_ROUNDSYNC
-#define GVS_SP_ROUNDSYNC 1  // A/B builds: 0 = no barrier between rounds without expiry
-#endif
-__device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
-  constexpr int NB = GVS_SP_NB;
-  const CtrRound1J c1 = ctr_round1_row(c.rk, te, 0u, row, epoch, (lane_id() & 7u) * 8u);
-#pragma unroll
-  for (uint32_t i = 0; i < 8; i += NB) {
-    uint4 ks[NB];
-    ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      v[i + b] = xor4(v[i + b], ks[b]);
-      keep4(v[i + b]);  // XORed here, not sunk to the re-encryption with both keystreams held
-    }
-  }
-}
-
 // A value the compiler must treat as unknown where this is called: the loop
 // bodies below recompute what depends on it instead of hoisting invariant
 // pieces (round-1 AES lookups of the fixed counter words, the header PRF's
@@ -170,6 +149,38 @@ __device__ inline B2State opaque(const B2State& k) {
     r.h[i] = (uint64_t)lo | ((uint64_t)hi << 32);
   }
   return r;
+}
+
+// XOR the keystream of (message table, row, epoch) blocks 8 (L & 7) .. + 7
+// into the lane's registers (the row is the lane's own, L >> 3 of the chunk),
+// NB blocks in flight at a time
+#ifndef GVS_SP_NB
+#define GVS_SP_NB 2
+#endif
+#ifndef GVS_SP_ROUNDSYNC
+#define GVS_SP_ROUNDSYNC 1  // A/B builds: 0 = no barrier between rounds without expiry
+#endif
+__device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
+  constexpr int NB = GVS_SP_NB;
+  // the row's high word and the lane's block offset are the same for every
+  // chunk: left visible, the compiler hoisted the round-1 lookup addresses
+  // that depend only on them out of the stream, and at 16 waves spilled them
+  // (a scratch reload in front of every keystream)
+  const uint64_t r = ((uint64_t)opaque((uint32_t)(row >> 32)) << 32) | opaque((uint32_t)row);
+  const CtrRound1J c1 = ctr_round1_row(c.rk, te, 0u, r, epoch, opaque((lane_id() & 7u) * 8u));
+#pragma unroll
+  for (uint32_t i = 0; i < 8; i += NB) {
+    uint4 ks[NB];
+    if (GVS_SP_DUAL)
+      ctr_keystream_jn2<NB>(c.rk, te, c1, i, ks);
+    else
+      ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      v[i + b] = xor4(v[i + b], ks[b]);
+      keep4(v[i + b]);  // XORed here, not sunk to the re-encryption with both keystreams held
+    }
+  }
 }
 
 // NW waves; every slot line of the partition staged in LDS (LB) or read and
@@ -191,7 +202,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
-  load_te(s_lds, a.te);
+  if (GVS_SP_DUAL)
+    load_te2(s_lds, a.te);
+  else
+    load_te(s_lds, a.te);
   if (tid < 64) s_lk[tid] = a.sc.leafk0[tid >> 3].h[tid & 7u];
   const uint32_t nwd = a.S / 32u;
   for (uint32_t o = tid; o < nwd; o += 64 * NW) {
@@ -264,6 +278,15 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   const LdsTe te = lds_te(s_lds);
   const uint32_t ngroups = a.S / 32u, rounds = (ngroups + NW - 1) / NW;
   const uint32_t u = lane >> 3, f = lane & 7u;
+  // Phase skew: a chunk is two AES stretches (LDS-bound: 145 table reads per
+  // block) between BLAKE2b stretches (VALU-bound).  Waves that start together
+  // stay in step, so the CU alternates between a saturated LDS with idle VALUs
+  // and the reverse.  The waves sharing a SIMD (wave / 4) start a fraction of
+  // a chunk apart and are not re-synchronised in the stream (no per-round
+  // barrier without expiry): wave-uniform, data-independent.
+  if (a.skew) {
+    for (uint32_t k = (wave >> 2) * a.skew; k >= 64u; k -= 64u) __builtin_amdgcn_s_sleep(64);
+  }
   for (uint32_t t = 0; t < rounds; ++t) {
     uint32_t xc = 0;
     const uint32_t g = t * NW + wave;
@@ -348,7 +371,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
     // (without expiry they do not meet in the stream, so waves drift apart
     // and one's AES rounds overlap another's BLAKE2b; a.xon is kernel-uniform)
     if (lane == 0) s_xc[wave] = xc;
-    if (GVS_SP_ROUNDSYNC || a.xon) __syncthreads();
+    if ((GVS_SP_ROUNDSYNC && !a.skew) || a.xon) __syncthreads();
     if (a.xon) {
       const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
       __syncthreads();
