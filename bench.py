@@ -56,8 +56,6 @@ def parse():
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12, 16),
                    help="--auth: waves per workgroup of the sealed message pass (0: the store's choice)")
-    p.add_argument("--sealed-skew", type=int, default=-1,
-                   help="--auth: start offset per SIMD wave slot of the sealed pass, x 64 cycles (-1: the engine's)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
@@ -505,8 +503,6 @@ def main():
                                       store.get_option("txn_slots")], device=dev)
     if a.auth:
         store.set_option("sealed_pass_waves", a.sealed_waves)
-        if a.sealed_skew >= 0:
-            store.set_option("sealed_pass_skew", a.sealed_skew)
     g = torch.Generator(device=dev)
     g.manual_seed(gdist.shard_seed(0x6772617065 + 3, rank))
     pool = torch.randint(0, 256, (1 << 19, 32), dtype=torch.uint8, device=dev, generator=g)

@@ -33,6 +33,9 @@
 #include "gvs_sr25519.h"
 #include "gvs_spass.h"
 #include "gvs_mauth.h"
+#ifndef GVS_MA_EXTRA_LDS
+#define GVS_MA_EXTRA_LDS 0  // A/B builds: extra dynamic LDS (one sealed mailbox workgroup per CU)
+#endif
 
 using namespace gvs;
 
@@ -262,7 +265,6 @@ struct gvs_handle {
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12, 16; 0: by S)
-  uint32_t sealed_skew = 0;  // its per-SIMD-slot start offset, x 64 cycles (gvs_spass.h)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -910,7 +912,9 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   mark(h, "copy");
   {
     MetaArgs a{e.img, e.types, e.ops, e.kinds, e.s1keys, n, B, e.Q, e.logQ, e.N, e.kc, xbase, e.idn};
-    hipLaunchKernelGGL(k_meta, dim3(e.nblk), dim3(1024), 0, s, a);
+    // one op per thread, no block-level work: 256-thread workgroups spread
+    // the batch over every CU (1024-thread ones filled a quarter of them)
+    hipLaunchKernelGGL(k_meta, dim3(B / 256), dim3(256), 0, s, a);
   }
   mark(h, "meta");
   if (int r = sort_keys<Key128, 1>(h, e.s1keys, B)) return r;
@@ -925,7 +929,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   }
   mark(h, "gtx");
   if (h->auth)
-    hipLaunchKernelGGL(k_m1a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+    hipLaunchKernelGGL(k_m1a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + GVS_MA_EXTRA_LDS, s, margs2(h, e));
   else
     hipLaunchKernelGGL(k_m1x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
   {
@@ -998,7 +1002,6 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
     a.sc = seal_of(h, e);
     a.te = h->te;
     a.mtag = e.mtag;
-    a.skew = h->sealed_skew;
     // the previous batch's P (sealed at this epoch, by position) is unsealed
     // first, each row's final state to its slot's line of PS
     if (e.stamp_prev != kNone)
@@ -1085,7 +1088,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   }
   mark(h, "m2r");
   if (h->auth)
-    hipLaunchKernelGGL(k_m2a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+    hipLaunchKernelGGL(k_m2a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + GVS_MA_EXTRA_LDS, s, margs2(h, e));
   else
     hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + e.Sr * sizeof(uint4), s,
                        margs2(h, e));
@@ -2395,10 +2398,6 @@ int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
   if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12 || value == 16)) {
     h->sealed_nw = (int)value;
-    return GVS_OK;
-  }
-  if (std::strcmp(key, "sealed_pass_skew") == 0 && value >= 0 && value <= 65536) {
-    h->sealed_skew = (uint32_t)value;
     return GVS_OK;
   }
   return GVS_ERR_INVALID_ARG;

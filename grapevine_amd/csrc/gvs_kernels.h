@@ -354,7 +354,7 @@ struct MetaArgs {
   uint4* idn;      // B x 128 B: the image's first 80 B (id, sender, recipient), for k_rr1
 };
 
-__global__ __launch_bounds__(1024) void k_meta(MetaArgs a) {
+__global__ __launch_bounds__(256) void k_meta(MetaArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4* row = a.img + (uint64_t)i * 64;
   uint4 c0 = row[0], c1 = row[1], c2 = row[2], c3 = row[3], c4 = row[4], c5 = row[5];

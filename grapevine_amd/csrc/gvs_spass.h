@@ -278,15 +278,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   const LdsTe te = lds_te(s_lds);
   const uint32_t ngroups = a.S / 32u, rounds = (ngroups + NW - 1) / NW;
   const uint32_t u = lane >> 3, f = lane & 7u;
-  // Phase skew: a chunk is two AES stretches (LDS-bound: 145 table reads per
-  // block) between BLAKE2b stretches (VALU-bound).  Waves that start together
-  // stay in step, so the CU alternates between a saturated LDS with idle VALUs
-  // and the reverse.  The waves sharing a SIMD (wave / 4) start a fraction of
-  // a chunk apart and are not re-synchronised in the stream (no per-round
-  // barrier without expiry): wave-uniform, data-independent.
-  if (a.skew) {
-    for (uint32_t k = (wave >> 2) * a.skew; k >= 64u; k -= 64u) __builtin_amdgcn_s_sleep(64);
-  }
   for (uint32_t t = 0; t < rounds; ++t) {
     uint32_t xc = 0;
     const uint32_t g = t * NW + wave;
@@ -371,7 +362,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
     // (without expiry they do not meet in the stream, so waves drift apart
     // and one's AES rounds overlap another's BLAKE2b; a.xon is kernel-uniform)
     if (lane == 0) s_xc[wave] = xc;
-    if ((GVS_SP_ROUNDSYNC && !a.skew) || a.xon) __syncthreads();
+    if (GVS_SP_ROUNDSYNC || a.xon) __syncthreads();
     if (a.xon) {
       const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
       __syncthreads();

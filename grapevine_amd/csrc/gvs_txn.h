@@ -292,7 +292,6 @@ struct R2Args {
   uint64_t cutoff;
   uint4* xbuf;         // records written by this pass
   const uint4* xprev;  // records being deleted by this batch (exclusion)
-  uint32_t skew;       // sealed pass: start offset per wave slot of a SIMD, x 64 cycles (0: none)
 };
 
 // Expiry detection on a chunk (v1 x_detect plus the exclusion of rows whose

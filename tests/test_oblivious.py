@@ -251,19 +251,23 @@ def test_launch_sequence_and_grids_identical(shape, tmp_root):
 
 
 def exclusions(per):
-    """{mix: {batch index}}: the one batch of a process that re-walked the page
-    tables, if one did.
+    """{mix: {batch index}}: the one measured batch of a process that re-walked
+    the page tables, if one did.
 
     The rule ("Next round" 2): the uncached L2 requests
     (TCC_UC_REQ_sum) are recorded in the same --pmc pass as the byte counter,
-    for every dispatch; a batch whose kernels made more than UC_WALK of them
-    is a re-walk; the rule is the same for every mix (main and main#2
+    for every dispatch; a measured batch whose kernels made more than UC_WALK
+    of them is a re-walk; the rule is the same for every mix (main and main#2
     included); at most one batch per process is set aside, and only when it is
-    the process's only re-walk (two or more are all kept: the test then fails
-    on them); every exclusion is printed in the report."""
+    the process's only re-walk among its measured batches (two or more are all
+    kept: the test then fails on them); every exclusion is printed in the
+    report.  The prefill batches are not candidates: the first two of every
+    process touch their pages for the first time (~4000 walks each, the same in
+    every process: identical inputs), and they enter only the noise estimate."""
     out = {}
     for mix, bs in per.items():
-        walks = [i for i, b in enumerate(bs) if sum(x[4] for x in b) > UC_WALK]
+        n0 = len(bs) - N_MEAS
+        walks = [i for i in range(n0, len(bs)) if sum(x[4] for x in bs[i]) > UC_WALK]
         out[mix] = set(walks) if len(walks) == 1 else set()
     return out
 

@@ -54,12 +54,11 @@ case "$2" in
       GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
         python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
     done ;;
-  skew)  # sealed pass phase skew sweep (SKEW="WAVES:SKEW ...", in-tree library)
-    for v in ${SKEW:-12:0 12:360 12:720 12:1440 16:0 16:540 16:1080}; do
-      nw=${v%%:*}; sk=${v##*:}
-      step bench_auth_nw${nw}_skew$sk 300 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 \
-        --sealed-waves $nw --sealed-skew $sk
-    done ;;
+  m2ab)  # the sealed shape's FETCH_SIZE counters, in-tree build and ab/libgvstore_ma1wg.so
+    step obl_auth_v0 900 $PT tests/test_oblivious.py -k "hbm_bytes_identical and FETCH_SIZE-auth"
+    cp gpurun_out/oblivious_FETCH_SIZE_auth.txt "$O/obl_FETCH_auth_v0.txt"
+    GVS_LIB_OVERRIDE=ab/libgvstore_ma1wg.so step obl_auth_v1 900 $PT tests/test_oblivious.py -k "hbm_bytes_identical and FETCH_SIZE-auth"
+    cp gpurun_out/oblivious_FETCH_SIZE_auth.txt "$O/obl_FETCH_auth_v1.txt" ;;
   kplain)  # per-kernel stats of the device-buffer C3 batches alone (no host or wire paths)
     step kstats_plain 400 rocprofv3 --kernel-trace --stats -d "$O/kp" -o run --output-format csv -- \
       python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10 --warmup 2
