@@ -48,13 +48,10 @@
 
 namespace gvs {
 
-#ifndef GVS_SP_DUAL
-#define GVS_SP_DUAL 0  // A/B builds: 1 = T0 and T1 in the AES window (load_te2), every buffer after it
-#endif
-constexpr uint32_t kSpBufs = GVS_SP_DUAL ? 88 : 96;  // LDS staging buffers (1 KiB each)
+constexpr uint32_t kSpBufs = 96;              // LDS staging buffers (1 KiB each)
 constexpr uint32_t kSpSlots = 64;             // transaction slots per partition (c) with LDS staging
 constexpr uint32_t kSpDry = kSpBufs;          // the dry buffer
-constexpr uint32_t kSpHoles = GVS_SP_DUAL ? 0 : 32;  // buffers 0..31 live in the AES window's holes
+constexpr uint32_t kSpHoles = 32;             // buffers 0..31 live in the AES window's holes
 constexpr uint32_t kSpWords = kRowsMax / 32;  // bitmap words per partition
 
 // byte address (from the 64-KiB-aligned window at LDS 0) of 16-B block i of
@@ -64,7 +61,7 @@ __device__ inline uint32_t sp_addr(uint32_t b, uint32_t q, uint32_t i) {
   const uint32_t rot = ((i + q) & 7u) * 16u;
   const uint32_t hole = (8u * b + q) * 256u + 128u + rot;
   const uint32_t buf = 65536u + (b - kSpHoles) * 1024u + q * 128u + rot;
-  return kSpHoles ? selu32(b < kSpHoles, hole, buf) : buf;
+  return selu32(b < kSpHoles, hole, buf);
 }
 
 template <bool LB>
@@ -157,15 +154,6 @@ __device__ inline B2State opaque(const B2State& k) {
 #ifndef GVS_SP_NB
 #define GVS_SP_NB 2
 #endif
-#ifndef GVS_SP_JOBS
-#define GVS_SP_JOBS 0  // A/B builds: 1 = one BLAKE2b and one keystream call site per group loop
-#endif
-#ifndef GVS_SP_ROLL
-#define GVS_SP_ROLL 0  // A/B builds: 1 = AES rounds in a rolled loop (code size)
-#endif
-#ifndef GVS_SP_ROUNDSYNC
-#define GVS_SP_ROUNDSYNC 1  // A/B builds: 0 = no barrier between rounds without expiry
-#endif
 __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
   constexpr int NB = GVS_SP_NB;
   // the row's high word and the lane's block offset are the same for every
@@ -177,10 +165,7 @@ __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
 #pragma unroll
   for (uint32_t i = 0; i < 8; i += NB) {
     uint4 ks[NB];
-    if (GVS_SP_DUAL)
-      ctr_keystream_jn2<NB>(c.rk, te, c1, i, ks);
-    else
-      ctr_keystream_jn<NB, GVS_SP_ROLL>(c.rk, te, c1, i, ks);
+    ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       v[i + b] = xor4(v[i + b], ks[b]);
@@ -204,16 +189,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
   __shared__ uint32_t s_xc[NW];
-  __shared__ uint64_t s_lk[9 * 8];              // the message leaves' key states (leafk0), then headk
+  __shared__ uint64_t s_lk[8 * 8];              // the message leaves' key states (leafk0)
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
-  if (GVS_SP_DUAL)
-    load_te2(s_lds, a.te);
-  else
-    load_te(s_lds, a.te);
+  load_te(s_lds, a.te);
   if (tid < 64) s_lk[tid] = a.sc.leafk0[tid >> 3].h[tid & 7u];
-  if (tid < 8) s_lk[64 + tid] = a.sc.headk.h[tid];
   const uint32_t nwd = a.S / 32u;
   for (uint32_t o = tid; o < nwd; o += 64 * NW) {
     s_pbm[o] = 0u;
@@ -288,112 +269,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   for (uint32_t t = 0; t < rounds; ++t) {
     uint32_t xc = 0;
     const uint32_t g = t * NW + wave;
-#if GVS_SP_JOBS
-    if (g < ngroups) {
-      // One BLAKE2b compression per job, one call site: job 0 the group's
-      // header PRFs (lane l < 32 row g*32 + l at the read epoch, lane 32 + l
-      // at the write epoch), job 2k+1 the read tag of chunk k (then its
-      // decryption, slot work and re-encryption, one keystream call site),
-      // job 2k+2 its write tag and store.  The unrolled body (three
-      // compressions, two 8-block keystreams) was 107 KB of code, more than
-      // the instruction cache holds.
-      const uint32_t pbits = s_pbm[g], cbits = s_cbm[g];
-      uint64_t hh[2] = {0, 0};
-      uint4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = make_uint4(0, 0, 0, 0);
-      uint4 tl = make_uint4(0, 0, 0, 0);
-      uint32_t rj = g * 32u, rr = u;
-#pragma unroll 1
-      for (uint32_t job = 0; job < 9; ++job) {
-        const bool hdr = job == 0u, rd = (job & 1u) != 0u;
-        if (rd) {
-          rj = g * 32u + ((job - 1u) >> 1) * 8u;  // the chunk's first row in the partition
-          rr = rj - g * 32u + u;                   // the lane's row in the group
-          const uint4* tile = part + (uint64_t)rj * 64;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) v[i] = ld_row<true>(&tile[i * 64 + lane]);
-          tl = line_load(a.mtag + rowbase + rj);
-        }
-        if (hdr) {  // v holds the header block (header_block: row, epoch | table << 32, zeros)
-          const uint32_t r = lane & 31u;
-          const bool w = lane >= 32u;
-          const uint32_t tab = (((w ? cbits : pbits) >> r) & 1u) ? kPendTable : 0u;
-          const uint64_t hrow = rowbase + g * 32u + r;
-          v[0] = make_uint4((uint32_t)hrow, (uint32_t)(hrow >> 32), opaque(a.sc.epoch + (w ? 1u : 0u)), tab);
-#pragma unroll
-          for (int i = 1; i < 8; ++i) v[i] = make_uint4(0, 0, 0, 0);
-        }
-        uint64_t m[16];
-        leaf_words(v, m);
-        B2State k;  // the key state: the header PRF's (s_lk row 8) or the lane's leaf's
-#pragma unroll
-        for (int q = 0; q < 8; ++q) k.h[q] = s_lk[(hdr ? 8u : f) * 8u + q];
-        b2_compress(k, m, hdr ? 128 + 32 : 128 + 128, true);
-        uint64_t res[2] = {k.h[0], k.h[1]};
-        if (hdr) {
-          hh[0] = res[0];
-          hh[1] = res[1];
-          continue;
-        }
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {  // the row's leaf sum (its 8 lanes)
-          res[w] ^= shfl_u64(res[w], (int)(lane ^ 1u));
-          res[w] ^= shfl_u64(res[w], (int)(lane ^ 2u));
-          res[w] ^= shfl_u64(res[w], (int)(lane ^ 4u));
-        }
-        if (rd) {
-          // (2) verify, then decrypt, (3) slot work, re-encrypt
-          const uint4 want = shfl4(tl, (int)u);
-          const uint64_t hr0 = shfl_u64(hh[0], (int)rr), hr1 = shfl_u64(hh[1], (int)rr);
-          if (__ballot((u4lo(want) != (res[0] ^ hr0)) | (u4hi(want) != (res[1] ^ hr1))) && lane == 0)
-            atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
-#pragma unroll 1
-          for (uint32_t ph = 0; ph < 2; ++ph) {
-            lm_ctr(a.sc, te, rowbase + rj + u, opaque(a.sc.epoch + ph), v);
-            if (ph == 0u) {
-              const bool app = (pbits >> rr) & 1u, tch = (cbits >> rr) & 1u;
-              const uint32_t pslot = s_ppre[g] + __popc(pbits & ((1u << rr) - 1u));
-              const uint32_t cslot = s_cpre[g] + __popc(cbits & ((1u << rr) - 1u));
-              if (LB) {
-                const uint32_t bp = selu32(app, pslot, kSpDry), bs = selu32(tch, kSpBufs - 1u - cslot, kSpDry);
-      #pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) v[i] = sel4(app, sp_ld<LB>(s_lds, sp_addr(bp, f, i)), v[i]);
-      #pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) sp_st(s_lds, sp_addr(bs, f, i), v[i]);
-              } else {
-                if (app) {
-                  const uint4* src = a.ps + (sbase + pslot) * 64 + f * 8;
-      #pragma unroll
-                  for (uint32_t i = 0; i < 8; ++i) v[i] = ld_row<true>(&src[i]);
-                }
-                if (tch) {
-                  const uint32_t hp = s_sh[min(cslot, kShMax - 1u)];
-      #pragma unroll
-                  for (uint32_t i = 0; i < 8; ++i) st_drop(a.snapp, (uint64_t)hp * 64 + f * 8 + i, v[i]);
-                  if (f == 0u) {
-      #pragma unroll
-                    for (uint32_t i = 0; i < 8; ++i) st_drop(a.snapidp, (uint64_t)hp * 8 + i, v[i]);
-                  }
-                }
-              }
-              if (a.xon) xc = x_detect_lm(a, v, s_xw + wave * (kXepMax + 1) * 3, xc, s_xx, nx);
-            }
-          }
-        } else {
-          // (4) the write tag (lane r < 8 writes row r's: one whole line), the rows
-          const uint64_t t0 = shfl_u64(res[0] ^ shfl_u64(hh[0], (int)(32u + rr)), (int)(8u * (lane & 7u)));
-          const uint64_t t1 = shfl_u64(res[1] ^ shfl_u64(hh[1], (int)(32u + rr)), (int)(8u * (lane & 7u)));
-          if (lane < 8u)
-            a.mtag[rowbase + rj + lane] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1,
-                                                     (uint32_t)(t1 >> 32));
-          uint4* tile = part + (uint64_t)rj * 64;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) st_row<true>(&tile[i * 64 + lane], v[i]);
-        }
-      }
-    }
-#else
     if (g < ngroups) {
       // the group's header PRFs: lane l < 32 row g*32 + l at the read epoch,
       // lane 32 + l the same row at the write epoch; the pending flag of a
@@ -471,12 +346,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         for (int i = 0; i < 8; ++i) st_row<true>(&tile[i * 64 + lane], v[i]);
       }
     }
-#endif
     // the waves meet after every round: the expiry lists merge in row order
-    // (without expiry they do not meet in the stream, so waves drift apart
-    // and one's AES rounds overlap another's BLAKE2b; a.xon is kernel-uniform)
     if (lane == 0) s_xc[wave] = xc;
-    if (GVS_SP_ROUNDSYNC || a.xon) __syncthreads();
+    __syncthreads();
     if (a.xon) {
       const uint32_t tot = x_merge2<NW>(a.xep, s_xw, s_xc, s_xp, s_xt);
       __syncthreads();

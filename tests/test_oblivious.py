@@ -93,10 +93,11 @@ SHAPES = {
                  pmc_kernels=("k_wire_decode", "sr::k_sr_verify", "k_wire_encode")),
 }
 FILL_BATCHES = 3
-# A batch whose kernels made more uncached L2 requests than this re-walked the
-# page tables (an environmental GPU TLB invalidation, DESIGN.md §3 "A TLB
-# invalidation nothing in the process causes": ~140 per GiB touched; a normal
-# batch makes none); see exclusions() for how such a batch is treated.
+# A batch whose kernels made more uncached L2 requests than half the process's
+# first batch (and at least this) re-walked the page tables (an environmental
+# GPU TLB invalidation, DESIGN.md §3 "A TLB invalidation nothing in the process
+# causes": ~140 per GiB touched); see exclusions() for how such a batch is
+# treated.
 UC_WALK = 64
 SEEDS = (1234, 99, 5)
 PER_SEED = 2
@@ -267,7 +268,12 @@ def exclusions(per):
     out = {}
     for mix, bs in per.items():
         n0 = len(bs) - N_MEAS
-        walks = [i for i in range(n0, len(bs)) if sum(x[4] for x in bs[i]) > UC_WALK]
+        uc = [sum(x[4] for x in b) for b in bs]
+        # a re-walk touches every page the batch's kernels touch, as the
+        # process's first batch did on first touch: half of that is the bar
+        # (hot mixes make up to ~230 uncached requests in every batch)
+        bar = max(UC_WALK, uc[0] / 2)
+        walks = [i for i in range(n0, len(bs)) if uc[i] > bar]
         out[mix] = set(walks) if len(walks) == 1 else set()
     return out
 

@@ -54,22 +54,6 @@ case "$2" in
       GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
         python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
     done ;;
-  m2ab)  # the sealed shape's FETCH_SIZE counters, in-tree build and ab/libgvstore_ma1wg.so
-    step obl_auth_v0 900 $PT tests/test_oblivious.py -k "hbm_bytes_identical and FETCH_SIZE-auth"
-    cp gpurun_out/oblivious_FETCH_SIZE_auth.txt "$O/obl_FETCH_auth_v0.txt"
-    GVS_LIB_OVERRIDE=ab/libgvstore_ma1wg.so step obl_auth_v1 900 $PT tests/test_oblivious.py -k "hbm_bytes_identical and FETCH_SIZE-auth"
-    cp gpurun_out/oblivious_FETCH_SIZE_auth.txt "$O/obl_FETCH_auth_v1.txt" ;;
-  codesize)  # code-size variants of the sealed passes: parity, bench, the sealed counter shape
-    step seal_tests 600 $PT $SEALT
-    GVS_LIB_OVERRIDE=ab/libgvstore_jobs.so step seal_tests_jobs 600 $PT tests/test_gpu_seal.py
-    step bench_auth_intree 300 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0
-    for v in ${CSV:-jobs:12 jobs:16 roll:12}; do
-      lib=${v%%:*}; nw=${v##*:}
-      GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
-        python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
-    done
-    step obl_auth 900 $PT tests/test_oblivious.py -k "hbm_bytes_identical and FETCH_SIZE-auth"
-    cp gpurun_out/oblivious_FETCH_SIZE_auth.txt "$O/" ;;
   kplain)  # per-kernel stats of the device-buffer C3 batches alone (no host or wire paths)
     step kstats_plain 400 rocprofv3 --kernel-trace --stats -d "$O/kp" -o run --output-format csv -- \
       python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10 --warmup 2
