@@ -52,15 +52,28 @@ __device__ inline B2State leaf_key(const uint64_t* s_lk) {
 }
 
 // XOR of the row's four leaf PRFs (lanes 4u .. 4u + 3) over the lane's 256-B
-// leaf, in every lane of the row
-__device__ inline void leaf_sum4(const uint64_t* s_lk, const uint4 (&v)[kMA], uint64_t r[2]) {
-  uint64_t m[32];
+// leaf, in every lane of the row.  The leaf's two compressions share one copy
+// of the code: the halves of v are swapped between them (and back after).
+__device__ inline void leaf_sum4(const uint64_t* s_lk, uint4 (&v)[kMA], uint64_t r[2]) {
+  B2State k = leaf_key(s_lk);
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < 2; ++blk) {
+    uint64_t m[16];
 #pragma unroll
-  for (int q = 0; q < kMA; ++q) {
-    m[2 * q] = u4lo(v[q]);
-    m[2 * q + 1] = u4hi(v[q]);
+    for (int q = 0; q < 8; ++q) {
+      m[2 * q] = u4lo(v[q]);
+      m[2 * q + 1] = u4hi(v[q]);
+    }
+    b2_compress(k, m, 128u + 128u * (blk + 1u), blk == 1u);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 x = v[q];
+      v[q] = v[q + 8];
+      v[q + 8] = x;
+    }
   }
-  leaf_prf(leaf_key(s_lk), m, r);
+  r[0] = k.h[0];
+  r[1] = k.h[1];
 #pragma unroll
   for (int w = 0; w < 2; ++w) {
     r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 1u));
@@ -76,7 +89,7 @@ __device__ inline void ma_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
 #pragma unroll
   for (uint32_t i = 0; i < kMA; i += NB) {
     uint4 ks[NB];
-    ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
+    ctr_keystream_jn<NB, true>(c.rk, te, c1, i, ks);  // rounds rolled: code size (gvs_seal_dev.h)
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       v[i + b] = xor4(v[i + b], ks[b]);
@@ -422,39 +435,61 @@ __global__ __launch_bounds__(256, 2) void k_m2a(MArgs a) {
   for (uint32_t j0 = wave * kMA; j0 < a.Sr; j0 += kRowWaves * kMA, ++ci) {
     uint4 v[kMA];
     const uint64_t t = ((uint64_t)q * a.Sr + j0) / kMA;
-    ma_load(v, a.mbox, t);
-    ma_unseal(a, s_te, s_lk, q, j0, v);
-    // the chunk's side entries, lane u < 16 row u's plaintext
-    uint4 mine = *hole(s_te, kHoSide + j0 + (lane & (kMA - 1u)));
-    uint32_t mm = 0;
-#pragma unroll
-    for (int u = 0; u < kMA; ++u) mm |= (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0) ? (1u << u) : 0u;
-    mm = __builtin_amdgcn_readfirstlane(mm);
-    const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
-    const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
-    uint32_t mq = mm;
-    for (uint32_t r = 0; r < nr; ++r) {
-      const uint32_t low = mq & (0u - mq);
-      mq &= mq - 1u;
-      step(v, mine, low, j0, d0 + dlo + (r - nt));
-    }
-    // re-seal: the side entries (new ciphertext kept for the write headers),
-    // the rows, their leaf sums
-    const uint4 sct = xor4(mine, *hole(s_te, kHoKsw + j0 + (lane & (kMA - 1u))));
-    if (lane < (uint32_t)kMA) {
-      side[j0 + lane] = sct;
-      *hole(s_te, kHoKsw + j0 + lane) = sct;
-    }
     const uint32_t u = lane >> 2;
-    ma_ctr(a.sc, lds_te(s_te), (uint64_t)q * a.Sr + j0 + u, ep, v);
-    uint64_t ls[2];
-    leaf_sum4(s_lk, v, ls);
-    if ((lane & 3u) == 0u)
-      *hole(s_te, kHoLsum + j0 + u) = make_uint4((uint32_t)ls[0], (uint32_t)(ls[0] >> 32), (uint32_t)ls[1],
-                                                 (uint32_t)(ls[1] >> 32));
-    uint4* p = a.mbox + t * (kMA * 64);
+    const uint64_t row = (uint64_t)q * a.Sr + j0 + u;
+    // four jobs, one copy of each crypto step: 0 verify, 1 decrypt and the
+    // mailbox steps, 2 re-encrypt, 3 the new leaf sums and the stores.  The
+    // unrolled sequence (220 KB of code; k_m1a's 112 KB) made the read pass's
+    // FETCH_SIZE follow the request mix by 17-30 KiB under the all-miss and
+    // hot mixes (profiles/r05e_*, r05h_*), where the rolled form is flat
+    // within 1 KiB (r05g): the steps between the crypto stretches differ by
+    // chunk with the mix, and so did what instruction lines the unrolled code
+    // had to fetch again.
+#pragma unroll 1
+    for (uint32_t job = 0; job < 4; ++job) {
+      if (job == 0u) ma_load(v, a.mbox, t);
+      if (job == 0u || job == 3u) {
+        uint64_t ls[2];
+        leaf_sum4(s_lk, v, ls);
+        if (job == 0u) {  // the read tag: H at the read epoch (prepass) over the old side ciphertext
+          const uint4 hr = *hole(s_te, kHoHr + j0 + u);
+          const uint4 want = a.btag[row];  // 16 rows' tags: two whole lines
+          const bool bad = (u4lo(want) != (ls[0] ^ u4lo(hr))) | (u4hi(want) != (ls[1] ^ u4hi(hr)));
+          if (__ballot(bad) && lane == 0) atomicOr(&a.scal->error, 8u);
+        } else {  // the write tags are finished after the stream (H over the new side ciphertext)
+          if ((lane & 3u) == 0u)
+            *hole(s_te, kHoLsum + j0 + u) = make_uint4((uint32_t)ls[0], (uint32_t)(ls[0] >> 32), (uint32_t)ls[1],
+                                                       (uint32_t)(ls[1] >> 32));
+          uint4* p = a.mbox + t * (kMA * 64);
 #pragma unroll
-    for (int i = 0; i < kMA; ++i) st_stream(p, (uint64_t)i * 64 + lane, v[i]);
+          for (int i = 0; i < kMA; ++i) st_stream(p, (uint64_t)i * 64 + lane, v[i]);
+        }
+      } else {
+        ma_ctr(a.sc, lds_te(s_te), row, job == 1u ? a.sc.epoch : ep, v);
+        if (job == 1u) {
+          // the chunk's side entries, lane u < 16 row u's plaintext
+          uint4 mine = *hole(s_te, kHoSide + j0 + (lane & (kMA - 1u)));
+          uint32_t mm = 0;
+#pragma unroll
+          for (int uu = 0; uu < kMA; ++uu) mm |= (s_sg[j0 + uu] >= 0 || s_place[j0 + uu] >= 0) ? (1u << uu) : 0u;
+          mm = __builtin_amdgcn_readfirstlane(mm);
+          const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
+          const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
+          uint32_t mq = mm;
+          for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t low = mq & (0u - mq);
+            mq &= mq - 1u;
+            step(v, mine, low, j0, d0 + dlo + (r - nt));
+          }
+          // the new side entries sealed (ciphertext kept for the write headers)
+          const uint4 sct = xor4(mine, *hole(s_te, kHoKsw + j0 + (lane & (kMA - 1u))));
+          if (lane < (uint32_t)kMA) {
+            side[j0 + lane] = sct;
+            *hole(s_te, kHoKsw + j0 + lane) = sct;
+          }
+        }
+      }
+    }
   }
   if (nch == 0) {
     uint4 v[kMA], mine = make_uint4(0, 0, 0, 0);

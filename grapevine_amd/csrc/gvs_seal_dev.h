@@ -210,9 +210,11 @@ __device__ inline void ctr_keystream2_j(const AesRk& rk, const LdsTe& te, const 
 // The same for NB independent blocks at once: each round issues all 16 NB
 // lookups before combining them, so a lane waits for NB / 2 times fewer LDS
 // round trips per block (the sealed pass is bound by that latency).
-template <int R0, int NB>
+template <int R0, int NB, bool ROLL = false>
 __device__ inline void aes128_rounds_n(const AesRk& rk, const LdsTe& te, uint32_t (&s)[NB][4]) {
-#pragma unroll
+  // ROLL: one copy of the round (round keys read by index, scalar loads), for
+  // the sealed mailbox passes (gvs_mauth.h)
+#pragma unroll(ROLL ? 1 : 8)
   for (int r = R0; r < 10; ++r) {
     uint32_t l[NB][16];
 #pragma unroll
@@ -245,7 +247,7 @@ __device__ inline void aes128_rounds_n(const AesRk& rk, const LdsTe& te, uint32_
 }
 
 // keystream blocks j0 + i0 .. j0 + i0 + NB - 1 of the row (ctr_round1_row)
-template <int NB>
+template <int NB, bool ROLL = false>
 __device__ inline void ctr_keystream_jn(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1, uint32_t i0,
                                         uint4 (&ks)[NB]) {
   uint32_t s[NB][4];
@@ -257,7 +259,7 @@ __device__ inline void ctr_keystream_jn(const AesRk& rk, const LdsTe& te, const 
     s[b][2] = c1.t[2];
     s[b][3] = c1.t[3];
   }
-  aes128_rounds_n<2, NB>(rk, te, s);
+  aes128_rounds_n<2, NB, ROLL>(rk, te, s);
 #pragma unroll
   for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
 }
