@@ -11,7 +11,7 @@
 
 #include <cstdio>
 
-constexpr int kSteps = 2048;
+constexpr int kSteps = 32768;  // long enough that launch and setup (~7 us) do not matter
 
 template <int K>
 __global__ __launch_bounds__(1024) void k_op(uint32_t* out, uint32_t seed) {
@@ -47,6 +47,10 @@ __global__ __launch_bounds__(1024) void k_op(uint32_t* out, uint32_t seed) {
       } else if (K == 6) {  // table read: address from the previous value, conflict-free
         const uint32_t addr = ((a[i] & 0xffu) << 8) | lane4;
         a[i] = s_t[addr >> 2] ^ b;
+      } else if (K == 8) {  // the same XOR in the 8-byte VOP3 encoding
+        asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+      } else if (K == 9) {  // v_add_u32 (VOP2)
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
       } else if (K == 7) {  // v_xor_b32 pair (64-bit XOR) + 2 v_alignbit (64-bit rotate by 24)
         uint32_t lo = (uint32_t)c[i], hi = (uint32_t)(c[i] >> 32);
         asm volatile("v_xor_b32 %0, %0, %2\n\tv_xor_b32 %1, %1, %3\n\t"
@@ -95,6 +99,8 @@ int main() {
     run<5>("v_xor_b32", 1, w, d);
     run<6>("ds_read_b32 (+and/or/xor)", 1, w, d);
     run<7>("2 x v_xor_b32 + 2 x v_alignbit_b32", 4, w, d);
+    run<8>("v_xor_b32_e64 (VOP3 encoding)", 1, w, d);
+    run<9>("v_add_u32 (VOP2)", 1, w, d);
   }
   (void)hipFree(d);
   return 0;
