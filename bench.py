@@ -68,6 +68,7 @@ def parse():
     p.add_argument("--prediction-json", default=os.path.join(ROOT, "profiles", "scale_prediction.json"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     p.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_auth_latest.json"))
+    p.add_argument("--valu-mix-json", default=os.path.join(ROOT, "profiles", "valu_mix_k_spass.json"))
     return p.parse_args()
 
 
@@ -667,8 +668,22 @@ def main():
             except (OSError, ValueError):
                 pass
             v_ach = insts / (rpass_ms * 1e-3) / 1e9 if insts else None
+            # the ceiling of the pass's own instruction mix: three-source
+            # operations issue 1.35-1.55x slower than the nominal rate
+            # (tools/valu_mix_peak.py over tools/valu_rate_probe.hip)
+            mix = None
+            try:
+                with open(a.valu_mix_json) as f:
+                    mj = json.load(f)
+                if mj.get("source_sha") == src_sha and not a.sealed_waves:
+                    mix = {"ceiling": mj["ceiling_g_wave_instr_per_s"], "unit": "G wave-instr/s",
+                           "frac": v_ach / mj["ceiling_g_wave_instr_per_s"] if v_ach else None,
+                           "source": os.path.relpath(a.valu_mix_json, ROOT), "probe": mj.get("probe")}
+            except (OSError, ValueError, KeyError):
+                pass
             roofline = {"bound": "valu", "achieved": v_ach, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                         "frac": v_ach / VALU_PEAK_GINST if v_ach else None, "traffic": None,
+                        "mix_ceiling": mix,
                         "kernel": f"k_spass (fixed-schedule sealed message-table pass; "
                                   f"{a.sealed_waves or 'default'} waves per workgroup)",
                         "valu_insts_per_launch": insts, "kernel_ms": rpass_ms,

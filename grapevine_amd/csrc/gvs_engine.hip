@@ -162,6 +162,7 @@ struct Engine {
 struct Router {
   uint32_t* dest = nullptr;
   uint64_t* rkey = nullptr;  // routing keys, sorted per window (hot-key cap)
+  uint64_t* marks = nullptr; // shed marks by sorted position, then sorted back to request order
   uint32_t* shed = nullptr;
   uint32_t* bcnt = nullptr;
   uint32_t* pos = nullptr;
@@ -653,6 +654,7 @@ static int router_init(gvs_handle* h, Router& r) {
   const uint64_t B = h->Bsub, SC = (uint64_t)h->S * h->C;
   if (int rc = dalloc_t(h, &r.dest, B)) return rc;
   if (int rc = dalloc_t(h, &r.rkey, B)) return rc;
+  if (int rc = dalloc_t(h, &r.marks, B)) return rc;
   if (int rc = dalloc_t(h, &r.shed, B)) return rc;
   if (int rc = dalloc_t(h, &r.bcnt, (B / 1024) * h->S)) return rc;
   if (int rc = dalloc_t(h, &r.pos, B)) return rc;
@@ -1129,7 +1131,9 @@ static int route(gvs_handle* h, const Router& r, const Engine& e, const uint4* i
   const uint32_t nblk = h->Bsub / 1024;
   hipLaunchKernelGGL(k_route_dest, dim3(nblk), dim3(1024), 0, s, a);
   if (int rc = sort_keys<uint64_t, 1>(h, r.rkey, h->Bsub)) return rc;  // by (routing key, index)
-  hipLaunchKernelGGL(k_route_cap, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_route_mark, dim3(nblk), dim3(1024), 0, s, a, r.marks);
+  if (int rc = sort_keys<uint64_t, 1>(h, r.marks, h->Bsub)) return rc;  // back to request order
+  hipLaunchKernelGGL(k_route_apply, dim3(nblk), dim3(1024), 0, s, a, (const uint64_t*)r.marks);
   hipLaunchKernelGGL(k_route_hist, dim3(nblk), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_route_pos, dim3(nblk), dim3(1024), 0, s, a);
   if (n) hipLaunchKernelGGL(k_route_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
@@ -2648,7 +2652,7 @@ int gvs_route_plan(const gvs_config* cfg, const gvs_request* reqs, uint32_t n, u
     dest[i] = route_dest_key(a, i, k);
     keys[i] = ((uint64_t)k << 32) | i;
   }
-  std::sort(keys.begin(), keys.end());  // the hot-key cap, as k_route_cap
+  std::sort(keys.begin(), keys.end());  // the hot-key cap, as k_route_mark / k_route_apply
   if (shed) std::fill(shed, shed + n, (uint8_t)0);
   for (uint32_t j = kRouteKeyCap; j < n; ++j) {
     const uint32_t k = (uint32_t)(keys[j] >> 32), i = (uint32_t)keys[j];

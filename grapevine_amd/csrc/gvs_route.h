@@ -42,7 +42,7 @@ struct RouteArgs {
   const uint4* in;   // caller requests (kAbiU4 stride)
   uint32_t n, B, S, C;
   uint32_t* dest;    // B
-  uint64_t* rkey;    // B: routing key << 32 | index, sorted by k_route_cap's caller
+  uint64_t* rkey;    // B: routing key << 32 | index, sorted by the router (k_route_mark reads them)
   uint32_t* shed;    // B: 1 = shed (the key's cap was reached)
   uint32_t* bcnt;    // nblk * S: per-block per-shard counts
   uint32_t* pos;     // B: slot in `send`, or kNone
@@ -114,31 +114,32 @@ __global__ __launch_bounds__(1024) void k_route_dest(RouteArgs a) {
 // Over the keys sorted by (key, index): a request is shed when the request
 // kRouteKeyCap places before it has the same key (it is at least the
 // (kRouteKeyCap + 1)-th of its key in this window); a shed request goes to
-// shard i mod S.  One workgroup: the flags go through an LDS bitmap indexed
-// by request, so the data-dependent permutation (sorted position -> request)
-// stays inside one XCD's L2 (DESIGN.md §3 rule 4: scattered 4-B writes from
-// many workgroups made FETCH_SIZE follow the key order), and shed / dest are
-// written in request order.
-constexpr uint32_t kRouteCapWords = 16384;  // bitmap words: B <= 2^19
-__global__ __launch_bounds__(1024) void k_route_cap(RouteArgs a) {
-  __shared__ uint32_t s_bits[kRouteCapWords];
-  const uint32_t nw = (a.B + 31) / 32;
-  for (uint32_t w = threadIdx.x; w < nw; w += 1024) s_bits[w] = 0;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < a.B; j += 1024) {
-    const uint64_t k = a.rkey[j];
-    const uint64_t kp = a.rkey[j >= kRouteKeyCap ? j - kRouteKeyCap : j];
-    const uint32_t key = (uint32_t)(k >> 32), i = (uint32_t)k;
-    const bool shed = j >= kRouteKeyCap && (key & 3u) != kKeyNone && (uint32_t)(kp >> 32) == key;
-    atomicOr(&s_bits[i >> 5], (shed ? 1u : 0u) << (i & 31u));  // one per position, always
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < a.B; i += 1024) {
-    const bool shed = (s_bits[i >> 5] >> (i & 31u)) & 1u;
-    const uint32_t d = a.dest[i];
-    a.shed[i] = shed ? 1u : 0u;
-    a.dest[i] = shed ? i % a.S : d;
-  }
+// shard i mod S.  The flag is found at the sorted position and taken back to
+// request order by a second sort (by index), not by a scatter:
+//   * round 3 scattered 4-B writes by request index from many workgroups:
+//     FETCH_SIZE followed the key order (DESIGN.md §3 rule 4);
+//   * round 4 set bits of an LDS bitmap by request index in one workgroup:
+//     a hot key's sorted run has dense request indices, so the wave's LDS
+//     atomics met on few words and serialised, and the kernel ran 10-20 us
+//     longer under the hot mixes (profiles/r05k_timing_c3_routed.txt).
+// k_route_mark: sorted position j -> (index << 32 | shed), coalesced
+__global__ __launch_bounds__(1024) void k_route_mark(RouteArgs a, uint64_t* marks) {
+  const uint32_t j = blockIdx.x * 1024 + threadIdx.x;
+  const uint64_t k = a.rkey[j];
+  const uint64_t kp = a.rkey[j >= kRouteKeyCap ? j - kRouteKeyCap : j];
+  const uint32_t key = (uint32_t)(k >> 32), i = (uint32_t)k;
+  const bool shed = j >= kRouteKeyCap && (key & 3u) != kKeyNone && (uint32_t)(kp >> 32) == key;
+  marks[j] = ((uint64_t)i << 32) | (shed ? 1u : 0u);
+}
+
+// after the marks are sorted (by index): shed flags and destinations in
+// request order
+__global__ __launch_bounds__(1024) void k_route_apply(RouteArgs a, const uint64_t* marks) {
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const bool shed = (marks[i] & 1u) != 0u;
+  const uint32_t d = a.dest[i];
+  a.shed[i] = shed ? 1u : 0u;
+  a.dest[i] = shed ? i % a.S : d;
 }
 
 // per-block per-shard histogram of the final destinations (all S bins stored)

@@ -214,7 +214,8 @@ template <int R0, int NB, bool ROLL = false>
 __device__ inline void aes128_rounds_n(const AesRk& rk, const LdsTe& te, uint32_t (&s)[NB][4]) {
   // ROLL: one copy of the round (round keys read by index, scalar loads), for
   // the sealed mailbox passes (gvs_mauth.h)
-#pragma unroll(ROLL ? 1 : 8)
+  constexpr int kUnroll = ROLL ? 1 : 10;
+#pragma unroll kUnroll
   for (int r = R0; r < 10; ++r) {
     uint32_t l[NB][16];
 #pragma unroll

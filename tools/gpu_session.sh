@@ -54,6 +54,15 @@ case "$2" in
       GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
         python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
     done ;;
+  timeall)  # every timing shape, then the default bench line
+    step timing_all 1000 $PT tests/test_timing.py
+    cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
+    step bench 400 python3 bench.py --no-cpu ;;
+  routed)  # the sharded path: parity, counters, timing
+    step sharded_tests 600 $PT tests/test_gpu_sharded.py
+    step obl_routed 900 $PT tests/test_oblivious.py -k "routed"
+    step timing_routed 600 $PT tests/test_timing.py -k "routed"
+    cp gpurun_out/timing_c3_routed.txt gpurun_out/oblivious_FETCH_SIZE_routed.txt gpurun_out/oblivious_WRITE_SIZE_routed.txt "$O/" 2>/dev/null ;;
   kplain)  # per-kernel stats of the device-buffer C3 batches alone (no host or wire paths)
     step kstats_plain 400 rocprofv3 --kernel-trace --stats -d "$O/kp" -o run --output-format csv -- \
       python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10 --warmup 2
