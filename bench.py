@@ -54,7 +54,7 @@ def parse():
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
-    p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12, 16),
+    p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12),
                    help="--auth: waves per workgroup of the sealed message pass (0: the store's choice)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "

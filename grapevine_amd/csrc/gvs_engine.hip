@@ -265,7 +265,7 @@ struct gvs_handle {
   uint32_t* te = nullptr;    // AES table on the device
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
-  int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12, 16; 0: by S)
+  int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12; 0: by S)
   HostPipe pipe;
   WireStage wire;
   WirePipe wpipe;
@@ -841,6 +841,16 @@ static AllocArgs aargs(const Engine& e) {
 
 // ------------------------------------------- pipeline 2: fixed-slot transactions
 
+// a prime not dividing n (so x -> x * m mod n is a permutation) with n * m
+// below 2^32 (the kernels compute x * m in 32 bits): the largest such prime
+// of the list, 1 when none is
+static uint32_t scatter_mul(uint64_t n) {
+  for (uint32_t m : {4093u, 4091u, 4079u, 2039u, 2029u, 1021u, 1019u, 509u, 503u, 251u, 241u, 127u, 113u,
+                     61u, 59u, 31u, 29u, 13u, 11u, 7u, 5u, 3u})
+    if (n % m != 0u && n * m < (1ull << 32)) return m;
+  return 1u;
+}
+
 static MArgs margs2(const gvs_handle* h, const Engine& e) {
   MArgs a = margs(h, e);
   a.gtx = e.gtx;
@@ -850,17 +860,9 @@ static MArgs margs2(const gvs_handle* h, const Engine& e) {
   a.mdry = e.mdry;
   a.stamp = e.stamp_run;
   a.cm = e.cm;
-  // a prime not dividing Q*cm (so x -> x * m mod Q*cm is a permutation) with
-  // Q*cm * m below 2^32 (gvs_mtx.h computes slot x * m in 32 bits): the
-  // largest such prime of the list, 1 when none is
-  const uint64_t qc = (uint64_t)e.Q * e.cm;
-  a.sink_mul = 1;
-  for (uint32_t m : {4093u, 4091u, 4079u, 2039u, 2029u, 1021u, 1019u, 509u, 503u, 251u, 241u, 127u, 113u,
-                     61u, 59u, 31u, 29u, 13u, 11u, 7u, 5u, 3u})
-    if (qc % m != 0u && qc * m < (1ull << 32)) {
-      a.sink_mul = m;
-      break;
-    }
+  a.sink_mul = scatter_mul((uint64_t)e.Q * e.cm);
+  a.snap_mul = scatter_mul(e.B);
+  a.snap_n = e.B;
   return a;
 }
 
@@ -940,6 +942,8 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     a.mpos = e.mpos;
     a.ops = e.ops;
     a.msnapp = e.msnapp;
+    a.snap_mul = scatter_mul(e.B);
+    a.snap_n = e.B;
     a.mpid = e.mpid;
     a.m1out = e.m1out;
     a.N = e.N;
@@ -1016,8 +1020,6 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
       hipLaunchKernelGGL((k_spass<8, false>), dim3(e.W), dim3(512), 0, s, a);
     else if (nw == 12)
       hipLaunchKernelGGL((k_spass<12, true>), dim3(e.W), dim3(768), 0, s, a);
-    else if (nw == 16)
-      hipLaunchKernelGGL((k_spass<16, true>), dim3(e.W), dim3(1024), 0, s, a);
     else if (nw == 4)
       hipLaunchKernelGGL((k_spass<4, true>), dim3(e.W), dim3(256), 0, s, a);
     else
@@ -2400,7 +2402,7 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
 
 int gvs_set_option(gvs_handle* h, const char* key, int64_t value) {
   if (!h || !key) return GVS_ERR_INVALID_ARG;
-  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12 || value == 16)) {
+  if (std::strcmp(key, "sealed_pass_waves") == 0 && (value == 0 || value == 4 || value == 8 || value == 12)) {
     h->sealed_nw = (int)value;
     return GVS_OK;
   }

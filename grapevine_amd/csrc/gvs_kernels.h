@@ -494,7 +494,17 @@ struct MArgs {
   uint4* mdry;         // Q x 8 KiB: each workgroup's dry-run lines (gvs_mtx.h: one 1 KiB per use)
   uint32_t stamp, cm;
   uint32_t sink_mul;   // MSNAP sink line of global slot x: x * sink_mul mod Q*cm (a permutation)
+  uint32_t snap_mul, snap_n;  // MSNAPP line of head position p: p * snap_mul mod snap_n (snap_line)
 };
+
+// The MSNAPP line of sorted position p: a permutation of the B lines (snap_mul
+// prime to B, B * snap_mul < 2^32).  In position order, a partition's group
+// snapshots fell on neighbouring lines while its unused slots' sink lines are
+// scattered (sink_mul), and the two kinds of write ran at different speeds:
+// k_m1x 11 us faster under batches without mailbox groups at the routed
+// shape's partition sizes (profiles/r05l_timing_c3_routed.txt).  Both are
+// scattered the same way now.
+__device__ inline uint32_t snap_line(uint32_t p, uint32_t mul, uint32_t n) { return (p * mul) % n; }
 
 // ---------------------------------------------------------- allocation
 

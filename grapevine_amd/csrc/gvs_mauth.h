@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
                            make_uint4(0, 0, 0, 0));
     cur = sel4(lane == 0, hdr, sel4(lane == 1 || slot_it, make_uint4(0, 0, 0, 0), cur));
     const uint32_t sl = (uint32_t)(((uint64_t)(q * a.cm + (uint32_t)k) * a.sink_mul) % ((uint64_t)a.Q * a.cm));
-    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : a.msnap + (uint64_t)sl * 64;
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)snap_line(G.head, a.snap_mul, a.snap_n) * 64 : a.msnap + (uint64_t)sl * 64;
     st_drop(dst, lane, cur);
   };
   uint32_t ci = 0;
@@ -316,7 +316,10 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
 // the sealed write pass (k_m2x): every row rewritten, every result slot read
 // once; rows re-encrypted and their side entries re-sealed at epoch + 1, the
 // tags after the stream
-__global__ __launch_bounds__(256, 2) void k_m2a(MArgs a) {
+#ifndef GVS_M2A_WGS
+#define GVS_M2A_WGS 2  // workgroups per CU the register budget is sized for
+#endif
+__global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   extern __shared__ uint4 s_dyn[];
   GroupM* g = reinterpret_cast<GroupM*>(s_dyn);
   GVS_TE_LDS s_te[kTeWords];

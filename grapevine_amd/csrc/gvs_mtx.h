@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     // lines over MSNAPP: the partition's 1-KiB sink lines written in a row
     // made a batch without groups 7-9 us faster (DRAM page locality)
     const uint32_t sl = ((q * a.cm + (uint32_t)k) * a.sink_mul) % (a.Q * a.cm);
-    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : a.msnap + (uint64_t)sl * 64;
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)snap_line(G.head, a.snap_mul, a.snap_n) * 64 : a.msnap + (uint64_t)sl * 64;
     st_drop(dst, lane, cur);
   };
   uint32_t ci = 0;  // the wave's chunk index
@@ -393,7 +393,8 @@ struct M1rArgs {
   GVS_VSCAN_FIELDS
   const uint4* mpos;
   const OpState* ops;
-  const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions
+  const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions (snap_line)
+  uint32_t snap_mul, snap_n;
   const uint4* mpid;    // B x 16 B: each position's message id (k_gtx)
   M1Out* m1out;
   uint64_t N;
@@ -427,7 +428,7 @@ struct M1rOp {
   // every op reads its own position's line (heads find their group's
   // snapshot there; the others' lines are read and ignored)
   __device__ static const uint4* src_of(const Args& a, uint32_t p, uint4) {
-    return a.msnapp + (uint64_t)p * 64;
+    return a.msnapp + (uint64_t)snap_line(p, a.snap_mul, a.snap_n) * 64;
   }
   // k_vscan_a: every op's line is read, the defining op's kept
   __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4*) {

@@ -230,13 +230,27 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
   constexpr uint32_t R = kGatherPerWave;
   static_assert(R == 8, "wave_put_rec8");
   __shared__ uint4 s_rec[4][R * kAbiU4];
+  __shared__ uint32_t s_pos[4 * R], s_shed[4 * R];
   const uint32_t i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R, lane = lane_id();
+  // the block's 32 positions and shed flags: their two 128-B lines read whole
+  // by one instruction of wave 0 (the four waves' 32-B pieces, read by each
+  // wave itself, were fetched in 32- or 64-B requests as their timing fell:
+  // FETCH_SIZE +3.7 KiB under the all-miss and hot mixes, r05m)
+  if (threadIdx.x < 64) {
+    const uint32_t b = min(blockIdx.x * 4 * R + (lane & 31u), n - 1u);
+    const uint32_t x = lane < 32 ? pos[b] : shed[b];
+    if (lane < 32)
+      s_pos[lane] = x;
+    else
+      s_shed[lane - 32] = x;
+  }
+  __syncthreads();
   if (i0 >= n) return;
-  uint4 v[R], tw[R];
+  uint4 v[R], t = make_uint4(0, 0, 0, 0);  // t: lane r holds request r's status word
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {  // wave-uniform conditions
-    const uint32_t i = min(i0 + r, n - 1u);
-    const uint32_t p = pos[i];
+    const uint32_t i = min(i0 + r, n - 1u), il = i - blockIdx.x * 4 * R;
+    const uint32_t p = s_pos[il];
     // an overflowed batch (p == kNone) fails as a whole; out is then undefined
     // the status word's and the time word's 128-B lines are each read whole,
     // by 8 lanes in one instruction, and the word taken by a shuffle: a 16-B
@@ -245,7 +259,7 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
     // the hot mixes, profiles/r04ze_oblivious_FETCH_SIZE_routed.txt)
     v[r] = p != kNone ? back[(uint64_t)p * kSlotU4 + lane] : make_uint4(0, 0, 0, 0);
     const uint4 tl = p != kNone ? back[(uint64_t)p * kSlotU4 + 64 + (lane & 7u)] : make_uint4(0, 0, 0, 0);
-    tw[r] = shfl4(tl, 0);
+    uint4 tw = shfl4(tl, 0);
     const uint64_t tsa = (uint64_t)i * kAbiU4 + 5;  // the request's server time (record word 5)
     const uint4 tsl = in[(tsa & ~7ull) + (lane & 7u)];
     uint4 ts = shfl4(tsl, (int)(tsa & 7u));
@@ -254,15 +268,16 @@ __global__ __launch_bounds__(256) void k_route_gather(const uint32_t* __restrict
     // line was then read once per shed request: FETCH_SIZE followed the mix)
     keep4(ts);
     keep4(v[r]);
-    keep4(tw[r]);
-    const bool s = shed[i] != 0u;
-    v[r] = s ? (lane == 5 ? make_uint4(ts.x, ts.y, 0u, 0u) : make_uint4(0, 0, 0, 0)) : v[r];
-    tw[r] = s ? make_uint4(8u, 0, 0, 0) : tw[r];
+    keep4(tw);
+    const bool s = s_shed[il] != 0u;
+    v[r] = sel4(s, sel4(lane == 5, make_uint4(ts.x, ts.y, 0u, 0u), make_uint4(0, 0, 0, 0)), v[r]);
+    tw = sel4(s, make_uint4(8u, 0, 0, 0), tw);
+    // a mask select: `lane == r ? tw[r] : t` over an array was compiled to a
+    // select of addresses, which put the array in scratch (160 B per lane);
+    // scratch lines written back or not with the timing moved FETCH_SIZE by
+    // +-25 KiB (profiles/r05l_oblivious_FETCH_SIZE_routed.txt)
+    t = sel4(lane == r, tw, t);
   }
-  // the status words: lane r holds request r's
-  uint4 t = tw[0];
-#pragma unroll
-  for (uint32_t r = 1; r < R; ++r) t = lane == r ? tw[r] : t;
   wave_put_rec8(out + (uint64_t)i0 * kAbiU4, s_rec[threadIdx.x >> 6], v, t, n - i0);
 }
 

@@ -265,6 +265,81 @@ __device__ inline void ctr_keystream_jn(const AesRk& rk, const LdsTe& te, const 
   for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
 }
 
+// Two tables in the 64-KiB window (the sealed message pass, gvs_spass.h):
+// T0 as above, and T1 = T0 rotated right by 8 in the holes (entry x of
+// replica r at byte 256 x + 128 + 4 r: the same bank as T0's entry, so a
+// half-wave is still conflict-free).  A round column is then
+// T0[a] ^ T1[b] ^ ror16(T0[c] ^ T1[d]) ^ rk (FIPS-197 §5.2.1's T-table
+// identities): one rotation instead of three.  The pass is bound by the issue
+// of its three-source instructions (DESIGN.md §8 "Issue rates"), and the
+// rotations were 28 % of them.
+__device__ inline void load_te2(uint32_t* s_te, const uint32_t* g_te) {
+  for (uint32_t i = threadIdx.x; i < 256 * kTeRep; i += blockDim.x) {
+    const uint32_t t = g_te[i / kTeRep];
+    s_te[(i / kTeRep) * 64 + (i % kTeRep)] = t;
+    s_te[(i / kTeRep) * 64 + 32 + (i % kTeRep)] = (t >> 8) | (t << 24);
+  }
+}
+
+__device__ inline uint32_t te1_at(const LdsTe& t, uint32_t s, int k) {
+  const uint32_t off = __builtin_amdgcn_perm(s, t.lane4, 0x0c0c0400u | ((uint32_t)(4 + k) << 8));
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.base) + 128u + off);
+}
+
+// aes128_rounds_n on the two-table window
+template <int R0, int NB>
+__device__ inline void aes128_rounds_n2(const AesRk& rk, const LdsTe& te, uint32_t (&s)[NB][4]) {
+#pragma unroll
+  for (int r = R0; r < 10; ++r) {
+    uint32_t l[NB][16];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        l[b][4 * i + 0] = te_at(te, s[b][i], 3);
+        l[b][4 * i + 1] = te1_at(te, s[b][(i + 1) & 3], 2);
+        l[b][4 * i + 2] = te_at(te, s[b][(i + 2) & 3], 1);
+        l[b][4 * i + 3] = te1_at(te, s[b][(i + 3) & 3], 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        s[b][i] = xor3(l[b][4 * i], l[b][4 * i + 1], ror32(l[b][4 * i + 2] ^ l[b][4 * i + 3], 16)) ^ rk.w[4 * r + i];
+  }
+  uint32_t l[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) l[b][4 * i + k] = te_at(te, s[b][(i + k) & 3], 3 - k);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      s[b][i] = sbox_pack(l[b][4 * i], l[b][4 * i + 1], l[b][4 * i + 2], l[b][4 * i + 3]) ^ rk.w[40 + i];
+}
+
+template <int NB>
+__device__ inline void ctr_keystream_jn2(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1, uint32_t i0,
+                                         uint4 (&ks)[NB]) {
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint32_t t = te_at(te, c1.x3b0 ^ (i0 + (uint32_t)b), 0);
+    s[b][0] = c1.t[0] ^ ror32(t, 24);
+    s[b][1] = c1.t[1];
+    s[b][2] = c1.t[2];
+    s[b][3] = c1.t[3];
+  }
+  aes128_rounds_n2<2, NB>(rk, te, s);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
+}
+
 // The tile layout of a sealed message (or block) table: rows in tiles of 8
 // (8 KiB); inside a tile, 16-B unit i * 64 + L holds block 8 (L & 7) + i of
 // row L >> 3.  A wave's coalesced load of unit i into lane L (8 whole-KiB

@@ -48,10 +48,13 @@
 
 namespace gvs {
 
-constexpr uint32_t kSpBufs = 96;              // LDS staging buffers (1 KiB each)
+#ifndef GVS_SP_DUAL
+#define GVS_SP_DUAL 1  // T0 and T1 in the AES window (load_te2), every staging buffer after it
+#endif
+constexpr uint32_t kSpBufs = GVS_SP_DUAL ? 86 : 96;  // LDS staging buffers (1 KiB each)
 constexpr uint32_t kSpSlots = 64;             // transaction slots per partition (c) with LDS staging
 constexpr uint32_t kSpDry = kSpBufs;          // the dry buffer
-constexpr uint32_t kSpHoles = 32;             // buffers 0..31 live in the AES window's holes
+constexpr uint32_t kSpHoles = GVS_SP_DUAL ? 0 : 32;  // buffers living in the AES window's holes
 constexpr uint32_t kSpWords = kRowsMax / 32;  // bitmap words per partition
 
 // byte address (from the 64-KiB-aligned window at LDS 0) of 16-B block i of
@@ -61,7 +64,7 @@ __device__ inline uint32_t sp_addr(uint32_t b, uint32_t q, uint32_t i) {
   const uint32_t rot = ((i + q) & 7u) * 16u;
   const uint32_t hole = (8u * b + q) * 256u + 128u + rot;
   const uint32_t buf = 65536u + (b - kSpHoles) * 1024u + q * 128u + rot;
-  return selu32(b < kSpHoles, hole, buf);
+  return kSpHoles ? selu32(b < kSpHoles, hole, buf) : buf;
 }
 
 template <bool LB>
@@ -165,7 +168,10 @@ __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
 #pragma unroll
   for (uint32_t i = 0; i < 8; i += NB) {
     uint4 ks[NB];
-    ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
+    if (GVS_SP_DUAL)
+      ctr_keystream_jn2<NB>(c.rk, te, c1, i, ks);
+    else
+      ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       v[i + b] = xor4(v[i + b], ks[b]);
@@ -193,7 +199,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
-  load_te(s_lds, a.te);
+  if (GVS_SP_DUAL)
+    load_te2(s_lds, a.te);
+  else
+    load_te(s_lds, a.te);
   if (tid < 64) s_lk[tid] = a.sc.leafk0[tid >> 3].h[tid & 7u];
   const uint32_t nwd = a.S / 32u;
   for (uint32_t o = tid; o < nwd; o += 64 * NW) {

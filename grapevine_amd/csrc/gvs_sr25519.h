@@ -420,13 +420,15 @@ GVS_SR_FN uint32_t sc_mask_lt_l(const Fe& s) {
   return 0u - ((uint32_t)(t >> 32) & 1u);
 }
 
-// a 512-bit little-endian integer mod l, one bit at a time (fixed 512 steps)
-GVS_SR_FN_NI Fe sc_reduce_wide(const uint32_t w[16]) {
+// a 512-bit little-endian integer mod l, one bit at a time (fixed 512 steps);
+// word i at w[i * stride] (a thread's LDS column: a private array passed by
+// pointer to this out-of-line function lived in scratch)
+GVS_SR_FN_NI Fe sc_reduce_wide(const uint32_t* w, uint32_t stride) {
   const Fe l = sc_l();
   Fe r = fe_zero();
 #pragma unroll
   for (int wi = 15; wi >= 0; --wi) {
-    const uint32_t word = w[wi];
+    const uint32_t word = w[wi * stride];
     for (int b = 31; b >= 0; --b) {
       uint32_t c = (word >> b) & 1u;
 #pragma unroll
@@ -698,7 +700,7 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   Strobe s{sponge + tid, 0, 0, 0};
   for (int w = 0; w < 50; ++w) s.st[w * kSrThreads] = 0;
   {
-    const char init[] = "\x01\xa8\x01\x00\x01\x60STROBEv1.0.2";
+    const char* init = "\x01\xa8\x01\x00\x01\x60STROBEv1.0.2";  // the literal, not a local copy
     for (int i = 0; i < 18; ++i) s.xor_byte(i, (uint8_t)init[i]);
     s.keccak();
   }
@@ -706,7 +708,7 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   s.label("dom-sep");
   s.meta_len(14);
   s.begin_op(2u);
-  const char sctx[] = "SigningContext";
+  const char* sctx = "SigningContext";
   for (int i = 0; i < 14; ++i) s.absorb((uint8_t)sctx[i]);
   s.label("");
   s.meta_len(a.ctx_len);
@@ -721,7 +723,7 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   s.label("proto-name");
   s.meta_len(11);
   s.begin_op(2u);
-  const char proto[] = "Schnorr-sig";
+  const char* proto = "Schnorr-sig";
   for (int i = 0; i < 11; ++i) s.absorb((uint8_t)proto[i]);
   // commit_point(b"sign:pk", pk), commit_point(b"sign:R", R)
   s.label("sign:pk");
@@ -736,13 +738,13 @@ __global__ void __launch_bounds__(kSrThreads) k_sr_verify(SrArgs a) {
   s.label("sign:c");
   s.meta_len(64);
   s.begin_op(1u | 2u | 4u);  // I | A | C
-  uint32_t wide[16];
+  // the 16 words go to sponge words 50-65 of this thread (past the state)
   for (int i = 0; i < 16; ++i) {
     uint32_t w = 0;
     for (int c = 0; c < 4; ++c) w |= s.squeeze() << (8 * c);
-    wide[i] = w;
+    s.st[(50 + i) * kSrThreads] = w;
   }
-  const Fe kc = sc_reduce_wide(wide);
+  const Fe kc = sc_reduce_wide(s.st + 50 * kSrThreads, kSrThreads);
 
   Fe sc, A_s, R_s;
 #pragma unroll

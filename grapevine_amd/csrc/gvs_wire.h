@@ -244,13 +244,15 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDecArgs a) {
                       : u <= 4 ? rc_i + 16u * (u - 3u)
                       : u == 5 ? pl_i : pl_i + 16u * u - 88u;
     uint4 v = lds_bytes16(m, at);
-    v = u == 5 ? make_uint4(tlo, thi, v.x, v.y) : v;
+    // mask selects: a `c ? x : y` over uint4 values was compiled to a select
+    // of their addresses, with the values in scratch (64 B per lane)
+    v = sel4(u == 5, make_uint4(tlo, thi, v.x, v.y), v);
     uint4* dst = a.out + (uint64_t)(k0 + i) * kAbiU4;
-    dst[lane] = ok_i ? v : z;
-    if (lane == 0) dst[64] = ok_i ? make_uint4(rt_i, 0, 0, 0) : z;
+    dst[lane] = sel4(ok_i, v, z);
+    if (lane == 0) dst[64] = sel4(ok_i, make_uint4(rt_i, 0, 0, 0), z);
     if (a.sigs && lane < 4) {
       const uint4 sg = lds_bytes16(m, sg_i + 16u * lane);
-      a.sigs[(uint64_t)(k0 + i) * 4u + lane] = ok_i ? sg : z;
+      a.sigs[(uint64_t)(k0 + i) * 4u + lane] = sel4(ok_i, sg, z);
     }
   }
   if (a.status && mine) a.status[k] = st;

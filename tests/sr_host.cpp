@@ -45,7 +45,7 @@ void sr_host_reduce_wide(const uint8_t* in, uint8_t* out) {
     w[i] = 0;
     for (int c = 0; c < 4; ++c) w[i] |= (uint32_t)in[4 * i + c] << (8 * c);
   }
-  fe_to(sc_reduce_wide(w), out);
+  fe_to(sc_reduce_wide(w, 1), out);
 }
 
 // a*b and a^2 mod p, canonical

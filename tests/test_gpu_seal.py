@@ -53,7 +53,7 @@ STAGED = dict(n_msgs=65536, rpp=256)  # the staged pass, 8 waves
 
 
 @pytest.mark.parametrize("n_msgs,rpp,waves", [(4096, 0, 8), (4096, 512, 4), (65536, 256, 8), (65536, 512, 4),
-                                              (65536, 1024, 12), (65536, 1024, 16), (65536, 1024, 0)])
+                                              (65536, 1024, 12), (65536, 1024, 0)])
 def test_auth_mode_parity_stream(n_msgs, rpp, waves):
     store, model = make_pair(n_msgs=n_msgs, rpp=rpp)
     store.set_option("sealed_pass_waves", waves)

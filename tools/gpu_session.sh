@@ -54,6 +54,21 @@ case "$2" in
       GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
         python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
     done ;;
+  sealrw)  # the sealed tests, the sealed A/B (SEALAB), then the routed and wire counter shapes
+    step seal_tests 600 $PT $SEALT && \
+    for v in ${SEALAB:-dual:12 nodual:12 m2a1:12}; do
+      lib=${v%%:*}; nw=${v##*:}
+      GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step bench_auth_${lib}_nw$nw 300 \
+        python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 --sealed-waves $nw
+    done && \
+    step obl_rw 900 $PT tests/test_oblivious.py -k "routed or wire"
+    cp gpurun_out/oblivious_*_routed.txt gpurun_out/oblivious_*_wire.txt "$O/" 2>/dev/null ;;
+  fixcheck)  # the GPU suite (no counters/timing), routed counters, routed and store timing, the bench line
+    tests && \
+    step obl_routed 600 $PT tests/test_oblivious.py -k "routed" && \
+    step timing_rs 600 $PT tests/test_timing.py -k "routed or (independent_of_mix and not sealed)" && \
+    step bench 400 python3 bench.py --no-cpu
+    cp gpurun_out/timing_c3_*.txt gpurun_out/oblivious_*_routed.txt "$O/" 2>/dev/null ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
