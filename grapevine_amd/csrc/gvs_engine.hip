@@ -861,8 +861,6 @@ static MArgs margs2(const gvs_handle* h, const Engine& e) {
   a.stamp = e.stamp_run;
   a.cm = e.cm;
   a.sink_mul = scatter_mul((uint64_t)e.Q * e.cm);
-  a.snap_mul = scatter_mul(e.B);
-  a.snap_n = e.B;
   return a;
 }
 
@@ -942,8 +940,6 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     a.mpos = e.mpos;
     a.ops = e.ops;
     a.msnapp = e.msnapp;
-    a.snap_mul = scatter_mul(e.B);
-    a.snap_n = e.B;
     a.mpid = e.mpid;
     a.m1out = e.m1out;
     a.N = e.N;

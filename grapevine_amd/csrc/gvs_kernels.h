@@ -494,17 +494,7 @@ struct MArgs {
   uint4* mdry;         // Q x 8 KiB: each workgroup's dry-run lines (gvs_mtx.h: one 1 KiB per use)
   uint32_t stamp, cm;
   uint32_t sink_mul;   // MSNAP sink line of global slot x: x * sink_mul mod Q*cm (a permutation)
-  uint32_t snap_mul, snap_n;  // MSNAPP line of head position p: p * snap_mul mod snap_n (snap_line)
 };
-
-// The MSNAPP line of sorted position p: a permutation of the B lines (snap_mul
-// prime to B, B * snap_mul < 2^32).  In position order, a partition's group
-// snapshots fell on neighbouring lines while its unused slots' sink lines are
-// scattered (sink_mul), and the two kinds of write ran at different speeds:
-// k_m1x 11 us faster under batches without mailbox groups at the routed
-// shape's partition sizes (profiles/r05l_timing_c3_routed.txt).  Both are
-// scattered the same way now.
-__device__ inline uint32_t snap_line(uint32_t p, uint32_t mul, uint32_t n) { return (p * mul) % n; }
 
 // ---------------------------------------------------------- allocation
 
@@ -569,6 +559,7 @@ __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
 __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   __shared__ uint32_t s_off[2][1024];
   __shared__ uint32_t s_win[kWinRing];
+  __shared__ uint32_t s_stage[kWinGroup][1024];
   const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
   // block offsets (nblk <= 1024)
@@ -602,16 +593,31 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
       f[u] = c0 + u < a.nblk ? a.pflag[i] : 0u;
       slot[u] = c0 + u < a.nblk ? a.pslot[i] : 0u;
     }
+    // each block's 1024 entries staged in LDS in window order (its pops,
+    // then the rest) and written by consecutive threads: written straight
+    // from the lanes, a wave's stores formed one run or two by the data, and
+    // batches with pops ran 2-4 us slower (profiles/r05n_timing_c3_store.txt;
+    // the free ring's other writer, k_post_ring, rule 13)
 #pragma unroll
     for (uint32_t u = 0; u < kWinGroup; ++u) {
-      const uint32_t c = c0 + u, i = c * 1024 + tid;
+      const uint32_t c = c0 + u;
       if (c < a.nblk) {
         const bool pop = f[u] & 1u;
-        const uint32_t P = (c ? s_off[0][c - 1] : 0u) + ((f[u] >> 2) & 1023u);
-        const uint32_t pos = pop ? P : pops + (i - P);
-        a.ring[ring_at(tbase, pos, rs)] = pop ? slot[u] : kNone;
+        const uint32_t pp = (f[u] >> 2) & 1023u, P0 = c ? s_off[0][c - 1] : 0u, tp = s_off[0][c] - P0;
+        s_stage[u][pop ? pp : tp + (tid - pp)] = pop ? slot[u] : kNone;
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t c = c0 + u;
+      if (c < a.nblk) {
+        const uint32_t P0 = c ? s_off[0][c - 1] : 0u, tp = s_off[0][c] - P0;
+        const uint32_t pos = tid < tp ? P0 + tid : pops + (c * 1024 - P0) + (tid - tp);
+        a.ring[ring_at(tbase, pos, rs)] = s_stage[u][tid];
+      }
+    }
+    __syncthreads();  // the stage is refilled by the next group
   }
   __threadfence_block();
   __syncthreads();

@@ -234,33 +234,15 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   ma_prepass<false>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
   __syncthreads();
   // admission (grapevine.proto:74), as k_m1x
-  for (uint32_t k = tid; k < a.cm; k += 256) {
-    const GroupM& G = g[k];
-    atomicAdd(&s_empt, (k < ng && G.slot >= 0 && G.len == min(G.n_del, G.len)) ? 1u : 0u);
-  }
+  count_empty(g, ng, a.cm, &s_empt);
   __syncthreads();
-  const uint32_t freeq = (a.Sr - s_occ) + s_empt;
-  for (uint32_t k = tid; k < a.cm; k += 256) {
-    GroupM& G = g[k];
-    const bool real = k < ng;
-    const uint32_t len1 = (real && G.slot >= 0) ? G.len - min(G.n_del, G.len) : 0u;
-    const bool exists1 = len1 > 0;
-    const bool isnew = real && !exists1 && G.n_create > 0;
-    uint32_t rank = 0;
-    for (uint32_t k2 = 0; k2 < a.cm; ++k2) {
-      const GroupM& H = g[k2];
-      const uint32_t hl = (k2 < ng && H.slot >= 0) ? H.len - min(H.n_del, H.len) : 0u;
-      rank += (k2 < ng && hl == 0 && H.n_create > 0 && H.fcs < G.fcs) ? 1u : 0u;
-    }
-    G.fl = len1;
-    G.flags = (exists1 ? 1u : 0u) | ((isnew && rank < freeq) ? 2u : 0u);
-  }
+  admit_groups(g, ng, a.cm, (a.Sr - s_occ) + s_empt);
   __syncthreads();
   uint4* dry = a.mdry + (uint64_t)q * kMDryU4;
   if (tid < kRowWaves) s_tw[tid] = 0;
   __syncthreads();
   for (uint32_t j = tid; j < a.Sr; j += 256) atomicAdd(&s_tw[(j / kMA) % kRowWaves], s_sg[j] >= 0 ? 1u : 0u);
-  for (uint32_t k = tid; k < a.cm; k += 256) s_tf[k] = (k < ng && g[k].slot >= 0) ? 0 : 1;
+  for (uint32_t k = tid; k < a.cm; k += 256) s_tf[k] = ((k < ng) & ((int32_t)group_fields(g[k]).slot >= 0)) ? 0 : 1;
   __syncthreads();
   block_flag_scan(s_tf, a.cm, s_tp, s_w);
   for (uint32_t k = tid; k < a.cm; k += 256)
@@ -283,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
                            make_uint4(0, 0, 0, 0));
     cur = sel4(lane == 0, hdr, sel4(lane == 1 || slot_it, make_uint4(0, 0, 0, 0), cur));
     const uint32_t sl = (uint32_t)(((uint64_t)(q * a.cm + (uint32_t)k) * a.sink_mul) % ((uint64_t)a.Q * a.cm));
-    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)snap_line(G.head, a.snap_mul, a.snap_n) * 64 : a.msnap + (uint64_t)sl * 64;
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : a.msnap + (uint64_t)sl * 64;
     st_drop(dst, lane, cur);
   };
   uint32_t ci = 0;
@@ -354,13 +336,14 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   for (uint32_t k = tid; k < a.cm; k += 256) {
     GroupM& G = g[k];
     const bool real = k < ng;
-    const uint32_t len = (real && G.slot >= 0) ? G.len : 0u;
+    const GroupFields f = group_fields(G);
+    const uint32_t len = selu32(real & ((int32_t)f.slot >= 0), f.len, 0u);
     const uint32_t dp = min(G.n_del, len);
     const uint64_t lenmask = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
     const uint64_t mask = (((uint64_t)G.mhi << 32) | G.mlo) & lenmask & ~((1ull << dp) - 1ull);
     const uint32_t nk = len - dp - (uint32_t)__popcll(mask);
-    G.fl = real ? nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk) : 0u;
-    s_gflag[k] = (real && G.slot < 0 && G.fl > 0) ? 1 : 0;
+    G.fl = selu32(real, nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk), 0u);
+    s_gflag[k] = (real & ((int32_t)f.slot < 0) & (G.fl > 0)) ? 1 : 0;
     s_ld[k] = 0;
   }
   __syncthreads();

@@ -147,6 +147,52 @@ struct GroupM {  // 64 B
   uint32_t pad;
 };
 
+// A group slot's fields, read whatever the batch holds: a short-circuit
+// `k < ng && G.slot >= 0 && ...` compiled to branches that skipped the reads
+// of unused slots, so the admission ranks (cm x cm reads) ran 10 us faster
+// under batches without mailbox groups at the routed shape's cm
+// (profiles/r05l-r05p_timing_c3_routed.txt, k_m1x)
+struct GroupFields {
+  uint32_t slot, len, n_del, n_create, fcs;
+};
+__device__ inline GroupFields group_fields(const GroupM& G) {
+  GroupFields f{(uint32_t)G.slot, G.len, G.n_del, G.n_create, G.fcs};
+  asm volatile("" : "+v"(f.slot), "+v"(f.len), "+v"(f.n_del), "+v"(f.n_create), "+v"(f.fcs));
+  return f;
+}
+// the group's length after its pops (0: no row, or not a group of this batch)
+__device__ inline uint32_t len_after_pops(const GroupFields& f, bool real) {
+  return selu32(real & ((int32_t)f.slot >= 0), f.len - min(f.n_del, f.len), 0u);
+}
+// admission (grapevine.proto:74): rows that empty after the pops are free
+// again (s_empt), new recipients are admitted by the seq of their first create
+__device__ inline void count_empty(const GroupM* g, uint32_t ng, uint32_t cm, uint32_t* s_empt) {
+  for (uint32_t k = threadIdx.x; k < cm; k += 256) {
+    const GroupFields f = group_fields(g[k]);
+    const bool real = k < ng;
+    atomicAdd(s_empt, (real & ((int32_t)f.slot >= 0) & (f.len == min(f.n_del, f.len))) ? 1u : 0u);
+  }
+}
+__device__ inline void admit_groups(GroupM* g, uint32_t ng, uint32_t cm, uint32_t freeq) {
+  for (uint32_t k = threadIdx.x; k < cm; k += 256) {
+    GroupM& G = g[k];
+    const GroupFields f = group_fields(G);
+    const bool real = k < ng;
+    const uint32_t len1 = len_after_pops(f, real);
+    const bool exists1 = len1 > 0;
+    const bool isnew = real & !exists1 & (f.n_create > 0);
+    uint32_t rank = 0;
+    for (uint32_t k2 = 0; k2 < cm; ++k2) {  // every slot, every field: fixed work
+      const GroupFields h = group_fields(g[k2]);
+      const bool r2 = k2 < ng;
+      const uint32_t hl = len_after_pops(h, r2);
+      rank += (r2 & (hl == 0) & (h.n_create > 0) & (h.fcs < f.fcs)) ? 1u : 0u;
+    }
+    G.fl = len1;
+    G.flags = (exists1 ? 1u : 0u) | ((isnew & (rank < freeq)) ? 2u : 0u);
+  }
+}
+
 // group of (hi, glo) among g[0, ng) (sorted), or -1: a fixed-step search
 // (g holds cm + 1 entries: the slots and the sink g[cm])
 __device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, uint64_t hi, uint64_t glo) {
@@ -155,11 +201,15 @@ __device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, ui
   for (uint32_t step = kGroupMax; step > 0; step >>= 1) {
     const uint32_t c = pos + step;
     const GroupM& G = g[min(c - 1, cm)];
-    const bool less = G.hi < hi || (G.hi == hi && G.glo < glo);
-    pos = (c <= ng && less) ? c : pos;
+    uint64_t ghi = G.hi, gglo = G.glo;  // both read at every step (no short-circuit branch)
+    asm volatile("" : "+v"(ghi), "+v"(gglo));
+    const bool less = (ghi < hi) | ((ghi == hi) & (gglo < glo));
+    pos = ((c <= ng) & less) ? c : pos;
   }
   const GroupM& G = g[min(pos, cm)];
-  return (pos < ng && G.hi == hi && G.glo == glo) ? (int)pos : -1;
+  uint64_t ghi = G.hi, gglo = G.glo;
+  asm volatile("" : "+v"(ghi), "+v"(gglo));
+  return ((pos < ng) & (ghi == hi) & (gglo == glo)) ? (int)pos : -1;
 }
 
 // occupied rows of the partition -> groups, every side entry read; s_keep
@@ -289,29 +339,9 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   __syncthreads();
   side_prepass_m(a, q, g, ng, s_sg, s_occb, &s_occ);
   __syncthreads();
-  // admission (grapevine.proto:74): rows that empty after the pops are free
-  // again; new recipients are admitted by the seq of their first create
-  for (uint32_t k = tid; k < a.cm; k += 256) {
-    const GroupM& G = g[k];
-    atomicAdd(&s_empt, (k < ng && G.slot >= 0 && G.len == min(G.n_del, G.len)) ? 1u : 0u);
-  }
+  count_empty(g, ng, a.cm, &s_empt);
   __syncthreads();
-  const uint32_t freeq = (a.Sr - s_occ) + s_empt;
-  for (uint32_t k = tid; k < a.cm; k += 256) {
-    GroupM& G = g[k];
-    const bool real = k < ng;
-    const uint32_t len1 = (real && G.slot >= 0) ? G.len - min(G.n_del, G.len) : 0u;
-    const bool exists1 = len1 > 0;
-    const bool isnew = real && !exists1 && G.n_create > 0;
-    uint32_t rank = 0;
-    for (uint32_t k2 = 0; k2 < a.cm; ++k2) {  // every slot: fixed work
-      const GroupM& H = g[k2];
-      const uint32_t hl = (k2 < ng && H.slot >= 0) ? H.len - min(H.n_del, H.len) : 0u;
-      rank += (k2 < ng && hl == 0 && H.n_create > 0 && H.fcs < G.fcs) ? 1u : 0u;
-    }
-    G.fl = len1;
-    G.flags = (exists1 ? 1u : 0u) | ((isnew && rank < freeq) ? 2u : 0u);
-  }
+  admit_groups(g, ng, a.cm, (a.Sr - s_occ) + s_empt);
   __syncthreads();
   // group snapshots go to MSNAPP at the head's sorted position, so that every
   // op of k_m1r_c reads line p (an address stream that does not depend on the
@@ -322,7 +352,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
   if (tid < kRowWaves) s_tw[tid] = 0;
   __syncthreads();
   for (uint32_t j = tid; j < a.Sr; j += 256) atomicAdd(&s_tw[(j / kMU) % kRowWaves], s_sg[j] >= 0 ? 1u : 0u);
-  for (uint32_t k = tid; k < a.cm; k += 256) s_tf[k] = (k < ng && g[k].slot >= 0) ? 0 : 1;
+  for (uint32_t k = tid; k < a.cm; k += 256) s_tf[k] = ((k < ng) & ((int32_t)group_fields(g[k]).slot >= 0)) ? 0 : 1;
   __syncthreads();
   block_flag_scan(s_tf, a.cm, s_tp, s_w);
   for (uint32_t k = tid; k < a.cm; k += 256)
@@ -351,7 +381,7 @@ __global__ __launch_bounds__(256) void k_m1x(MArgs a) {
     // lines over MSNAPP: the partition's 1-KiB sink lines written in a row
     // made a batch without groups 7-9 us faster (DRAM page locality)
     const uint32_t sl = ((q * a.cm + (uint32_t)k) * a.sink_mul) % (a.Q * a.cm);
-    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)snap_line(G.head, a.snap_mul, a.snap_n) * 64 : a.msnap + (uint64_t)sl * 64;
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? a.msnapp + (uint64_t)G.head * 64 : a.msnap + (uint64_t)sl * 64;
     st_drop(dst, lane, cur);
   };
   uint32_t ci = 0;  // the wave's chunk index
@@ -393,8 +423,7 @@ struct M1rArgs {
   GVS_VSCAN_FIELDS
   const uint4* mpos;
   const OpState* ops;
-  const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions (snap_line)
-  uint32_t snap_mul, snap_n;
+  const uint4* msnapp;  // B x 1 KiB: group snapshots at their heads' positions
   const uint4* mpid;    // B x 16 B: each position's message id (k_gtx)
   M1Out* m1out;
   uint64_t N;
@@ -428,7 +457,7 @@ struct M1rOp {
   // every op reads its own position's line (heads find their group's
   // snapshot there; the others' lines are read and ignored)
   __device__ static const uint4* src_of(const Args& a, uint32_t p, uint4) {
-    return a.msnapp + (uint64_t)snap_line(p, a.snap_mul, a.snap_n) * 64;
+    return a.msnapp + (uint64_t)p * 64;
   }
   // k_vscan_a: every op's line is read, the defining op's kept
   __device__ static uint4 elem_value(const Args& a, uint32_t p, const uint4*) {
@@ -731,13 +760,14 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   for (uint32_t k = tid; k < a.cm; k += 256) {
     GroupM& G = g[k];
     const bool real = k < ng;
-    const uint32_t len = (real && G.slot >= 0) ? G.len : 0u;
+    const GroupFields f = group_fields(G);
+    const uint32_t len = selu32(real & ((int32_t)f.slot >= 0), f.len, 0u);
     const uint32_t dp = min(G.n_del, len);
     const uint64_t lenmask = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
     const uint64_t mask = (((uint64_t)G.mhi << 32) | G.mlo) & lenmask & ~((1ull << dp) - 1ull);
     const uint32_t nk = len - dp - (uint32_t)__popcll(mask);
-    G.fl = real ? nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk) : 0u;
-    s_gflag[k] = (real && G.slot < 0 && G.fl > 0) ? 1 : 0;
+    G.fl = selu32(real, nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk), 0u);
+    s_gflag[k] = (real & ((int32_t)f.slot < 0) & (G.fl > 0)) ? 1 : 0;
     s_ld[k] = 0;
   }
   __syncthreads();

@@ -18,17 +18,18 @@
 //   * sealed rows are stored in the tile layout (gvs_seal_dev.h tile_unit):
 //     a coalesced load leaves each lane one whole 128-B leaf, so the leaf
 //     hashes read registers and the per-wave stage is gone;
-//   * the AES table keeps 32 replicas (conflict-free for ds_read_b32,
-//     gvs_seal_dev.h), and the other half of its 64-KiB window (256 holes of
-//     128 B) stages 32 slot lines;
+//   * the AES tables keep 32 replicas each (conflict-free for ds_read_b32,
+//     gvs_seal_dev.h): T0 and T1 fill the 64-KiB window (GVS_SP_DUAL, one
+//     rotation per column instead of three: 5.4 % faster, r05m); with T0
+//     alone the window's other half (256 holes of 128 B) stages 32 slot lines;
 //   * kSpBufs 1-KiB staging buffers hold the previous batch's final states
 //     (buffer k = previous slot k, read before the stream, all c of them) and
 //     this batch's snapshots (buffer kSpBufs - 1 - k = slot k, written after
 //     the stream, all c of them).  The two batches' used slots of a partition
 //     share the buffers: k_sjoint fails a batch (GVS_ERR_BATCH_OVERFLOW)
 //     before anything changes when they would overlap, i.e. when the
-//     partition's distinct rows over the two batches exceed kSpBufs (96 at
-//     C3/C5 against a mean of 32: beyond 11 standard deviations);
+//     partition's distinct rows over the two batches exceed kSpBufs (86 at
+//     C3/C5 against a mean of 32: beyond 9 standard deviations);
 //   * in the stream every chunk of 8 rows does the same LDS work: each row
 //     reads a final state (its own buffer or a dry one) and writes a
 //     snapshot (its own buffer or the dry one), selected per lane.

@@ -69,6 +69,17 @@ case "$2" in
     step timing_rs 600 $PT tests/test_timing.py -k "routed or (independent_of_mix and not sealed)" && \
     step bench 400 python3 bench.py --no-cpu
     cp gpurun_out/timing_c3_*.txt gpurun_out/oblivious_*_routed.txt "$O/" 2>/dev/null ;;
+  timeab)  # routed and store timing for the in-tree build and each ab/ library in TIMEAB
+    step timing_rs_base 600 $PT tests/test_timing.py -k "routed or (independent_of_mix and not sealed)"
+    for f in gpurun_out/timing_c3_*.txt; do cp "$f" "$O/base_$(basename $f)"; done
+    for lib in ${TIMEAB:-even}; do
+      GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step timing_rs_$lib 600 $PT tests/test_timing.py -k "routed or (independent_of_mix and not sealed)"
+      for f in gpurun_out/timing_c3_*.txt; do cp "$f" "$O/${lib}_$(basename $f)"; done
+    done ;;
+  admit)  # the GPU suite (no counters/timing), then every timing shape
+    tests && \
+    step timing_all 900 $PT tests/test_timing.py
+    cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
