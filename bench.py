@@ -56,6 +56,8 @@ def parse():
                    help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12),
                    help="--auth: waves per workgroup of the sealed message pass (0: the store's choice)")
+    p.add_argument("--mailbox-slots", type=int, default=256,
+                   help="mailbox rows per partition (gvs_config.mailbox_partition_slots; R = N/16 either way)")
     p.add_argument("--expiry", type=int, default=0,
                    help="expiry sweep: X deletes per batch (DESIGN.md §9); each batch then carries "
                         "batch - X requests and every prefilled message is past the cutoff")
@@ -488,12 +490,12 @@ def main():
     if world > 1 or a.routed:
         # one shard per rank; the store's own RCCL communicator carries the data path
         cfg = abi.make_config(N, max_batch=B, device=local, shard_count=world, shard_index=rank,
-                              auth_storage=a.auth)
+                              auth_storage=a.auth, mailbox_partition_slots=a.mailbox_slots)
         cid = gdist.broadcast_bytes(ri, comm_unique_id() if rank == 0 else None, device=dev)
         store = ObliviousStore(cfg, comm_id=cid)
     else:
         cfg = abi.make_config(N, max_batch=B, device=local, auth_storage=a.auth,
-                              expiry_per_batch=a.expiry)
+                              expiry_per_batch=a.expiry, mailbox_partition_slots=a.mailbox_slots)
         store = ObliviousStore(cfg)
     shard_batch = store.stats()["shard_batch"]
     # what the data path spans, from the store's own RCCL communicator
@@ -724,6 +726,7 @@ def main():
                        + f"2^{a.log2n} message capacity per GPU, {B}-request batches",
                        "msg_capacity": N, "batch": B,
                        "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,
+                       "mailbox_partition_slots": cfg.mailbox_partition_slots,
                        "parallelism": f"shards{world}",
                        "route_capacity": store.stats()["route_capacity"],
                        "shard_batch": shard_batch, "auth_storage": bool(a.auth),

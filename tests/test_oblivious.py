@@ -33,7 +33,9 @@ TLB invalidation nothing in the process causes"): every kernel of one batch
 then reads ~140 uncached lines per GiB more.  Each --pmc pass also records
 TCC_UC_REQ_sum per dispatch; a process's one batch whose kernels made more
 than UC_WALK uncached requests is left out of both checks (exclusions()); the
-report lists every batch's count and every exclusion."""
+report lists every batch's count and every exclusion.  A process that
+re-walked in every measured batch is measured again in a fresh process
+(rewalk_processes())."""
 import csv
 import ctypes
 import glob
@@ -207,6 +209,28 @@ def split_batches(vals):
 
 
 _CACHE = {}
+_RERUNS = []
+
+
+def walk_levels(per):
+    """{mix: median uncached L2 requests over the process's measured batches}."""
+    return {mix: statistics.median(sum(x[4] for x in b) for b in bs[-N_MEAS:]) for mix, bs in per.items()}
+
+
+def rewalk_processes(per):
+    """Processes whose every measured batch re-walked page tables: a measured-
+    batch median of uncached L2 requests above 3x the median over all the
+    shape's processes (and above UC_WALK).  Seen in one process at a time, a
+    different mix in different runs (r05i: expiry x_all; r05r: plain deletes
+    and expiry x_few, 300-430 uncached requests in every measured batch against
+    20-100, their prefill batches like every other process's), with +0.3-1 KiB
+    in a few small kernels.  Such a process is measured once more in a fresh
+    process; the same rule for every mix, main and main#2 included, and every
+    re-run is printed in the report.  A byte count that follows the mix
+    follows it into the fresh process too."""
+    lv = walk_levels(per)
+    med = statistics.median(lv.values())
+    return [m for m, v in lv.items() if v > max(UC_WALK, 3.0 * med)]
 
 
 def measure(shape, counter, tmp_root):
@@ -221,6 +245,16 @@ def measure(shape, counter, tmp_root):
             m = mix.split("#")[0]
             d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}")
             res[mix] = split_batches(rocprof(counter, m, d, shape))
+        # a process that re-walked the page tables in every measured batch is
+        # measured again in a fresh process, once (rewalk_processes())
+        for mix in rewalk_processes(res):
+            m = mix.split("#")[0]
+            d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}_again")
+            levels = walk_levels(res)
+            res[mix] = split_batches(rocprof(counter, m, d, shape))
+            _RERUNS.append(f"{shape}/{counter}/{mix}: measured-batch walk level {levels[mix]:.0f} against a "
+                           f"median of {statistics.median(levels.values()):.0f}; again: "
+                           f"{walk_levels(res)[mix]:.0f}")
         _CACHE[key] = res
     return _CACHE[key]
 
@@ -309,6 +343,8 @@ def report(shape, counter, lines, bad):
         f.write("\n".join(lines) + "\n")
         f.write(f"violations: {bad}\n")
         f.write("probe starts: " + "; ".join(x for x in _VRAM["log"] if x.startswith(f"{shape}/")) + "\n")
+        f.write("re-run processes (page-table re-walks in every measured batch): "
+                + "; ".join(x for x in _RERUNS if x.startswith(f"{shape}/{counter}/")) + "\n")
 
 
 @pytest.mark.parametrize("shape", sorted(SHAPES))

@@ -80,6 +80,10 @@ case "$2" in
     tests && \
     step timing_all 900 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
+  mbox)  # the plain bench line at several mailbox partition sizes
+    for sr in ${MBOX:-256 512 1024}; do
+      step bench_mbox$sr 300 python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --mailbox-slots $sr
+    done ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
