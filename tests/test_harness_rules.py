@@ -34,5 +34,5 @@ def test_whole_process_rewalk_is_measured_again():
            "hot_next": quiet, "main#2": quiet}
     assert ob.rewalk_processes(per) == ["deletes"]
     # within 3x of the shape's median: no re-run
-    per["deletes"] = _proc(_pre([80, 90, 70, 85, 75, 60]))
+    per["deletes"] = _proc(_pre([50, 55, 60, 45, 70, 55]))
     assert ob.rewalk_processes(per) == []
