@@ -141,6 +141,10 @@ case "$2" in
       python3 -c "import json; d=json.load(open('$O/scale_prediction.json')); json.dump(d, open('profiles/scale_prediction.json','w'), indent=1)"
     rm -rf "$O/pmc_valu"
     step bench_auth 600 python3 bench.py --auth --no-cpu --steps 5
-    step bench_expiry 300 python3 bench.py --expiry 1024 --no-cpu ;;
+    step bench_expiry 300 python3 bench.py --expiry 1024 --no-cpu
+    step kstats_auth 400 rocprofv3 --kernel-trace --stats -d "$O/ka" -o run --output-format csv -- \
+      python3 bench.py --auth --no-cpu --host-steps 0 --wire-steps 0 --steps 5 --warmup 2
+    find "$O/ka" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_auth.csv" \;
+    rm -rf "$O/ka" ;;
 esac
 echo ALL_DONE
