@@ -105,6 +105,10 @@ case "$2" in
     rm -rf "$O/ka" ;;
   authsq) step auth_sq 900 bash tools/gpu_auth_sq.sh "$1/sq" ;;
   driver) step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread ;;
+  final)  # the driver's round-end command, then smoke()
+    step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread
+    cp gpurun_out/oblivious_*.txt gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
+    step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   tests) tests ;;
   timing) timing ;;
   bench) bench ;;
