@@ -251,7 +251,8 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   const uint32_t nfree = s_tp[a.cm];
   uint32_t d0, dn;
   slot_share(s_tw, a.cm, wave, &d0, &dn);
-  const uint32_t nch = a.Sr > wave * kMA ? (a.Sr - wave * kMA + kRowWaves * kMA - 1) / (kRowWaves * kMA) : 0u;
+  const uint32_t nch = __builtin_amdgcn_readfirstlane(
+      a.Sr > wave * kMA ? (a.Sr - wave * kMA + kRowWaves * kMA - 1) / (kRowWaves * kMA) : 0u);
   // one iteration: a touched row's snapshot or a slot without a row (k_m1x)
   auto step = [&](const uint4 (&v)[kMA], uint32_t bit, uint32_t j0, uint32_t di) {
     const bool slot_it = bit == 0u;
@@ -385,7 +386,8 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   const uint32_t nfree = s_gpfx[a.cm];
   uint32_t d0, dn;
   slot_share(s_tw, a.cm, wave, &d0, &dn);
-  const uint32_t nch = a.Sr > wave * kMA ? (a.Sr - wave * kMA + kRowWaves * kMA - 1) / (kRowWaves * kMA) : 0u;
+  const uint32_t nch = __builtin_amdgcn_readfirstlane(
+      a.Sr > wave * kMA ? (a.Sr - wave * kMA + kRowWaves * kMA - 1) / (kRowWaves * kMA) : 0u);
   const uint4* res = a.m2tx + (uint64_t)q * a.cm * kVLineU4;
   const uint4* dry = a.mdry + (uint64_t)q * kMDryU4 + 256;
   // the wave's compaction stage (m2_row): its row buffer's slots in the holes
@@ -421,7 +423,11 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   for (uint32_t j0 = wave * kMA; j0 < a.Sr; j0 += kRowWaves * kMA, ++ci) {
     uint4 v[kMA];
     const uint64_t t = ((uint64_t)q * a.Sr + j0) / kMA;
-    const uint32_t u = lane >> 2;
+    // the per-lane row recomputed per chunk: hoisted, its 64-bit base stayed
+    // live across the loop and was spilled to scratch (k_m2a, 24 B per lane)
+    uint32_t ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t u = ln >> 2;
     const uint64_t row = (uint64_t)q * a.Sr + j0 + u;
     // four jobs, one copy of each crypto step: 0 verify, 1 decrypt and the
     // mailbox steps, 2 re-encrypt, 3 the new leaf sums and the stores.  The

@@ -7,8 +7,9 @@ timing.  Round 5 found `k_route_gather` with a 160-B/lane array in scratch (a
 `c ? x : y` over uint4 values compiled to a select of their addresses): 10 MB
 of FETCH_SIZE per launch and +-25 KiB of noise that failed the routed counter
 test (profiles/r05l_oblivious_FETCH_SIZE_routed.txt, r05m after the fix).
-Every kernel is now checked for scratch; the two that keep some are listed
-with their bound and the reason.
+Every kernel is now checked for scratch; the one that keeps some is listed
+with its bound and the reason (k_m2a's 24-B register spills are gone: its
+per-lane row is recomputed per chunk).
 """
 import os
 import re
@@ -26,10 +27,6 @@ ALLOWED = {
     # out-of-line curve functions take field elements by reference; its
     # counters are exact in every run (profiles/r05m_oblivious_*_wire.txt)
     "k_sr_verify": (80, "reference arguments of out-of-line curve functions"),
-    # 5 spilled registers at two workgroups per CU; sized for one workgroup
-    # (GVS_M2A_WGS=1) it has none but takes 4.36 ms instead of 2.95
-    # (profiles/r05m_sealed_ab.txt)
-    "k_m2a": (24, "register spills at two workgroups per CU"),
 }
 
 

@@ -84,6 +84,11 @@ case "$2" in
     for sr in ${MBOX:-256 512 1024}; do
       step bench_mbox$sr 300 python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --mailbox-slots $sr
     done ;;
+  sealchk)  # the sealed tests, the sealed counter shapes, the sealed bench line
+    step seal_tests 600 $PT $SEALT && \
+    step oblivious_auth 900 $PT tests/test_oblivious.py -k "auth" && \
+    step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0
+    cp gpurun_out/oblivious_*_auth.txt "$O/" 2>/dev/null ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
