@@ -224,10 +224,12 @@ def rewalk_processes(per):
     different mix in different runs (r05i: expiry x_all; r05r: plain deletes
     and expiry x_few, 300-430 uncached requests in every measured batch against
     20-100, their prefill batches like every other process's), with +0.3-1 KiB
-    in a few small kernels.  Such a process is measured once more in a fresh
-    process; the same rule for every mix, main and main#2 included, and every
-    re-run is printed in the report.  A byte count that follows the mix
-    follows it into the fresh process too."""
+    in a few small kernels.  Such a process is measured again in a fresh
+    process, at most twice (the state can outlive one process: r05v, the
+    sealed shape's deletes, 318 then 162 against a median of 14, quiet in the
+    r05i, r05r and r05u runs); the same rule for every mix, main and main#2
+    included, and every re-run is printed in the report.  A byte count that
+    follows the mix follows it into the fresh processes too."""
     lv = walk_levels(per)
     med = statistics.median(lv.values())
     return [m for m, v in lv.items() if v > max(UC_WALK, 3.0 * med)]
@@ -246,15 +248,16 @@ def measure(shape, counter, tmp_root):
             d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}")
             res[mix] = split_batches(rocprof(counter, m, d, shape))
         # a process that re-walked the page tables in every measured batch is
-        # measured again in a fresh process, once (rewalk_processes())
-        for mix in rewalk_processes(res):
-            m = mix.split("#")[0]
-            d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}_again")
-            levels = walk_levels(res)
-            res[mix] = split_batches(rocprof(counter, m, d, shape))
-            _RERUNS.append(f"{shape}/{counter}/{mix}: measured-batch walk level {levels[mix]:.0f} against a "
-                           f"median of {statistics.median(levels.values()):.0f}; again: "
-                           f"{walk_levels(res)[mix]:.0f}")
+        # measured again in a fresh process, at most twice (rewalk_processes())
+        for attempt in range(2):
+            for mix in rewalk_processes(res):
+                m = mix.split("#")[0]
+                d = os.path.join(tmp_root, f"{shape}_{counter}_{mix.replace('#', '_')}_again{attempt}")
+                levels = walk_levels(res)
+                res[mix] = split_batches(rocprof(counter, m, d, shape))
+                _RERUNS.append(f"{shape}/{counter}/{mix}: measured-batch walk level {levels[mix]:.0f} against a "
+                               f"median of {statistics.median(levels.values()):.0f}; again: "
+                               f"{walk_levels(res)[mix]:.0f}")
         _CACHE[key] = res
     return _CACHE[key]
 
