@@ -32,7 +32,11 @@ namespace gvs {
 namespace sr {
 
 #define GVS_SR_FN __host__ __device__ __forceinline__
-#define GVS_SR_FN_NI __host__ __device__
+// the larger steps (each called once per signature): inlined too.  Out of
+// line, their reference arguments, out-parameters and point returns lived in
+// scratch (80 B per lane, tests/test_code_object.py); inlined, the kernel has
+// none, at the same registers and occupancy
+#define GVS_SR_FN_NI __host__ __device__ __forceinline__
 
 struct Fe {
   uint32_t v[8];

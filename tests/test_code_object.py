@@ -7,9 +7,10 @@ timing.  Round 5 found `k_route_gather` with a 160-B/lane array in scratch (a
 `c ? x : y` over uint4 values compiled to a select of their addresses): 10 MB
 of FETCH_SIZE per launch and +-25 KiB of noise that failed the routed counter
 test (profiles/r05l_oblivious_FETCH_SIZE_routed.txt, r05m after the fix).
-Every kernel is now checked for scratch; the one that keeps some is listed
-with its bound and the reason (k_m2a's 24-B register spills are gone: its
-per-lane row is recomputed per chunk).
+Every kernel is now checked for scratch, and none has any (k_m2a's 24-B
+register spills are gone: its per-lane row is recomputed per chunk;
+k_sr_verify's 80 B went with its out-of-line curve functions).  ALLOWED would
+list an exception with its bound and the reason.
 """
 import os
 import re
@@ -23,11 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 # kernel symbol substring -> (max scratch bytes per lane, why)
-ALLOWED = {
-    # out-of-line curve functions take field elements by reference; its
-    # counters are exact in every run (profiles/r05m_oblivious_*_wire.txt)
-    "k_sr_verify": (80, "reference arguments of out-of-line curve functions"),
-}
+ALLOWED = {}
 
 
 def kernel_scratch(lib):

@@ -89,6 +89,11 @@ case "$2" in
     step oblivious_auth 900 $PT tests/test_oblivious.py -k "auth" && \
     step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0
     cp gpurun_out/oblivious_*_auth.txt "$O/" 2>/dev/null ;;
+  srprof)  # the signature and wire tests, the wire counters, then the profiling session
+    step sr_tests 600 $PT tests/test_gpu_sr25519.py tests/test_gpu_wire.py && \
+    step obl_wire 600 $PT tests/test_oblivious.py -k "wire" && \
+    cp gpurun_out/oblivious_*_wire.txt "$O/" && \
+    bash "$0" "$1" prof ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
