@@ -118,7 +118,9 @@ case "$2" in
   final)  # the driver's round-end command, then smoke()
     step driver_x 1100 python3 -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread
     cp gpurun_out/oblivious_*.txt gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
-    step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+    step bench 400 python3 bench.py
+    step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 ;;
   tests) tests ;;
   timing) timing ;;
   bench) bench ;;
