@@ -354,10 +354,10 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
 int gvs_synchronize(gvs_handle *h);
 
 /* Tuning knobs (engine-internal choices that never change results):
- * "sealed_pass_waves" = 8 (default: the authenticated message-table pass runs
- * 8 waves of 8 rows per workgroup, two per SIMD, when a partition's rows are
- * a multiple of 512) or 4 (4 waves of 16 rows, one per SIMD).  Unknown keys
- * or values return GVS_ERR_INVALID_ARG. */
+ * "sealed_pass_waves" = 0 (default: the authenticated message-table pass runs
+ * 12 waves of 8-row chunks per workgroup, three per SIMD, when a partition has
+ * at least 1024 rows, else 8), or 4, 8 or 12 to fix it.  Unknown keys or
+ * values return GVS_ERR_INVALID_ARG. */
 int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 
 /* Read-only engine parameters of shard 0: "txn_slots" (transaction slots per
