@@ -952,7 +952,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     AllocArgs a = aargs(e);
     hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_alloc_b, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_alloc_b, dim3(nblk * 4), dim3(256), 0, s, a);
   }
   mark(h, "alloc");
   if (int r = sort_keys<uint64_t, 1>(h, e.rkeys, B)) return r;

@@ -678,17 +678,18 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
 }
 
 // Per op: statuses, ids, message-pass routing keys, partition histogram.
-__global__ __launch_bounds__(1024) void k_alloc_b(AllocArgs a) {
-  __shared__ uint32_t s_w[16];
+// 256-thread workgroups: in 1024-thread ones the kernel ran on a quarter of
+// the CUs (B / 1024 = 64 workgroups at C3), as k_meta did
+__global__ __launch_bounds__(256) void k_alloc_b(AllocArgs a) {
   const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
-  // S_i: block offset + in-block prefix of mailbox-ok creates
+  // S_i: offset of the op's 1024-op block + its in-block prefix of
+  // mailbox-ok creates (k_alloc_sum, pflag bits 12..21)
+  const uint32_t i = blockIdx.x * 256 + tid, c = i >> 10;
   uint32_t boff = 0;
-  for (uint32_t b = 0; b < blockIdx.x; ++b) boff += a.bsum[2 * b + 1];
-  const uint32_t i = blockIdx.x * 1024 + tid;
+  for (uint32_t b = 0; b < c; ++b) boff += a.bsum[2 * b + 1];
   const uint32_t f = a.pflag[i];
-  uint32_t tot;
-  const uint32_t S_i = boff + block1024_prefix((f & 2u) != 0u, s_w, &tot);
+  const uint32_t S_i = boff + ((f >> 12) & 1023u);
   const uint32_t kind = a.kinds[i];
   const OpState os = a.ops[i];
   const M1Out m1 = a.m1out[i];

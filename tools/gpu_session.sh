@@ -94,6 +94,8 @@ case "$2" in
     step obl_wire 600 $PT tests/test_oblivious.py -k "wire" && \
     cp gpurun_out/oblivious_*_wire.txt "$O/" && \
     bash "$0" "$1" prof ;;
+  tprof)  # the GPU suite without counters/timing, then the profiling session
+    tests && bash "$0" "$1" prof ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
