@@ -96,6 +96,13 @@ case "$2" in
     bash "$0" "$1" prof ;;
   tprof)  # the GPU suite without counters/timing, then the profiling session
     tests && bash "$0" "$1" prof ;;
+  scrubab)  # sealed FETCH_SIZE counters: in-tree build, then each ab/ library in SCRUBAB
+    step fetch_auth_base 600 $PT tests/test_oblivious.py -k "FETCH_SIZE and auth"
+    for f in gpurun_out/oblivious_FETCH_SIZE_*auth.txt; do cp "$f" "$O/base_$(basename $f)"; done
+    for lib in ${SCRUBAB:-scrub}; do
+      GVS_LIB_OVERRIDE=ab/libgvstore_$lib.so step fetch_auth_$lib 600 $PT tests/test_oblivious.py -k "FETCH_SIZE and auth"
+      for f in gpurun_out/oblivious_FETCH_SIZE_*auth.txt; do cp "$f" "$O/${lib}_$(basename $f)"; done
+    done ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
