@@ -951,7 +951,6 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   {
     AllocArgs a = aargs(e);
     hipLaunchKernelGGL(k_alloc_sum, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_alloc_pops, dim3(nblk), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_alloc_ring, dim3(1), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_alloc_b, dim3(nblk * 4), dim3(256), 0, s, a);
   }
@@ -1067,7 +1066,7 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
     PostArgs a{e.kinds, e.rres, e.rop, e.dflag, e.dslot, e.bsum2, e.ring, e.scal, B, nblk,
                e.ring_size};
     hipLaunchKernelGGL(k_post_sum, dim3(nblk), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_post_ring, dim3(nblk), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_post_ring, dim3(1), dim3(1024), 0, s, a);
   }
   mark(h, "post");
   {

@@ -552,40 +552,14 @@ __global__ __launch_bounds__(1024) void k_alloc_sum(AllocArgs a) {
   }
 }
 
-// (1) delete-next pops -> free ring window [tail, tail+B) in seq order (a
-// permutation of the window), one workgroup per 1024-op block.  Each block's
-// 1024 entries are staged in LDS in window order (its pops, then the rest)
-// and written by consecutive threads: written straight from the lanes, a
-// wave's stores formed one run or two by the data, and batches with pops ran
-// 2-4 us slower (profiles/r05n_timing_c3_store.txt; the free ring's other
-// writer, k_post_ring, rule 13).  In k_alloc_ring's single workgroup this
-// step took about half of its 47 us.
-__global__ __launch_bounds__(1024) void k_alloc_pops(AllocArgs a) {
-  __shared__ uint32_t s_stage[1024];
-  const uint32_t tid = threadIdx.x, c = blockIdx.x;
-  if (a.scal->error) return;
-  uint32_t p0 = 0, pops = 0;  // pops before this block, and in the batch (every count read)
-  for (uint32_t b = 0; b < a.nblk; ++b) {
-    const uint32_t x = a.bsum[2 * b];
-    pops += x;
-    p0 += b < c ? x : 0u;
-  }
-  const uint32_t rs = (uint32_t)a.ring_size, tbase = (uint32_t)(a.scal->tail % a.ring_size);
-  const uint32_t i = c * 1024 + tid, f = a.pflag[i], slot = a.pslot[i], tp = a.bsum[2 * c];
-  const bool pop = f & 1u;
-  const uint32_t pp = (f >> 2) & 1023u;
-  s_stage[pop ? pp : tp + (tid - pp)] = pop ? slot : kNone;
-  __syncthreads();
-  const uint32_t pos = tid < tp ? p0 + tid : pops + (c * 1024 - p0) + (tid - tp);
-  a.ring[ring_at(tbase, pos, rs)] = s_stage[tid];
-}
-
-// One workgroup, after k_alloc_pops: (2) the allocation window
+// One workgroup: (1) delete-next pops -> free ring window [tail, tail+B) in seq
+// order (a permutation of the window); (2) the allocation window
 // [head, head+B) is read in order, exactly once, and its first m entries are
 // handed to the successful creates in seq order (TOO_MANY_MESSAGES cutoff).
 __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   __shared__ uint32_t s_off[2][1024];
   __shared__ uint32_t s_win[kWinRing];
+  __shared__ uint32_t s_stage[kWinGroup][1024];
   const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
   // block offsets (nblk <= 1024)
@@ -604,11 +578,47 @@ __global__ __launch_bounds__(1024) void k_alloc_ring(AllocArgs a) {
   Scal* sc = a.scal;
   const uint64_t tail0 = sc->tail, head0 = sc->head;
   const uint32_t rs = (uint32_t)a.ring_size;
-  const uint32_t hbase = (uint32_t)(head0 % a.ring_size);
+  const uint32_t tbase = (uint32_t)(tail0 % a.ring_size), hbase = (uint32_t)(head0 % a.ring_size);
   const uint64_t count1 = sc->count - pops;
   const uint64_t room = a.N - count1;
   const uint64_t m = scnt < room ? scnt : room;
-  // (1) pops -> ring: k_alloc_pops, before this kernel
+  // (1) pops -> ring.  In-block prefixes come from k_alloc_sum (pflag bits
+  // 2..11), so the blocks are independent: no barrier, loads in flight
+  // together.
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += kWinGroup) {
+    uint32_t f[kWinGroup], slot[kWinGroup];  // loads of 8 blocks in flight together
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t i = (c0 + u) * 1024 + tid;
+      f[u] = c0 + u < a.nblk ? a.pflag[i] : 0u;
+      slot[u] = c0 + u < a.nblk ? a.pslot[i] : 0u;
+    }
+    // each block's 1024 entries staged in LDS in window order (its pops,
+    // then the rest) and written by consecutive threads: written straight
+    // from the lanes, a wave's stores formed one run or two by the data, and
+    // batches with pops ran 2-4 us slower (profiles/r05n_timing_c3_store.txt;
+    // the free ring's other writer, k_post_ring, rule 13)
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t c = c0 + u;
+      if (c < a.nblk) {
+        const bool pop = f[u] & 1u;
+        const uint32_t pp = (f[u] >> 2) & 1023u, P0 = c ? s_off[0][c - 1] : 0u, tp = s_off[0][c] - P0;
+        s_stage[u][pop ? pp : tp + (tid - pp)] = pop ? slot[u] : kNone;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < kWinGroup; ++u) {
+      const uint32_t c = c0 + u;
+      if (c < a.nblk) {
+        const uint32_t P0 = c ? s_off[0][c - 1] : 0u, tp = s_off[0][c] - P0;
+        const uint32_t pos = tid < tp ? P0 + tid : pops + (c * 1024 - P0) + (tid - tp);
+        a.ring[ring_at(tbase, pos, rs)] = s_stage[u][tid];
+      }
+    }
+    __syncthreads();  // the stage is refilled by the next group
+  }
   __threadfence_block();
   __syncthreads();
   // (2) allocation window [head, head + B), read in order in 1024-entry
@@ -754,30 +764,51 @@ __global__ __launch_bounds__(1024) void k_post_sum(PostArgs a) {
 // threads, so that every wave writes consecutive ring entries whatever the
 // split (scattered straight from the lanes, a wave's writes formed one run or
 // two by the data: k_post_ring 2.7 us faster at C3 without by-id deletes).
-// One workgroup per 1024-op block (a single workgroup looping over the blocks
-// took 22 us): the block's entries in run order through LDS, its deletes,
-// then the rest, written by consecutive threads (rule 13); block 0 commits
-// the counters.
 __global__ __launch_bounds__(1024) void k_post_ring(PostArgs a) {
-  __shared__ uint32_t s_run[1024];
-  const uint32_t tid = threadIdx.x, c = blockIdx.x;
+  __shared__ uint32_t s_off[1024];
+  __shared__ uint32_t s_run[8][1024];
+  const uint32_t tid = threadIdx.x;
   if (a.scal->error) return;
-  uint32_t p0 = 0, nd = 0;  // deletes before this block, and in the batch (every count read)
-  for (uint32_t b = 0; b < a.nblk; ++b) {
-    const uint32_t x = a.bsum[b];
-    nd += x;
-    p0 += b < c ? x : 0u;
+  s_off[tid] = tid < a.nblk ? a.bsum[tid] : 0u;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t x = tid >= off ? s_off[tid - off] : 0u;
+    __syncthreads();
+    s_off[tid] += x;
+    __syncthreads();
   }
+  const uint32_t nd = s_off[1023];
   Scal* sc = a.scal;
   const uint32_t rs = (uint32_t)a.ring_size;
   const uint32_t tbase = (uint32_t)((sc->tail0 + sc->pops) % a.ring_size);
-  const uint32_t i = c * 1024 + tid, f = a.dflag[i], slot = a.dslot[i], Dc = a.bsum[c], r = f >> 1;
-  const bool d = f & 1u;
-  s_run[d ? r : Dc + (tid - r)] = d ? slot : kNone;
-  __syncthreads();
-  const uint32_t pos = tid < Dc ? p0 + tid : nd + c * 1024 - p0 + (tid - Dc);
-  a.ring[ring_at(tbase, pos, rs)] = s_run[tid];
-  if (c == 0 && tid == 0) {
+  for (uint32_t c0 = 0; c0 < a.nblk; c0 += 8) {  // no barrier: blocks are independent
+    uint32_t f[8], slot[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t i = (c0 + u) * 1024 + tid;
+      f[u] = c0 + u < a.nblk ? a.dflag[i] : 0u;
+      slot[u] = c0 + u < a.nblk ? a.dslot[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {  // run order: the block's deletes, then the rest
+      const uint32_t c = c0 + u;
+      const bool d = f[u] & 1u;
+      const uint32_t Dc = c < a.nblk ? s_off[c] - (c ? s_off[c - 1] : 0u) : 0u, r = f[u] >> 1;
+      s_run[u][d ? r : Dc + (tid - r)] = d ? slot[u] : kNone;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t c = c0 + u;
+      if (c < a.nblk) {
+        const uint32_t P0 = c ? s_off[c - 1] : 0u, Dc = s_off[c] - P0;
+        const uint32_t pos = tid < Dc ? P0 + tid : nd + c * 1024 - P0 + (tid - Dc);
+        a.ring[ring_at(tbase, pos, rs)] = s_run[u][tid];
+      }
+    }
+    __syncthreads();  // the next group restages
+  }
+  if (tid == 0) {
     sc->nd = nd;
     sc->count = sc->count1 + sc->m - nd;
     sc->head = sc->head0 + sc->m;
