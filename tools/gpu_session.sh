@@ -105,8 +105,8 @@ case "$2" in
     done ;;
   spassnoise)  # request-level counters of the sealed pass over identical and differing inputs
     PMC_OUT="$O/pmc" PMC_ARGS="--oram --log2n 20 --batch 65536 --auth" PMC_KERN=k_spass \
-      PMC_CTRS="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_UC_REQ_sum TCC_HIT_sum" \
-      PMC_RUNS="main:1234 main:1234 main:99 all_read:1234 all_write:1234" \
+      PMC_CTRS="${SPN_CTRS:-TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_UC_REQ_sum TCC_HIT_sum}" \
+      PMC_RUNS="${SPN_RUNS:-main:1234 main:99 all_read:1234 all_write:1234 all_write:99}" \
       step pmc_spass 900 bash tools/gpu_pmc_mix.sh
     find "$O/pmc" -mindepth 1 -maxdepth 1 -type d -exec rm -rf {} + ;;
   timeall)  # every timing shape, then the default bench line
