@@ -109,6 +109,12 @@ case "$2" in
       PMC_RUNS="${SPN_RUNS:-main:1234 main:99 all_read:1234 all_write:1234 all_write:99}" \
       step pmc_spass 900 bash tools/gpu_pmc_mix.sh
     find "$O/pmc" -mindepth 1 -maxdepth 1 -type d -exec rm -rf {} + ;;
+  rollab)  # the sealed pass's requests and speed: the in-tree build against ab/libgvstore_roll.so
+    GVS_LIB_OVERRIDE=ab/libgvstore_roll.so SPN_CTRS="SQC_TC_INST_REQ SQ_INSTS_VALU TCC_EA0_RDREQ_sum TCC_HIT_sum" \
+      bash "$0" "$1/roll" spassnoise && \
+    step bench_auth_base 300 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 && \
+    GVS_LIB_OVERRIDE=ab/libgvstore_roll.so step bench_auth_roll 300 \
+      python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
