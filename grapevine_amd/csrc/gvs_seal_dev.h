@@ -286,10 +286,16 @@ __device__ inline uint32_t te1_at(const LdsTe& t, uint32_t s, int k) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.base) + 128u + off);
 }
 
-// aes128_rounds_n on the two-table window
+// aes128_rounds_n on the two-table window.  The rounds are rolled: unrolled,
+// the sealed pass's loop body did not fit the instruction cache (15.8 M
+// instruction requests to L2 per 2^20-row launch, a count that followed the
+// request mix, and refetched code lines made its FETCH_SIZE noisy: ~900 64-B
+// reads between two seeds of one mix); rolled, 133 K requests, the same under
+// every mix, read requests within 13 of each other, 2.5 % slower
+// (profiles/r05ai_spass_inst_requests.txt, r05aj_spass_roll_ab.txt)
 template <int R0, int NB>
 __device__ inline void aes128_rounds_n2(const AesRk& rk, const LdsTe& te, uint32_t (&s)[NB][4]) {
-#pragma unroll
+#pragma unroll 1
   for (int r = R0; r < 10; ++r) {
     uint32_t l[NB][16];
 #pragma unroll

@@ -115,6 +115,8 @@ case "$2" in
     step bench_auth_base 300 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 && \
     GVS_LIB_OVERRIDE=ab/libgvstore_roll.so step bench_auth_roll 300 \
       python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
+  allfinal)  # the GPU suite without counters/timing, the profiling session, then the driver's command, smoke and bench lines
+    tests && bash "$0" "$1" prof && bash "$0" "$1" final ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null
