@@ -32,9 +32,11 @@ template <>
 __device__ inline bool key_lt<uint64_t>(const uint64_t& a, const uint64_t& b) {
   return a < b;
 }
+// bitwise & and |: a short-circuit || / && may compile to a branch on the
+// keys (tests/test_code_object.py checks the sort kernels for any)
 template <>
 __device__ inline bool key_lt<Key128>(const Key128& a, const Key128& b) {
-  return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo);
+  return (a.hi < b.hi) | ((a.hi == b.hi) & (a.lo < b.lo));
 }
 
 // c ? a : b per component (a select of whole structs goes through scratch)
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(1024) void k_bitonic_tile(K* data, uint32_t kmerge,
 // it showed in FETCH_SIZE under regular key orders).
 template <typename K>
 __device__ inline void cx_static(K& a, K& b, bool live) {  // a at the lower index
-  const bool sw = live && key_lt(b, a);
+  const bool sw = live & key_lt(b, a);
   const K ta = a;
   a = key_sel(sw, b, a);
   b = key_sel(sw, ta, b);

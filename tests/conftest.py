@@ -24,24 +24,14 @@ def oracle_lib():
 
 # Whole-pipeline property tests (byte counters, kernel durations) run after
 # every parity test: under `pytest -x` a failing property must not keep the
-# oracle-parity evidence from being collected.  The sealed shapes' byte
-# counters run last of all: the sealed pass's FETCH_SIZE has a known noise
-# residue (DESIGN.md §3 "What is left"; a marginal bias on some sealed mix in
-# about one full run of two), and under -x it must not keep the plain, routed,
-# wire and expiry counters and the timing shapes from being run.
+# oracle-parity evidence from being collected.  Inside each module the file's
+# own order holds.
 PROPERTY_MODULES = ("test_oblivious.py", "test_timing.py")
-SEALED_COUNTER_SHAPES = ("auth", "oram_auth", "omap_auth")
 
 
 def _property_rank(item):
     name = os.path.basename(str(item.fspath))
-    if name not in PROPERTY_MODULES:
-        return 0
-    cs = getattr(item, "callspec", None)
-    if (name == "test_oblivious.py" and item.originalname == "test_hbm_bytes_identical" and cs is not None
-            and cs.params.get("shape") in SEALED_COUNTER_SHAPES):
-        return len(PROPERTY_MODULES) + 1
-    return PROPERTY_MODULES.index(name) + 1
+    return PROPERTY_MODULES.index(name) + 1 if name in PROPERTY_MODULES else 0
 
 
 @pytest.hookimpl(trylast=True)  # after -m deselection

@@ -36,3 +36,108 @@ def test_whole_process_rewalk_is_measured_again():
     # within 3x of the shape's median: no re-run
     per["deletes"] = _proc(_pre([50, 55, 60, 45, 70, 55]))
     assert ob.rewalk_processes(per) == []
+
+
+# ---- the timing test's rules (tests/test_timing.py evaluate(), evaluate_interleaved())
+
+import random  # noqa: E402
+
+import test_timing as tt  # noqa: E402
+
+KERNELS = [("k_sort", 5.0), ("k_scan", 6.0), ("k_pass", 5600.0)]
+
+
+def _timing_proc(seed, n_batches=3 + tt.N_MEAS, bump=None, scale=1.0):
+    """One process: per-batch (kernel, us) with small noise; bump = {(measured
+    batch, kernel index): extra us}."""
+    r = random.Random(seed)
+    out = []
+    for i in range(n_batches):
+        j = i - (n_batches - tt.N_MEAS)
+        out.append([(k, v * scale + r.gauss(0, 0.05 if v < 100 else 3.0) + (bump or {}).get((j, idx), 0.0))
+                    for idx, (k, v) in enumerate(KERNELS)])
+    return out
+
+
+def _shape(**bumps):
+    mixes = ["rud", "main", "hot_next", "deletes", "rud#2"]
+    return {m: _timing_proc(n, bump=bumps.get(m.replace("#", "_"))) for n, m in enumerate(mixes)}
+
+
+def test_timing_clean_shape_passes():
+    res = tt.evaluate(_shape(), "rud")
+    assert not res["bad"] and res["aside"] is None and not res["rerun"]
+
+
+def test_timing_stall_batch_is_one_set_aside():
+    # one batch of one process: two unrelated kernels over the bound together
+    res = tt.evaluate(_shape(hot_next={(4, 0): 24.6, (4, 1): 6.0}), "rud")
+    assert not res["bad"], res["bad"]
+    assert res["aside"][:2] == ("hot_next", 4) and len(res["aside"][2]) == 2
+
+
+def test_timing_two_stall_batches_in_one_process_fail_and_rerun():
+    res = tt.evaluate(_shape(hot_next={(1, 0): 20.0, (4, 1): 20.0}), "rud")
+    assert res["aside"] is None
+    assert {(v[1], v[2], v[5]) for v in res["bad"] if v[2] == "batch"} == {("hot_next", "batch", 1),
+                                                                           ("hot_next", "batch", 4)}
+    assert res["rerun"] == ["hot_next"]
+    # the fresh process may not set anything aside
+    assert tt.evaluate(_shape(hot_next={(4, 0): 20.0}), "rud", fresh=("hot_next",))["bad"]
+
+
+def test_timing_excursion_repeated_across_mixes_is_not_set_aside():
+    # the same kernel and measured batch in two processes: a draw-tied leak
+    res = tt.evaluate(_shape(main={(2, 0): 20.0}, deletes={(2, 0): 20.0}), "rud")
+    assert res["aside"] is None and len([v for v in res["bad"] if v[2] == "batch"]) == 2
+
+
+def test_timing_one_set_aside_per_shape():
+    res = tt.evaluate(_shape(main={(2, 0): 20.0}, deletes={(3, 1): 20.0}), "rud")
+    assert res["aside"] == ("main", 2, [("k_sort", 20.0)]) or res["aside"][0] == "main"
+    assert [v[1] for v in res["bad"] if v[2] == "batch"] == ["deletes"] and res["rerun"] == ["deletes"]
+
+
+def test_timing_leak_in_every_batch_fails_bias():
+    leak = {(j, 0): 3.0 for j in range(tt.N_MEAS)}
+    res = tt.evaluate(_shape(deletes=leak), "rud")
+    assert any(v[1] == "deletes" and v[2] == "bias" and v[0] == "k_sort" for v in res["bad"]), res["bad"]
+
+
+def test_timing_slow_reference_process_widens_the_noise():
+    # a reference process slow in every batch differs from its second process
+    # by as much: that difference is part of the noise, not a failure of
+    # every other mix (the r05af case)
+    per = _shape()
+    per["rud"] = _timing_proc(0, bump={(j, 2): 60.0 for j in range(tt.N_MEAS)})
+    res = tt.evaluate(per, "rud")
+    assert not res["bad"], res["bad"]
+
+
+def _interleaved(bump=None, sigma=3.0, offsets=(0.0, 40.0)):
+    mixes = ["rud", "main", "hot_next", "deletes"]
+    procs = []
+    for p, off in enumerate(offsets):
+        r = random.Random(100 + p)
+        procs.append({m: [[(k, v + (off if v > 100 else 0.0) + r.gauss(0, sigma if v > 100 else 0.05)
+                            + (bump or {}).get((m, j, idx), 0.0)) for idx, (k, v) in enumerate(KERNELS)]
+                          for j in range(tt.N_MEAS)] for m in mixes})
+    return procs
+
+
+def test_interleaved_process_offset_cancels():
+    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(), "rud")
+    assert not bad, bad
+    assert mdb["2:k_pass"] < 12.0, mdb  # 40-us process offset, 3-us batch noise
+
+
+def test_interleaved_small_leak_in_the_pass_is_seen():
+    leak = {("hot_next", j, 2): 12.0 for j in range(tt.N_MEAS)}
+    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(leak), "rud")
+    assert [(v[0], v[1]) for v in bad] == [("k_pass", "hot_next")], bad
+
+
+def test_interleaved_one_stalled_batch_is_dropped():
+    stall = {("main", 3, 0): 25.0}
+    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(stall), "rud")
+    assert not bad, bad

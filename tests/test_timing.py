@@ -1,7 +1,7 @@
 """Timing side of the obliviousness contract (api/proto/grapevine.proto:120-122:
 READ, UPDATE and DELETE must be indistinguishable in access patterns *and
-timings*) at the headline shape, BASELINE config 3: a 2^24-message store and
-64K-request batches.
+timings*; README.md:64-71) at the headline shape, BASELINE config 3: a
+2^24-message store and 64K-request batches.
 
 Each mix runs tools/oblivious_probe.py under `rocprofv3 --kernel-trace`.  The
 measured batches are seed-controlled, as in tests/test_oblivious.py: SEEDS x
@@ -10,19 +10,41 @@ so that a mix's difference from the reference can be told from a difference
 between two draws.  The prefill batches are identical in every process, and a
 second reference process runs the reference mix again: both are the noise.
 
-Two checks per kernel (the counter test's, in microseconds):
+Per-process checks, per kernel (evaluate(); microseconds):
   * every measured batch of every mix within 3x the noise range + 2 us of the
-    reference median.  One excursion per process is set aside, printed in the
-    report: a single batch of one kernel over the bound, the only one in its
-    process and not repeated by that kernel in any other measured batch of the
-    mix (a leak follows the mix, and each mix runs six independent draws).
-    Such one-offs were 2-10 us on 5-us kernels in random mixes and positions
-    (profiles/r05o-r05q_timing_c3_*.txt), the same kind as the counter test's
-    one-batch re-walks;
+    reference median;
   * no bias: a mix's mean within 5 standard errors (sigma pooled from the
-    identical-input samples) + 2 us of the reference mean.  A pass whose
-    workgroups did work in proportion to the rows or groups a batch touches
-    shows here under the hot and all-miss mixes.
+    identical-input samples) + 2 us of the reference mean.
+
+Stalls.  The box sometimes stalls a process for a few tens of microseconds
+(one hot_next batch in which five unrelated sort and scan
+kernels ran 2-25 us long together).  The unit of a stall is the measured
+batch, not the kernel: one batch of one process whose kernels exceed the
+bound is set aside, with all its excursions, when (a) it is that process's
+only batch with an excursion, (b) no other process has an excursion in the
+same kernel and measured batch (inputs are seed-controlled, so a leak tied to
+a draw repeats across mixes), and (c) no other batch of the shape was set
+aside (one per shape).  The set-aside batch is left out of that process's
+bias too.  Any other process with a violation is run again once in a fresh
+process (at most two per shape), and the fresh process must have no
+violation at all: a leak follows the inputs, which are the same.  When most
+mixes fail the same kernel's bias in the same direction, the reference
+process is the one run again.  Every set-aside and re-run is printed in the
+report, and the assertion message carries the violations with their measured
+batch and process, and the per-kernel rows they come from.
+
+In-process comparison (check_interleaved()).  A process-level offset of the
+table pass (tens of microseconds between two processes of identical inputs)
+limits what a comparison between processes can see.  The headline and sealed
+shapes therefore also run every mix interleaved in one process (the probe's
+'a+b+...' schedule: per seed, the mixes in a rotated order, the generator
+reseeded before each), in two processes with different rotations.  Per kernel
+the bias of a mix is the mean over processes of (mix mean - reference mean)
+in that process, against 5 standard errors from the pooled within-process
+sigma + 2 us.  Each (process, mix) group drops its single most extreme batch
+(the same rule for every mix, the reference included), so one stalled batch
+cannot decide the result; a leak in every batch of a mix cannot hide.  The
+report gives every kernel's minimal detectable bias (the bound).
 
 Shapes: the store under seven mixes, including adversarial ones (every request
 aimed at one recipient, every read missing, only deletes); the expiry sweep
@@ -31,6 +53,7 @@ storage (2^22 messages, the production sealed pass, README.md:49-50); the
 2-shard router and padded all-to-all."""
 import csv
 import glob
+import importlib.util
 import math
 import os
 import shutil
@@ -66,6 +89,16 @@ PER_SEED = 2
 N_MEAS = len(SEEDS) * PER_SEED
 FLOOR_US = 2.0       # trace-clock jitter floor, per batch and for the bias
 BIAS_SIGMAS = 5.0
+MAX_RERUNS = 2       # fresh processes per shape
+# in-process comparison: processes and their rotations of the mix order
+INTERLEAVED_ROTATIONS = (0, 3)
+
+
+def load_probe():
+    spec = importlib.util.spec_from_file_location("oblivious_probe_sched", PROBE)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def kernel_trace(mix, outdir, args):
@@ -89,19 +122,27 @@ def kernel_trace(mix, outdir, args):
             for x in rows]
 
 
-def check_durations(shape, tmp_path):
-    sh = SHAPES[shape]
-    ref_mix = sh["ref"]
-    per = {}
-    for mix in sh["mixes"] + [ref_mix + "#2"]:
-        d = str(tmp_path / f"{shape}_{mix.replace('#', '_')}")
-        per[mix] = [[(k, v) for k, _, _, v in b] for b in
-                    split_batches([(k, None, None, v) for k, v in
-                                   kernel_trace(mix.split("#")[0], d, sh["args"])])]
+def batches_of(mix, outdir, args):
+    """Per-batch lists of (kernel, duration us) of one probe process."""
+    return [[(k, v) for k, _, _, v in b] for b in
+            split_batches([(k, None, None, v) for k, v in kernel_trace(mix, outdir, args)])]
+
+
+def evaluate(per, ref_mix, fresh=()):
+    """The per-process checks (module docstring) on {process: per-batch lists of
+    (kernel, us)}; the reference's second process is `ref_mix + '#2'`.
+
+    Returns dict(lines=per-kernel report rows, bad=violations, aside=the batch
+    set aside or None, rerun=processes to run again).  A violation is (kernel,
+    process, kind, value, bound, measured batch or None, process index).
+    Processes in `fresh` were already run again: no set-aside for them."""
+    procs = list(per)
     ref_b = per[ref_mix]
     kernels = [k for k, _ in ref_b[-1]]
+    for mix, bs in per.items():
+        assert [x[0] for x in bs[-1]] == kernels, f"{mix}: kernel sequence differs"
     n_pre = min(len(bs) for bs in per.values()) - N_MEAS
-    lines, bad, over = [], [], []
+    stats = []
     for idx, k in enumerate(kernels):
         # noise: the identical prefill batches (batch 0: cold) across the
         # processes, and the reference mix against its second process
@@ -118,41 +159,177 @@ def check_durations(shape, tmp_path):
             dof += 1
         sigma = math.sqrt(ss / dof) if dof else 0.0
         tol = 3.0 * rng + FLOOR_US
-        own = [b[idx][1] for b in ref_b[-N_MEAS:]]
-        ref, mu = statistics.median(own), statistics.fmean(own)
+        ref = statistics.median(b[idx][1] for b in ref_b[-N_MEAS:])
         btol = BIAS_SIGMAS * sigma * math.sqrt(2.0 / N_MEAS) + FLOOR_US
+        stats.append((rng, sigma, tol, ref, btol))
+
+    # per-batch excursions: {process: {measured batch: [(kernel index, dev)]}}
+    exc = {m: {} for m in procs}
+    for m, bs in per.items():
+        for j, b in enumerate(bs[-N_MEAS:]):
+            for idx, (_, v) in enumerate(b):
+                if abs(v - stats[idx][3]) > stats[idx][2]:
+                    exc[m].setdefault(j, []).append((idx, round(v - stats[idx][3], 1)))
+    hit = {}  # (kernel index, measured batch) -> processes with an excursion there
+    for m, bj in exc.items():
+        for j, es in bj.items():
+            for idx, _ in es:
+                hit.setdefault((idx, j), set()).add(m)
+    aside = None
+    for m in procs:  # (a) one batch, (b) not repeated elsewhere, (c) one per shape, not a fresh process
+        if aside is None and m not in fresh and len(exc[m]) == 1:
+            (j, es), = exc[m].items()
+            if all(hit[(idx, j)] == {m} for idx, _ in es):
+                aside = (m, j, [(kernels[idx], d) for idx, d in es])
+
+    def kept(m, idx):
+        return [b[idx][1] for j, b in enumerate(per[m][-N_MEAS:]) if not (aside and aside[:2] == (m, j))]
+
+    bad, lines = [], []
+    for m, bj in exc.items():
+        for j, es in sorted(bj.items()):
+            if aside and aside[:2] == (m, j):
+                continue
+            for idx, d in es:
+                bad.append((kernels[idx], m, "batch", d, round(stats[idx][2], 1), j, procs.index(m)))
+    for idx, k in enumerate(kernels):
+        rng, sigma, tol, ref, btol = stats[idx]
+        mu = statistics.fmean(kept(ref_mix, idx))
         row = [f"{k[:30]:30s} ref={ref:10.1f}us range={rng:7.1f} sigma={sigma:6.2f} tol={tol:7.1f} btol={btol:6.1f}"]
-        for mix, bs in per.items():
-            assert [x[0] for x in bs[-1]] == kernels, f"{mix}: kernel sequence differs"
-            meas = [b[idx][1] for b in bs[-N_MEAS:]]
-            dev = max(abs(v - ref) for v in meas)
-            bias = statistics.fmean(meas) - mu
-            row.append(f"{mix}:{dev:.1f}/{bias:+.1f}")
-            for j, v in enumerate(meas):
-                if abs(v - ref) > tol:
-                    over.append((mix, idx, k, j, round(abs(v - ref), 1), round(tol, 1)))
-            if mix != ref_mix and abs(bias) > btol:
-                bad.append((k, mix, "bias", round(bias, 1), round(btol, 1)))
+        for m in procs:
+            vals = [b[idx][1] for b in per[m][-N_MEAS:]]
+            dev = max(abs(v - ref) for v in vals)
+            bias = statistics.fmean(kept(m, idx)) - mu
+            row.append(f"{m}:{dev:.1f}/{bias:+.1f}")
+            if m != ref_mix and abs(bias) > btol:
+                bad.append((k, m, "bias", round(bias, 1), round(btol, 1), None, procs.index(m)))
         lines.append(" ".join(row))
-    # per-batch excursions: one per process may be set aside (module docstring)
-    aside = []
-    for mix in per:
-        ex = [o for o in over if o[0] == mix]
-        if len(ex) == 1:
-            aside.append(ex[0])
-        else:
-            bad += [(k, m, "batch", d, t) for m, _, k, _, d, t in ex]
+
+    # what a fresh process could settle: the processes with violations; the
+    # reference instead when most mixes fail one kernel's bias the same way
+    rerun = []
+    others = [m for m in procs if m != ref_mix]
+    for k in {v[0] for v in bad if v[2] == "bias"}:
+        signs = [math.copysign(1, v[3]) for v in bad if v[0] == k and v[2] == "bias"]
+        if len(signs) > len(others) / 2 and abs(sum(signs)) == len(signs):
+            rerun.append(ref_mix)
+            break
+    if not rerun:
+        rerun = list(dict.fromkeys(v[1] for v in bad))
+    rerun = [m for m in rerun if m not in fresh]
+    return dict(lines=lines, bad=bad, aside=aside, rerun=rerun, kernels=kernels)
+
+
+def failure_message(what, res, extra=""):
+    """Violations first (kernel, process, kind, value, bound, measured batch,
+    process index), then the report rows of the kernels involved."""
+    ks = {v[0][:30].rstrip() for v in res["bad"]}
+    rows = [ln for ln in res["lines"] if ln[:30].rstrip() in ks]
+    return (f"{what}: kernel durations depend on the request mix: {res['bad'][:24]}"
+            f"\nset aside: {res.get('aside')}\n{extra}" + "\n".join(rows[:12]))
+
+
+def check_durations(shape, tmp_path):
+    sh = SHAPES[shape]
+    ref_mix = sh["ref"]
+    per, fresh, log = {}, [], []
+    for mix in sh["mixes"] + [ref_mix + "#2"]:
+        d = str(tmp_path / f"{shape}_{mix.replace('#', '_')}")
+        per[mix] = batches_of(mix.split("#")[0], d, sh["args"])
+    res = evaluate(per, ref_mix)
+    while res["bad"] and res["rerun"] and len(fresh) < MAX_RERUNS:
+        for m in res["rerun"][:MAX_RERUNS - len(fresh)]:
+            d = str(tmp_path / f"{shape}_{m.replace('#', '_')}_again")
+            before = [v for v in res["bad"] if v[1] == m]
+            per[m] = batches_of(m.split("#")[0], d, sh["args"])
+            fresh.append(m)
+            log.append(f"{m} run again (violations {before[:6]})")
+        res = evaluate(per, ref_mix, fresh)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"timing_c3_{shape}.txt"), "w") as f:
+        f.write("\n".join(res["lines"]) + "\n")
+        f.write(f"set aside (process, measured batch, [(kernel, dev us)]): {res['aside']}\n")
+        f.write(f"run again in a fresh process: {log}\n")
+        f.write(f"violations: {res['bad']}\n")
+    if res["bad"]:
+        pytest.fail(failure_message(shape, res, f"run again: {log}\n"), pytrace=False)
+
+
+def evaluate_interleaved(procs, ref_mix):
+    """The in-process comparison on [{mix: [per-batch lists of (kernel, us)]}]
+    (one dict per process, the measured batches of each mix in run order).
+    Returns (report rows, violations, {kernel: minimal detectable bias})."""
+    mixes = list(procs[0])
+    kernels = [k for k, _ in procs[0][ref_mix][0]]
+    lines, bad, mdb = [], [], {}
+    for idx, k in enumerate(kernels):
+        groups = {}  # (process, mix) -> kept values (the most extreme batch dropped)
+        for p, per in enumerate(procs):
+            for m in mixes:
+                vals = [b[idx][1] for b in per[m]]
+                assert all(b[idx][0] == k for b in per[m]), f"{m}: kernel sequence differs"
+                med = statistics.median(vals)
+                drop = max(range(len(vals)), key=lambda i: abs(vals[i] - med))
+                groups[(p, m)] = [v for i, v in enumerate(vals) if i != drop]
+        ss, dof = 0.0, 0
+        for v in groups.values():
+            mu = statistics.fmean(v)
+            ss += sum((x - mu) ** 2 for x in v)
+            dof += len(v) - 1
+        sigma = math.sqrt(ss / dof) if dof else 0.0
+        n_ref = sum(len(groups[(p, ref_mix)]) for p in range(len(procs)))
+        ref_mu = statistics.fmean(x for p in range(len(procs)) for x in groups[(p, ref_mix)])
+        row = [f"{k[:30]:30s} ref={ref_mu:10.1f}us sigma_w={sigma:6.2f}"]
+        worst = 0.0
+        for m in mixes:
+            n_m = sum(len(groups[(p, m)]) for p in range(len(procs)))
+            bias = statistics.fmean(statistics.fmean(groups[(p, m)]) - statistics.fmean(groups[(p, ref_mix)])
+                                    for p in range(len(procs)))
+            btol = BIAS_SIGMAS * sigma * math.sqrt(1.0 / n_m + 1.0 / n_ref) + FLOOR_US
+            worst = max(worst, btol)
+            row.append(f"{m}:{bias:+.1f}")
+            if m != ref_mix and abs(bias) > btol:
+                bad.append((k, m, "bias", round(bias, 1), round(btol, 1), idx))
+        mdb[f"{idx}:{k}"] = round(worst, 1)
+        row.insert(1, f"mdb={worst:6.1f}")
+        lines.append(" ".join(row))
+    return lines, bad, mdb
+
+
+def check_interleaved(shape, tmp_path):
+    sh = SHAPES[shape]
+    probe = load_probe()
+    joined = "+".join(sh["mixes"])
+    procs = []
+    for r in INTERLEAVED_ROTATIONS:
+        d = str(tmp_path / f"{shape}_interleaved_r{r}")
+        bs = batches_of(joined, d, sh["args"] + ["--rotate", str(r)])
+        sched = probe.schedule(joined, list(SEEDS), PER_SEED, r)
+        meas = bs[-len(sched):]
+        per = {m: [] for m in sh["mixes"]}
+        for (m, *_), b in zip(sched, meas):
+            per[m].append(b)
+        procs.append(per)
+    lines, bad, mdb = evaluate_interleaved(procs, sh["ref"])
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"timing_c3_{shape}_interleaved.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
-        f.write("set aside (mix, kernel index, kernel, measured batch, dev us, tol us): "
-                f"{[(m, i, k, j, d, t) for m, i, k, j, d, t in aside]}\n")
+        f.write(f"minimal detectable bias per kernel (us): {mdb}\n")
         f.write(f"violations: {bad}\n")
-    assert not bad, f"kernel durations depend on the request mix: {bad}"
+    if bad:
+        ks = {v[0][:30].rstrip() for v in bad}
+        rows = [ln for ln in lines if ln[:30].rstrip() in ks]
+        pytest.fail(f"{shape} (one process, mixes interleaved): kernel durations depend on the request mix: "
+                    f"{bad[:24]}\n" + "\n".join(rows[:12]), pytrace=False)
+    return mdb
 
 
 def test_kernel_durations_independent_of_mix(tmp_path):
     check_durations("store", tmp_path)
+
+
+def test_kernel_durations_independent_of_mix_in_process(tmp_path):
+    check_interleaved("store", tmp_path)
 
 
 def test_kernel_durations_independent_of_expiry(tmp_path):
@@ -161,6 +338,10 @@ def test_kernel_durations_independent_of_expiry(tmp_path):
 
 def test_kernel_durations_independent_of_mix_sealed(tmp_path):
     check_durations("auth", tmp_path)
+
+
+def test_kernel_durations_independent_of_mix_sealed_in_process(tmp_path):
+    check_interleaved("auth", tmp_path)
 
 
 def test_kernel_durations_independent_of_mix_routed(tmp_path):

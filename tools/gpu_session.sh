@@ -117,6 +117,10 @@ case "$2" in
       python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
   allfinal)  # the GPU suite without counters/timing, the profiling session, then the driver's command, smoke and bench lines
     tests && bash "$0" "$1" prof && bash "$0" "$1" final ;;
+  ttime)  # the GPU suite without counters/timing, then every timing shape with per-test durations
+    tests && \
+    step timing_all 1000 $PT --durations=0 tests/test_timing.py
+    cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null ;;
   timeall)  # every timing shape, then the default bench line
     step timing_all 1000 $PT tests/test_timing.py
     cp gpurun_out/timing_c3_*.txt "$O/" 2>/dev/null

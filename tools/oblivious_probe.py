@@ -8,6 +8,10 @@ state and checks the responses.
     python tools/oblivious_probe.py MIX [--log2n L] [--batch B] [--auth]
                                         [--shards S] [--fill-batches F]
 
+MIX may name several message-store mixes joined by '+': they then run
+interleaved in one process (schedule(); the timing test's in-process
+comparison).
+
 --shards S > 1 runs the sharded store in its single-process form (S shards on
 one device, the router kernels k_route_* and the padded all-to-all), against
 the oracle's cluster model.
@@ -218,9 +222,35 @@ class WirePath:
             assert sum(1 for r in got if r) > len(got) // 2, "wire prefill: most requests must verify"
 
 
+def schedule(mix, seeds, per_seed, rotate=0):
+    """The measured batches as (mix, seed, reseed before it, index of the batch
+    among its mix's).  One mix: per_seed batches per seed.  An interleaved run
+    (MIX = 'a+b+c', tests/test_timing.py) runs every mix in one process: for
+    seed number s the mixes in the order rotated by s + rotate, per_seed batches
+    each, the generator reseeded before each mix's batches, so every mix sees
+    the same draws and the order of the mixes is balanced over the seeds."""
+    mixes = mix.split("+")
+    out, cnt = [], {m: 0 for m in mixes}
+    for si, sd in enumerate(seeds):
+        r = (si + rotate) % len(mixes)
+        for m in mixes[r:] + mixes[:r]:
+            for b in range(per_seed):
+                out.append((m, sd, b == 0, cnt[m]))
+                cnt[m] += 1
+    return out
+
+
+def mix_arg(v):
+    names = set(MIXES) | set(KV_MIXES["oram"]) | set(KV_MIXES["omap"])
+    if not v or any(m not in names for m in v.split("+")):
+        raise argparse.ArgumentTypeError(f"a mix, or mixes joined by '+', of {sorted(names)}")
+    return v
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("mix", choices=sorted(set(MIXES) | set(KV_MIXES["oram"]) | set(KV_MIXES["omap"])))
+    p.add_argument("mix", type=mix_arg, help="a mix, or mixes joined by '+' (interleaved in one process)")
+    p.add_argument("--rotate", type=int, default=0, help="interleaved runs: rotation of the mix order")
     p.add_argument("--log2n", type=int, default=20)
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--batches", type=int, default=3)
@@ -243,10 +273,13 @@ def main():
     p.add_argument("--omap", action="store_true", help="the key-value map (gvs_omap_*)")
     a = p.parse_args()
     if a.oram or a.omap:
+        assert "+" not in a.mix, "interleaved runs are for the message store"
         return run_kv(a, "oram" if a.oram else "omap")
-    assert a.wire or not a.mix.startswith("wire_"), "wire_* mixes need --wire"
-    assert bool(a.expiry) == a.mix.startswith("x_") or (a.expiry and a.mix == "main"), \
-        "x_* mixes need --expiry (and --expiry takes x_* mixes or main)"
+    for m in a.mix.split("+"):
+        assert a.wire or not m.startswith("wire_"), "wire_* mixes need --wire"
+        assert bool(a.expiry) == m.startswith("x_") or (a.expiry and m == "main"), \
+            "x_* mixes need --expiry (and --expiry takes x_* mixes or main)"
+        assert m in MIXES, f"{m}: not a message-store mix"
     S = a.shards if a.shards > 1 else 0
     cfg = abi.make_config(1 << a.log2n, max_batch=a.batch, auth_storage=a.auth, shard_count=S,
                           expiry_per_batch=a.expiry)
@@ -277,23 +310,23 @@ def main():
         want = model.process_batch(reqs)
         got = run(reqs)
         assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe (prefill)"
-    params = ffi.gen_params(n_identities=a.identities, bad_auth=0, bad_recipient=0, hard_error=0,
-                            zero_recipient=0, **{"miss": 0, **MIXES[a.mix]})
     seeds = [int(x) for x in a.seeds.split(",") if x] or [a.seed]
-    for k in range(len(seeds) * a.batches):
-        if k % a.batches == 0:
-            model.seed(seeds[k // a.batches])  # same request-generator state for every mix
+    for k, (mix, sd, fresh, kx) in enumerate(schedule(a.mix, seeds, a.batches, a.rotate)):
+        if fresh:
+            model.seed(sd)  # same request-generator state for every mix
         if a.expiry:
-            cut = expiry_cutoff(a.mix, k)
+            cut = expiry_cutoff(mix, kx)
             model.set_expiry_cutoff(cut)
             store.set_expiry_cutoff(cut)
+        params = ffi.gen_params(n_identities=a.identities, bad_auth=0, bad_recipient=0, hard_error=0,
+                                zero_recipient=0, **{"miss": 0, **MIXES[mix]})
         reqs = model.gen_batch(n, params)
         if wp:
-            wp.run(reqs, a.mix)
+            wp.run(reqs, mix)
             continue
         want = model.process_batch(reqs)
         got = run(reqs)
-        assert a.no_check or got.tobytes() == want.tobytes(), "parity failure inside the probe"
+        assert a.no_check or got.tobytes() == want.tobytes(), f"parity failure inside the probe ({mix})"
     store.synchronize()
     print("probe ok", a.mix, store.stats()["messages"])
 
