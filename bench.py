@@ -182,8 +182,14 @@ def host_cpu():
     # the GPU box runs one GPU's share of the host (OMP_NUM_THREADS = 16 there):
     # os.cpu_count() reports the whole machine, so the share caps the workers
     share = int(os.environ.get("OMP_NUM_THREADS") or 0) or affinity
+    mem = None
+    try:
+        with open("/proc/meminfo") as f:
+            mem = round(int(next(x for x in f if x.startswith("MemTotal")).split()[1]) / 2**20, 1)
+    except (OSError, StopIteration, ValueError):
+        pass
     return {"model": model, "logical_cpus": os.cpu_count(), "affinity": affinity,
-            "share": min(share, affinity)}
+            "share": min(share, affinity), "mem_gib": mem}
 
 
 def c1_single_thread():
@@ -211,6 +217,43 @@ def c1_single_thread():
     return ops / t
 
 
+def c3_single_instance(budget_s):
+    """One Path ORAM + cuckoo instance at the headline capacity, 2^24 messages
+    (BASELINE config 3's table), on one thread, C3 mix: the restatement of
+    cpu_baseline() without the reduced tree height.  Its tree arrays are lazy
+    anonymous mappings (oracle/gvs_pathoram.c tree_zalloc), so host memory
+    grows only with the paths the sample visits; the first touch of those
+    pages (minor faults, counted) is inside the timed accesses.  The prefill
+    is one 2048-create batch (the instance runs ~500 accesses/s)."""
+    import resource
+    from grapevine_amd import abi
+    from oracle import ffi
+    cfg = abi.make_config(1 << 24, max_batch=65536)
+    mix = ffi.gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=0, bad_auth=0,
+                         bad_recipient=0, hard_error=0, zero_recipient=0, n_identities=1 << 12)
+    fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=1 << 12)
+    seq, oram = ffi.Model(cfg), ffi.PathOramModel(cfg)
+    seq.seed(0x6772617065 + 24)
+    r = seq.gen_batch(2048, fill)
+    seq.process_batch(r)
+    oram.process_batch(r)
+    ops, t = 0, 0.0
+    f0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
+    while t < budget_s:
+        r = seq.gen_batch(512, mix)
+        t0 = time.perf_counter()
+        oram.process_batch(r)
+        t += time.perf_counter() - t0
+        seq.process_batch(r)
+        ops += len(r)
+    faults = resource.getrusage(resource.RUSAGE_SELF).ru_minflt - f0
+    oram.close()
+    seq.close()
+    return {"value": ops / t, "unit": "req/s", "cores": 1, "capacity": 1 << 24, "requests": ops,
+            "seconds": round(t, 2), "minor_faults_per_request": round(faults / max(ops, 1), 1),
+            "peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1)}
+
+
 def cpu_baseline(budget_s, threads):
     """The reference's CPU path, restated: the grapevine handler over Path ORAM
     (oracle/gvs_pathoram.c: CuckooHashTables over Path ORAM, Z = 4, recursive
@@ -227,6 +270,7 @@ def cpu_baseline(budget_s, threads):
     cpu = host_cpu()
     threads = threads or cpu["share"]
     c1 = c1_single_thread()
+    c3 = c3_single_instance(budget_s)
     log2n = 18  # two cuckoo tables at 50 % load: ~2.7 GB per instance
     cfg = abi.make_config(1 << log2n, max_batch=65536)
     mix = ffi.gen_params(create=25, read=25, update=25, delete=25, nxt=50, miss=0, bad_auth=0,
@@ -261,9 +305,10 @@ def cpu_baseline(budget_s, threads):
     ops = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": ops / wall, "unit": "req/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
+            "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"], "host_mem_gib": cpu["mem_gib"],
             "cpu_share": cpu["share"],
             "c1_single_thread_req_s": c1,
+            "c3_capacity_single_thread": c3,
             "sample": f"PathORAM + CuckooHashTable restatement of the reference CPU path (oracle/gvs_pathoram.c; "
                       f"aligned-cmov block moves over every stash and branch slot, single-pass eviction), "
                       f"2^{log2n} capacity (tree height reduced from C3's 2^24 to bound memory), "
@@ -271,7 +316,9 @@ def cpu_baseline(budget_s, threads):
                       f"(this process's CPU share of {cpu['logical_cpus']} logical CPUs), C3 mix, "
                       f"{ops} requests in {wall:.1f}s; per-instance rate {ops / wall / threads:.0f} req/s; "
                       f"BASELINE config 1 (2^16, seeded 10K 40/40/20 create/read/delete) on one "
-                      f"thread: {c1:.0f} req/s"}
+                      f"thread: {c1:.0f} req/s; one instance at the headline capacity 2^24 on one "
+                      f"thread: {c3['value']:.0f} req/s ({c3['requests']} requests in {c3['seconds']} s, "
+                      f"peak RSS {c3['peak_rss_gib']} GiB)"}
 
 
 def front_end(torch, store, dev, batches, nreq, B):

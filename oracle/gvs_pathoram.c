@@ -35,8 +35,10 @@
  * bit-for-bit against the seqmodel (gvs_oracle.c) on seeded streams, and
  * bench.py times it as the CPU baseline (BASELINE.json config 1).
  */
+#define _DEFAULT_SOURCE /* MAP_ANONYMOUS, MAP_NORESERVE */
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include "gvs_oracle.h"
 
@@ -92,11 +94,30 @@ static uint64_t sm64(uint64_t *s) {
   return z ^ (z >> 31);
 }
 
+/* Zeroed tree arrays.  Large ones are anonymous mappings without swap
+ * reservation: at the headline capacity (2^24 messages) a cuckoo table's tree
+ * is 64 GiB of address space, of which a timed sample touches only the paths
+ * it visits (bench.py c3_single_instance); malloc's overcommit check would
+ * refuse the whole allocation up front. */
+#define BIG_ALLOC (1ull << 30)
+static void *tree_zalloc(size_t bytes) {
+  if (bytes < BIG_ALLOC) return calloc(1, bytes);
+  void *p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  return p == MAP_FAILED ? NULL : p;
+}
+static void tree_free(void *p, size_t bytes) {
+  if (!p) return;
+  if (bytes < BIG_ALLOC)
+    free(p);
+  else
+    munmap(p, bytes);
+}
+
 static void oram_free(oram *o) {
   if (!o) return;
-  free(o->data);
-  free(o->meta);
-  free(o->leaf);
+  tree_free(o->data, o->nodes * Z * (size_t)o->bsz);
+  tree_free(o->meta, o->nodes * Z * sizeof(uint64_t));
+  tree_free(o->leaf, o->nodes * Z * sizeof(uint32_t));
   free(o->sdata);
   free(o->smeta);
   free(o->sleaf);
@@ -121,9 +142,9 @@ static oram *oram_new(uint64_t n, uint32_t bsz, uint64_t *rng) {
   while ((1ull << o->L) < need) o->L++;
   o->leaves = 1ull << o->L;
   o->nodes = 2 * o->leaves - 1;
-  o->data = (uint8_t *)calloc(o->nodes * Z, bsz);
-  o->meta = (uint64_t *)calloc(o->nodes * Z, sizeof(uint64_t));
-  o->leaf = (uint32_t *)calloc(o->nodes * Z, sizeof(uint32_t));
+  o->data = (uint8_t *)tree_zalloc(o->nodes * Z * (size_t)bsz);
+  o->meta = (uint64_t *)tree_zalloc(o->nodes * Z * sizeof(uint64_t));
+  o->leaf = (uint32_t *)tree_zalloc(o->nodes * Z * sizeof(uint32_t));
   o->sdata = (uint8_t *)calloc(STASH, bsz);
   o->smeta = (uint64_t *)calloc(STASH, sizeof(uint64_t));
   o->sleaf = (uint32_t *)calloc(STASH, sizeof(uint32_t));
