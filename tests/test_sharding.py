@@ -246,3 +246,59 @@ def test_realistic_traffic_is_never_shed(S):
         out = cl.process_batch(reqs)
         assert out is not None
         assert not (out["status_code"] == abi.STATUS_CODE_INTERNAL_ERROR).any(), batch
+
+
+HOT_MIXES = {  # tools/oblivious_probe.py's hot mixes: every op on one recipient, no ids
+    "hot_create": dict(create=100, read=0, update=0, delete=0, hot=100),
+    "hot_next": dict(create=30, read=35, update=0, delete=35, nxt=100, hot=100),
+    "hot_next_rud": dict(create=0, read=50, update=0, delete=50, nxt=100, hot=100),
+}
+
+
+@pytest.mark.parametrize("mix", sorted(HOT_MIXES))
+def test_hot_window_deviation_is_confined_to_shed_keys(mix):
+    """The sharded store's one semantic deviation from the unsharded store
+    ("What's missing" 5; DESIGN.md §6 "Hot keys"), pinned
+    against the unmodified unsharded model: the same hot window goes to both.
+    Every shed request is answered differently (INTERNAL_ERROR), and every
+    other answer that differs belongs to a later request with the same routing
+    key as a shed one (it sees the store without the shed request's effect).
+    A window of hot creates differs in exactly the shed requests: past the 62-
+    message limit the unsharded store refuses them too."""
+    S, B = 4, 1024
+    single = ffi.Model(abi.make_config(1 << 16, mailbox_partitions=64, mailbox_partition_slots=64,
+                                       max_batch=S * B))
+    cl = ffi.Cluster(cluster_cfg(S, N=1 << 15, B=B, Q=32, Sr=64, C=B))
+    single.seed(77)
+    fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=300)
+    for _ in range(2):
+        r = single.gen_batch(S * B, fill)
+        single.process_batch(r)
+        assert cl.process_batch(r) is not None
+    p = ffi.gen_params(n_identities=300, bad_auth=0, bad_recipient=0, hard_error=0, zero_recipient=0,
+                       **{"miss": 0, **HOT_MIXES[mix]})
+    n_shed = n_confined = 0
+    for _ in range(3):
+        reqs = single.gen_batch(S * B, p)
+        shed = ffi.route_shed(cl.config, reqs, B)
+        key = ffi.route_key(cl.config, reqs)
+        o1, o2 = single.process_batch(reqs), cl.process_batch(reqs)
+        assert o2 is not None
+        diff = o1["status_code"] != o2["status_code"]
+        for f in ("sender", "recipient", "timestamp", "payload"):
+            diff |= (o1["record"][f] != o2["record"][f]).reshape(len(reqs), -1).any(axis=1)
+        assert (o2["status_code"][shed] == abi.STATUS_CODE_INTERNAL_ERROR).all()
+        assert diff[shed].all()
+        first_shed = {}
+        for i in np.nonzero(shed)[0]:
+            first_shed.setdefault(int(key[i]), int(i))
+        for i in np.nonzero(diff & ~shed)[0]:
+            k = int(key[i])
+            assert k in first_shed and first_shed[k] < i, (mix, int(i))
+            n_confined += 1
+        if mix == "hot_create":
+            assert np.array_equal(diff, shed)
+        n_shed += int(shed.sum())
+    assert n_shed > 0
+    if mix == "hot_create":
+        assert n_confined == 0
