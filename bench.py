@@ -65,8 +65,10 @@ def parse():
                    help="S > 1: time one GPU holding all S shards of a sharded store (in-process "
                         "transport, S x the per-GPU load) and print the predicted per-GPU step of an "
                         "S-GPU run instead of the normal line")
-    p.add_argument("--xgmi-gbs", type=float, default=64.0,
-                   help="--predict-shards: assumed xGMI rate per peer link and direction (GB/s)")
+    p.add_argument("--xgmi-gbs", type=float, default=153.0,
+                   help="--predict-shards: assumed xGMI rate per peer link and direction (GB/s); the "
+                        "default is SURVEY.md §8(e)'s link budget (7 links x ~153 GB/s per GPU), not a "
+                        "measured RCCL rate: no multi-GPU box has run here")
     p.add_argument("--prediction-json", default=os.path.join(ROOT, "profiles", "scale_prediction.json"))
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     p.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_auth_latest.json"))

@@ -1262,6 +1262,11 @@ static int decode_error(gvs_handle* h, uint32_t e) {
     h->err = "batch overflow: more distinct rows of one message partition than its transaction slots";
     return GVS_ERR_BATCH_OVERFLOW;
   }
+  if (e & kJErr) {
+    h->err = "batch overflow: the distinct rows of one message partition in this and the previous batch "
+             "exceed the sealed pass's LDS staging buffers (" + std::to_string(kSpBufs) + ")";
+    return GVS_ERR_BATCH_OVERFLOW;
+  }
   if (e & kKvErr) {
     h->err = "invalid op: block index >= capacity or unknown op code";
     return GVS_ERR_INVALID_ARG;
@@ -1644,13 +1649,14 @@ int gvs_create_sharded(const gvs_config* cfg, const uint8_t comm_id[GVS_COMM_ID_
 static int h2d(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes);
 static int d2h(gvs_handle* h, int slot, void* dst, const void* src, size_t bytes);
 static int bounce_done(gvs_handle* h, int rc);
+static int bounce_begin(gvs_handle* h);
 
 int gvs_process_batch(gvs_handle* h, const gvs_request* reqs, uint32_t n, gvs_response* out) {
   if (!h || (!reqs && n) || (!out && n) || n > max_submit(h)) return GVS_ERR_INVALID_ARG;
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
-  h->bounce.pend.clear();
+  if (int r = bounce_begin(h)) return r;
   if (int r = h2d(h, 0, h->in_stage, reqs, (size_t)n * sizeof(gvs_request))) return r;
   if (int r = run_batch(h, h->in_stage, n, h->out_stage)) return r;
   if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * sizeof(gvs_response))) return r;
@@ -1689,9 +1695,12 @@ static bool is_pinned(const void* p) {
   return at.type == hipMemoryTypeHost;
 }
 
-// wait for the copies of an earlier call that ended on an error path before a
-// slot is rewritten or freed
-static int bounce_quiesce(gvs_handle* h) {
+// at the entry of a call that uses the bounce slots: wait for the copies of an
+// earlier call that ended on an error path (its slots may still be read or
+// written by the stream) before any slot is rewritten or freed.  Within one
+// call every slot is used once, so a call's own copies never wait here.
+static int bounce_begin(gvs_handle* h) {
+  h->bounce.pend.clear();
   if (!h->bounce.inflight) return GVS_OK;
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   h->bounce.inflight = false;
@@ -1700,7 +1709,6 @@ static int bounce_quiesce(gvs_handle* h) {
 
 static int bounce_grow(gvs_handle* h, int slot, size_t bytes) {
   Bounce& b = h->bounce;
-  if (int r = bounce_quiesce(h)) return r;
   if (b.cap[slot] >= bytes) return GVS_OK;
   if (b.buf[slot]) GVS_HIP(h, hipHostFree(b.buf[slot]));
   b.buf[slot] = nullptr;
@@ -2114,7 +2122,7 @@ int gvs_process_wire_batch(gvs_handle* h, const uint8_t* in, uint32_t in_stride,
   GVS_HIP(h, hipSetDevice(h->device));
   if (int rc = wire_stage_init(h, true)) return rc;
   WireStage& w = h->wire;
-  h->bounce.pend.clear();
+  if (int r = bounce_begin(h)) return r;
   if (n) {
     if (int r = h2d(h, 0, w.in, in, (size_t)n * in_stride)) return r;
     if (int r = h2d(h, 1, w.in_lens, in_lens, (size_t)n * 4)) return r;
@@ -2320,7 +2328,7 @@ int gvs_sr25519_verify(gvs_handle* h, const uint8_t* pks, const uint8_t* msgs, u
     h->sr_cap = need;
   }
   uint8_t* d = h->sr_dev;
-  h->bounce.pend.clear();
+  if (int r = bounce_begin(h)) return r;
   if (int r = h2d(h, 0, d, pks, b_pk)) return r;
   if (int r = h2d(h, 1, d + b_pk, msgs, b_msg)) return r;
   if (int r = h2d(h, 2, d + b_pk + b_msg, sigs, b_sig)) return r;
@@ -2383,6 +2391,12 @@ int gvs_get_option(gvs_handle* h, const char* key, int64_t* value) {
   const Engine& e = h->eng[0];
   if (std::strcmp(key, "txn_slots") == 0) *value = e.c;
   else if (std::strcmp(key, "group_slots") == 0) *value = e.cm;
+  else if (std::strcmp(key, "fixed_schedule_pass") == 0)
+    // 1: the message-table pass stages every slot line in LDS and runs the same
+    // memory schedule whatever the batch holds (k_rpass2s, or k_spass<NW, true>
+    // sealed); 0: more transaction slots than LDS stages (c above kStageSlots /
+    // kSpSlots, i.e. B / W large), and the slot lines are read in the stream
+    *value = h->auth ? (sealed_staged(e) ? 1 : 0) : ((e.c <= kStageSlots && e.S % (16 * 8) == 0) ? 1 : 0);
   else if (std::strcmp(key, "rccl_ranks") == 0) {
     // the store's own communicator (0 without one): what the data path spans
     int n = 0;
@@ -2756,7 +2770,7 @@ int gvs_oram_access_batch(gvs_oram* o, const gvs_block_op* ops, uint32_t n, uint
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
-  h->bounce.pend.clear();
+  if (int r = bounce_begin(h)) return r;
   if (int r = h2d(h, 0, h->in_stage, ops, (size_t)n * sizeof(gvs_block_op))) return r;
   if (int r = oram_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
   if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * 1024)) return r;
@@ -2812,7 +2826,7 @@ int gvs_omap_access_batch(gvs_omap* o, const gvs_omap_op* ops, uint32_t n, gvs_o
   if (h->poisoned) return GVS_ERR_INTEGRITY;
   if (int r = check_epoch(h)) return r;
   GVS_HIP(h, hipSetDevice(h->device));
-  h->bounce.pend.clear();
+  if (int r = bounce_begin(h)) return r;
   if (int r = h2d(h, 0, h->in_stage, ops, (size_t)n * sizeof(gvs_omap_op))) return r;
   if (int r = omap_batch(h, h->eng[0], h->in_stage, n, h->out_stage)) return r;
   if (int r = d2h(h, 4, out, h->out_stage, (size_t)n * sizeof(gvs_omap_result))) return r;

@@ -57,6 +57,7 @@ constexpr uint32_t kSpSlots = 64;             // transaction slots per partition
 constexpr uint32_t kSpDry = kSpBufs;          // the dry buffer
 constexpr uint32_t kSpHoles = GVS_SP_DUAL ? 0 : 32;  // buffers living in the AES window's holes
 constexpr uint32_t kSpWords = kRowsMax / 32;  // bitmap words per partition
+constexpr uint32_t kJErr = 128u;  // error bit: k_sjoint, two batches' rows of a partition exceed kSpBufs
 
 // byte address (from the 64-KiB-aligned window at LDS 0) of 16-B block i of
 // 128-B piece q of staging buffer b.  Blocks are rotated by the piece inside
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(256) void k_sjoint(const uint4* tprev, const uint4*
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) n += (uint32_t)__shfl_xor((int)n, o);
-  if (lane == 0 && n > cap) atomicOr(&scal->error, kRErr);
+  if (lane == 0 && n > cap) atomicOr(&scal->error, kJErr);
 }
 
 }  // namespace gvs

@@ -74,7 +74,12 @@ extern "C" {
 #define GVS_ERR_DEVICE (-2)      /* HIP / RCCL failure; see gvs_last_error */
 #define GVS_ERR_OUT_OF_MEMORY (-3)
 #define GVS_ERR_BATCH_OVERFLOW (-4) /* a fixed per-partition bound of the batch
-                                       was exceeded; the batch was not applied */
+                                       was exceeded; the batch was not applied.
+                                       Sealed stores also bound the distinct rows
+                                       of a message partition over this and the
+                                       previous batch (86, the pass's LDS stages):
+                                       that overflow depends on the previous batch,
+                                       and the next batch may succeed */
 #define GVS_ERR_NO_DEVICE (-5)
 #define GVS_ERR_INTERNAL (-6)
 #define GVS_ERR_INTEGRITY (-7) /* authenticated storage: a stored row failed
@@ -363,7 +368,15 @@ int gvs_set_option(gvs_handle *h, const char *key, int64_t value);
 /* Read-only engine parameters of shard 0: "txn_slots" (transaction slots per
  * message partition, c), "group_slots" (recipient-group slots per mailbox
  * partition), "rccl_ranks" / "rccl_rank" (ncclCommCount / ncclCommUserRank of
- * the store's own RCCL communicator; 0 / -1 when the store has none). */
+ * the store's own RCCL communicator; 0 / -1 when the store has none),
+ * "fixed_schedule_pass" (1 when the message-table pass stages every
+ * transaction slot's line in LDS, so that its memory schedule is the same
+ * whatever the batch holds; 0 when the store has more slots per partition
+ * than the stages: c = B/W + 8 sqrt(B/W) + 16 rounded up to 8, W = N / rows
+ * per partition, above 64, or a plain store whose partition rows are not a
+ * multiple of 128; e.g. B = 131072 over 4096
+ * partitions; the slot lines are then read inside the row stream, whose
+ * traffic follows which rows the batch touches). */
 int gvs_get_option(gvs_handle *h, const char *key, int64_t *value);
 
 /* Enable (on != 0) per-stage HIP-event timing of subsequent batches. */

@@ -74,3 +74,23 @@ def test_invalid_sharded_configs_rejected_before_device_use():
     assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
     bad = abi.make_config(4096, max_batch=1024, rows_per_partition=100)
     assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
+
+
+def test_sealed_mailbox_partition_limit():
+    """Sealed stores keep a mailbox partition's per-row values in the AES
+    window's holes (gvs_mauth.h kSrAuth): more than 256 rows per partition is
+    refused at create, before any device use; 256 passes validation (on a box
+    without a GPU it then fails with GVS_ERR_NO_DEVICE)."""
+    lib = load_library()
+    h = ctypes.c_void_p()
+    bad = abi.make_config(65536, mailbox_partitions=16, mailbox_partition_slots=512, max_batch=1024,
+                          auth_storage=True)
+    assert lib.gvs_create(ctypes.byref(bad), ctypes.byref(h)) == abi.GVS_ERR_INVALID_ARG
+    plain = abi.make_config(65536, mailbox_partitions=16, mailbox_partition_slots=512, max_batch=1024)
+    ok = abi.make_config(65536, mailbox_partitions=16, mailbox_partition_slots=256, max_batch=1024,
+                         auth_storage=True)
+    for cfg in (plain, ok):
+        rc = lib.gvs_create(ctypes.byref(cfg), ctypes.byref(h))
+        assert rc in (0, abi.GVS_ERR_NO_DEVICE), rc
+        if rc == 0:
+            lib.gvs_destroy(h)

@@ -282,3 +282,69 @@ def test_replayed_pending_state_is_detected():
     with pytest.raises(GvsError) as ei:
         run_one(store, model, params)
     assert ei.value.code == abi.ERR_INTEGRITY
+
+
+def test_joint_slot_overflow_over_two_batches():
+    """the sealed pass stages the previous batch's and this
+    batch's rows of a partition in the same 86 LDS buffers (gvs_spass.h), so
+    k_sjoint fails a batch whose rows plus the previous batch's rows in one
+    partition exceed them, even when the batch fits its own c slots.  Two
+    batches of 45 by-id reads in one partition (c = 64 here: 4096-request
+    batches over 256 partitions): the first is applied, the second fails with
+    GVS_ERR_BATCH_OVERFLOW and its own message before anything changes, and a
+    smaller batch after it (45 + 10 rows) is applied bit-exact with the oracle,
+    which never saw the failed batch; so is a random batch after that."""
+    store, model = make_pair(n_msgs=65536, Q=64, Sr=64, B=4096, rpp=256)
+    assert store.get_option("txn_slots") == 64 and store.get_option("fixed_schedule_pass") == 1
+    W = store.stats()["msg_partitions"]
+    model.seed(5)
+    fill = ffi.gen_params(create=100, read=0, update=0, delete=0, n_identities=1000)
+    live = []
+    for _ in range(7):
+        reqs = model.gen_batch(4096, fill)
+        got, want = store.process_batch(reqs), model.process_batch(reqs)
+        assert got.tobytes() == want.tobytes()
+        for r, o in zip(reqs, got):
+            if o["status_code"] == 1:
+                live.append((bytes(o["record"]["msg_id"]), r["auth_identity"].copy()))
+    part = {}
+    for mid, who in live:
+        slot, _ = ffi.id_decode(SECRET[:16], mid, 65536)
+        part.setdefault(slot % W, []).append((mid, who))
+    q, msgs = max(part.items(), key=lambda kv: len(kv[1]))
+    assert len(msgs) >= 100, len(msgs)
+
+    def reads(sel):
+        reqs = np.zeros(len(sel), dtype=abi.REQUEST_DTYPE)
+        for i, (mid, who) in enumerate(sel):
+            reqs[i]["request_type"] = 2
+            reqs[i]["msg_id"] = np.frombuffer(mid, np.uint8)
+            reqs[i]["auth_identity"] = who
+            reqs[i]["timestamp"] = 1_800_000_000 + i
+        return reqs
+
+    a, b, c = reads(msgs[:45]), reads(msgs[45:90]), reads(msgs[90:100])
+    got, want = store.process_batch(a), model.process_batch(a)
+    assert got.tobytes() == want.tobytes() and (got["status_code"] == 1).all()
+    before = store.stats()["messages"]
+    with pytest.raises(GvsError) as ei:
+        store.process_batch(b)
+    assert ei.value.code == abi.GVS_ERR_BATCH_OVERFLOW and "previous batch" in str(ei.value), str(ei.value)
+    assert store.stats()["messages"] == before
+    got, want = store.process_batch(c), model.process_batch(c)
+    assert got.tobytes() == want.tobytes() and (got["status_code"] == 1).all()
+    got, want = run_one(store, model, ffi.gen_params(n_identities=1000), n=4096)
+    assert got.tobytes() == want.tobytes()
+
+
+def test_fixed_schedule_pass_option():
+    """gvs_get_option("fixed_schedule_pass"): 1 where the message pass stages
+    every slot line in LDS (c <= 64), 0 past that: B = 16384
+    over 256 partitions gives c = 64 + 8 * 8 + 16 = 144."""
+    for auth in (False, True):
+        for B, want in ((1024, 1), (16384, 0)):
+            cfg = abi.make_config(65536, mailbox_partitions=16, mailbox_partition_slots=32, max_batch=B,
+                                  secret_key=SECRET, auth_storage=auth, rows_per_partition=256)
+            st = ObliviousStore(cfg)
+            assert st.get_option("fixed_schedule_pass") == want, (auth, B, st.get_option("txn_slots"))
+            st.close()
