@@ -114,26 +114,34 @@ def test_timing_slow_reference_process_widens_the_noise():
     assert not res["bad"], res["bad"]
 
 
-def _interleaved(bump=None, sigma=3.0, offsets=(0.0, 40.0)):
+def _interleaved(bump=None, sigma=3.0, offsets=(0.0, 40.0), drift=0.0):
+    """Processes of interleaved mixes: {mix: [(block, batch)]}, 3 blocks of 2
+    batches per mix; a process offset and a drift per block on the pass."""
     mixes = ["rud", "main", "hot_next", "deletes"]
     procs = []
     for p, off in enumerate(offsets):
         r = random.Random(100 + p)
-        procs.append({m: [[(k, v + (off if v > 100 else 0.0) + r.gauss(0, sigma if v > 100 else 0.05)
-                            + (bump or {}).get((m, j, idx), 0.0)) for idx, (k, v) in enumerate(KERNELS)]
-                          for j in range(tt.N_MEAS)] for m in mixes})
+        per = {m: [] for m in mixes}
+        for blk in range(3):
+            for m in mixes:
+                for j in range(2):
+                    per[m].append((blk, [(k, v + (off + drift * blk if v > 100 else 0.0)
+                                          + r.gauss(0, sigma if v > 100 else 0.05)
+                                          + (bump or {}).get((m, 2 * blk + j, idx), 0.0))
+                                         for idx, (k, v) in enumerate(KERNELS)]))
+        procs.append(per)
     return procs
 
 
-def test_interleaved_process_offset_cancels():
-    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(), "rud")
+def test_interleaved_process_offset_and_drift_cancel():
+    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(drift=30.0), "rud")
     assert not bad, bad
-    assert mdb["2:k_pass"] < 12.0, mdb  # 40-us process offset, 3-us batch noise
+    assert mdb["2:k_pass"] < 12.0, mdb  # 40-us process offset, 30-us drift, 3-us batch noise
 
 
 def test_interleaved_small_leak_in_the_pass_is_seen():
-    leak = {("hot_next", j, 2): 12.0 for j in range(tt.N_MEAS)}
-    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(leak), "rud")
+    leak = {("hot_next", j, 2): 12.0 for j in range(6)}
+    lines, bad, mdb = tt.evaluate_interleaved(_interleaved(leak, drift=30.0), "rud")
     assert [(v[0], v[1]) for v in bad] == [("k_pass", "hot_next")], bad
 
 

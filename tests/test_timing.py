@@ -38,13 +38,15 @@ table pass (tens of microseconds between two processes of identical inputs)
 limits what a comparison between processes can see.  The headline and sealed
 shapes therefore also run every mix interleaved in one process (the probe's
 'a+b+...' schedule: per seed, the mixes in a rotated order, the generator
-reseeded before each), in two processes with different rotations.  Per kernel
-the bias of a mix is the mean over processes of (mix mean - reference mean)
-in that process, against 5 standard errors from the pooled within-process
-sigma + 2 us.  Each (process, mix) group drops its single most extreme batch
-(the same rule for every mix, the reference included), so one stalled batch
-cannot decide the result; a leak in every batch of a mix cannot hide.  The
-report gives every kernel's minimal detectable bias (the bound).
+reseeded before each), in processes with different rotations (INTERLEAVED).
+Per kernel a two-way model, duration = block level + mix effect + noise (a
+block is one seed's run of every mix), takes a drift of the process out of
+the noise; a mix's bias is its mean within-block difference from the
+reference, against 5 standard errors from the model's residual sigma + 2 us.
+Each (process, mix) group drops its single most extreme batch (the same rule
+for every mix, the reference included), so one stalled batch cannot decide
+the result; a leak in every batch of a mix cannot hide.  The report gives
+every kernel's minimal detectable bias (the bound).
 
 Shapes: the store under seven mixes, including adversarial ones (every request
 aimed at one recipient, every read missing, only deletes); the expiry sweep
@@ -90,8 +92,10 @@ N_MEAS = len(SEEDS) * PER_SEED
 FLOOR_US = 2.0       # trace-clock jitter floor, per batch and for the bias
 BIAS_SIGMAS = 5.0
 MAX_RERUNS = 2       # fresh processes per shape
-# in-process comparison: processes and their rotations of the mix order
-INTERLEAVED_ROTATIONS = (0, 3)
+# in-process comparison, per shape: the processes' rotations of the mix order
+# and the batches per mix and seed (the sealed pass, ~11.5 ms and VALU-bound,
+# varies more from batch to batch: more batches for the same bound)
+INTERLEAVED = {"store": ((0, 3), 2), "auth": ((0, 2, 4, 6), 3)}
 
 
 def load_probe():
@@ -256,35 +260,51 @@ def check_durations(shape, tmp_path):
 
 
 def evaluate_interleaved(procs, ref_mix):
-    """The in-process comparison on [{mix: [per-batch lists of (kernel, us)]}]
-    (one dict per process, the measured batches of each mix in run order).
-    Returns (report rows, violations, {kernel: minimal detectable bias})."""
+    """The in-process comparison on [{mix: [(block, per-batch list of (kernel,
+    us))]}] (one dict per process; a block is one seed's run of every mix,
+    back to back).  A two-way model per kernel: duration = block level + mix
+    effect + noise, so that a slow drift of the process (clocks, heat) is a
+    block level and not noise.  Each (process, mix) group first drops its
+    single most extreme batch (the same rule for every mix).  The mix effect
+    against the reference is the mean over blocks of the within-block
+    difference of the two mixes' means; its bound is 5 standard errors from
+    the model's residual sigma + 2 us.  Returns (report rows, violations,
+    {kernel: minimal detectable bias})."""
     mixes = list(procs[0])
-    kernels = [k for k, _ in procs[0][ref_mix][0]]
+    kernels = [k for k, _ in procs[0][ref_mix][0][1]]
     lines, bad, mdb = [], [], {}
     for idx, k in enumerate(kernels):
-        groups = {}  # (process, mix) -> kept values (the most extreme batch dropped)
+        cells = {}  # (process, block, mix) -> kept values
         for p, per in enumerate(procs):
             for m in mixes:
-                vals = [b[idx][1] for b in per[m]]
-                assert all(b[idx][0] == k for b in per[m]), f"{m}: kernel sequence differs"
-                med = statistics.median(vals)
-                drop = max(range(len(vals)), key=lambda i: abs(vals[i] - med))
-                groups[(p, m)] = [v for i, v in enumerate(vals) if i != drop]
-        ss, dof = 0.0, 0
-        for v in groups.values():
-            mu = statistics.fmean(v)
-            ss += sum((x - mu) ** 2 for x in v)
-            dof += len(v) - 1
-        sigma = math.sqrt(ss / dof) if dof else 0.0
-        n_ref = sum(len(groups[(p, ref_mix)]) for p in range(len(procs)))
-        ref_mu = statistics.fmean(x for p in range(len(procs)) for x in groups[(p, ref_mix)])
-        row = [f"{k[:30]:30s} ref={ref_mu:10.1f}us sigma_w={sigma:6.2f}"]
+                vals = [(blk, b[idx][1]) for blk, b in per[m]]
+                assert all(b[idx][0] == k for _, b in per[m]), f"{m}: kernel sequence differs"
+                med = statistics.median(v for _, v in vals)
+                drop = max(range(len(vals)), key=lambda i: abs(vals[i][1] - med))
+                for i, (blk, v) in enumerate(vals):
+                    if i != drop:
+                        cells.setdefault((p, blk, m), []).append(v)
+        blocks = sorted({(p, blk) for p, blk, _ in cells})
+        cm = {c: statistics.fmean(v) for c, v in cells.items()}
+        # block levels (mean of the block's cell means) and mix effects
+        lvl = {pb: statistics.fmean(cm[c] for c in cm if c[:2] == pb) for pb in blocks}
+        eff = {m: statistics.fmean(cm[c] - lvl[c[:2]] for c in cm if c[2] == m) for m in mixes}
+        ss, n = 0.0, 0
+        for c, v in cells.items():
+            for x in v:
+                ss += (x - lvl[c[:2]] - eff[c[2]]) ** 2
+                n += 1
+        dof = n - len(blocks) - (len(mixes) - 1)
+        sigma = math.sqrt(ss / dof) if dof > 0 else 0.0
+        n_ref = sum(len(v) for c, v in cells.items() if c[2] == ref_mix)
+        row = [f"{k[:30]:30s} ref={statistics.fmean(x for c, v in cells.items() if c[2] == ref_mix for x in v):10.1f}us "
+               f"sigma={sigma:6.2f}"]
         worst = 0.0
         for m in mixes:
-            n_m = sum(len(groups[(p, m)]) for p in range(len(procs)))
-            bias = statistics.fmean(statistics.fmean(groups[(p, m)]) - statistics.fmean(groups[(p, ref_mix)])
-                                    for p in range(len(procs)))
+            diffs = [cm[(p, blk, m)] - cm[(p, blk, ref_mix)] for p, blk in blocks
+                     if (p, blk, m) in cm and (p, blk, ref_mix) in cm]
+            bias = statistics.fmean(diffs)
+            n_m = sum(len(v) for c, v in cells.items() if c[2] == m)
             btol = BIAS_SIGMAS * sigma * math.sqrt(1.0 / n_m + 1.0 / n_ref) + FLOOR_US
             worst = max(worst, btol)
             row.append(f"{m}:{bias:+.1f}")
@@ -298,21 +318,23 @@ def evaluate_interleaved(procs, ref_mix):
 
 def check_interleaved(shape, tmp_path):
     sh = SHAPES[shape]
+    rotations, per_seed = INTERLEAVED[shape]
     probe = load_probe()
     joined = "+".join(sh["mixes"])
     procs = []
-    for r in INTERLEAVED_ROTATIONS:
+    for r in rotations:
         d = str(tmp_path / f"{shape}_interleaved_r{r}")
-        bs = batches_of(joined, d, sh["args"] + ["--rotate", str(r)])
-        sched = probe.schedule(joined, list(SEEDS), PER_SEED, r)
+        bs = batches_of(joined, d, sh["args"] + ["--rotate", str(r), "--batches", str(per_seed)])
+        sched = probe.schedule(joined, list(SEEDS), per_seed, r)
         meas = bs[-len(sched):]
         per = {m: [] for m in sh["mixes"]}
-        for (m, *_), b in zip(sched, meas):
-            per[m].append(b)
+        for (m, sd, *_), b in zip(sched, meas):
+            per[m].append((SEEDS.index(sd), b))
         procs.append(per)
     lines, bad, mdb = evaluate_interleaved(procs, sh["ref"])
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"timing_c3_{shape}_interleaved.txt"), "w") as f:
+        f.write(f"processes (mix-order rotations): {list(rotations)}, {per_seed} batches per mix and seed\n")
         f.write("\n".join(lines) + "\n")
         f.write(f"minimal detectable bias per kernel (us): {mdb}\n")
         f.write(f"violations: {bad}\n")
