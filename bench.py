@@ -344,6 +344,7 @@ def front_end(torch, store, dev, batches, nreq, B):
         d_times.append(torch.from_numpy(q["timestamp"].view(np.int64)).to(dev))
     d_out = torch.empty((nreq, wire.RESPONSE_WIRE_BYTES), dtype=torch.uint8, device=dev)
     d_olen = torch.empty((nreq,), dtype=torch.int32, device=dev)
+    store.synchronize()
     torch.cuda.synchronize(dev)
     stage, lens = {}, None
     t0 = time.perf_counter()
@@ -353,6 +354,7 @@ def front_end(torch, store, dev, batches, nreq, B):
             None, d_out.data_ptr(), wire.RESPONSE_WIRE_BYTES, d_olen.data_ptr(), None, None))
         for k, v in store.last_timings().items():
             stage[k] = stage.get(k, 0.0) + v
+    store.synchronize()
     torch.cuda.synchronize(dev)
     t = time.perf_counter() - t0
     lens = torch.bincount(d_olen.to(torch.int64), minlength=1043)
@@ -369,6 +371,7 @@ def front_end(torch, store, dev, batches, nreq, B):
             d_chal.data_ptr(), d_out.data_ptr(), wire.RESPONSE_WIRE_BYTES, d_olen.data_ptr(), None, None))
         for k, v in store.last_timings().items():
             stage_c[k] = stage_c.get(k, 0.0) + v
+    store.synchronize()
     torch.cuda.synchronize(dev)
     t_c = time.perf_counter() - t0
     # the same requests from host memory, all batches in one double-buffered
@@ -390,11 +393,14 @@ def front_end(torch, store, dev, batches, nreq, B):
             h_times.ctypes.data, None if chal is None else chal.ctypes.data, h_out.ctypes.data,
             wire.RESPONSE_WIRE_BYTES, h_olen.ctypes.data, None, ctypes.byref(applied)))
     host_call(1, h_chal)  # first use allocates the pipeline's buffers (and loads the verifier)
+    store.synchronize()
     t0 = time.perf_counter()
     host_call(len(batches))
+    store.synchronize()  # the last batch's deferred mailbox write pass, in the timed region
     t_h = time.perf_counter() - t0
     t0 = time.perf_counter()
     host_call(len(batches), h_chal)
+    store.synchronize()
     t_hc = time.perf_counter() - t0
     # the same with the slabs in pinned memory (copied without staging)
     p_in = store.host_array(h_in.size, np.uint8).reshape(h_in.shape)
@@ -402,8 +408,10 @@ def front_end(torch, store, dev, batches, nreq, B):
     p_in[:] = h_in
     h_in, h_out = p_in, p_out
     host_call(1)
+    store.synchronize()
     t0 = time.perf_counter()
     host_call(len(batches))
+    store.synchronize()
     t_hp = time.perf_counter() - t0
     # batched signature check over B random (pk, 32-B challenge, signature)
     g = torch.Generator(device=dev)
@@ -584,6 +592,9 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     store.process_batches_device(timed_in.data_ptr(), [nreq] * a.steps, timed_out.data_ptr())
+    # the last batch's deferred mailbox write pass (gvs_synchronize): the timed
+    # region holds exactly the K batches' work (stats() above ran the warm-up's)
+    store.synchronize()
     torch.cuda.synchronize(dev)
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
@@ -607,11 +618,13 @@ def main():
 
     # for comparison: one gvs_process_batch_device call per batch (each call
     # waits for its batch's verdict before the next is enqueued)
+    store.synchronize()
     gdist.barrier(ri)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for x in one_by_one:
         store.process_batch_device(x.data_ptr(), nreq, d_out.data_ptr())
+    store.synchronize()
     torch.cuda.synchronize(dev)
     t_obo = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
     per_batch_api = {"value": world * nreq * a.steps / t_obo, "unit": "req/s",
@@ -636,17 +649,20 @@ def main():
         warm = np.ones(nreq, dtype=abi.RESPONSE_DTYPE)  # first call pins its staging buffers
         store._check(store.lib.gvs_process_batches(store.h, hb[-1].ctypes.data, counts.ctypes.data, 1,
                                                    warm.ctypes.data, ctypes.byref(applied)))
+        store.synchronize()
         gdist.barrier(ri)
         t0 = time.perf_counter()
         store._check(store.lib.gvs_process_batches(store.h, reqs_all.ctypes.data, counts.ctypes.data,
                                                    a.host_steps, out_all.ctypes.data,
                                                    ctypes.byref(applied)))
+        store.synchronize()
         t_pipe = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
         one = [np.ones(nreq, dtype=abi.RESPONSE_DTYPE) for _ in hb[a.host_steps:-1]]
         gdist.barrier(ri)
         t0 = time.perf_counter()
         for x, o in zip(hb[a.host_steps:-1], one):
             store._check(store.lib.gvs_process_batch(store.h, x.ctypes.data, nreq, o.ctypes.data))
+        store.synchronize()
         t_seq = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
         # the same batches from caller buffers in pinned memory (gvs_host_alloc):
         # copied to and from the device directly, no staging
@@ -654,11 +670,13 @@ def main():
         pin_out = store.host_array(len(reqs_all), abi.RESPONSE_DTYPE)
         pin_in[:] = reqs_all
         pin_out[:] = out_all
+        store.synchronize()
         gdist.barrier(ri)
         t0 = time.perf_counter()
         store._check(store.lib.gvs_process_batches(store.h, pin_in.ctypes.data, counts.ctypes.data,
                                                    a.host_steps, pin_out.ctypes.data,
                                                    ctypes.byref(applied)))
+        store.synchronize()
         t_pin = gdist.max_over_ranks(ri, time.perf_counter() - t0, device=dev)
         host_path = {"value": world * nreq * a.host_steps / t_pipe, "unit": "req/s",
                      "batches": a.host_steps, "ms_per_batch": t_pipe / a.host_steps * 1e3,

@@ -134,7 +134,16 @@ struct Engine {
   // fixed-slot mailbox passes (gvs_mtx.h)
   uint32_t cm = 0;           // group slots per mailbox partition
   uint4* mpos = nullptr;     // B
-  uint4* gtx = nullptr;      // (Q*cm + B) x 128 B
+  uint4* gtx = nullptr;      // (Q*cm + B) x 128 B: this batch's (one of gtxb)
+  uint4* gtxb[2] = {};       // ping-pong: a deferred write pass reads the previous batch's
+  uint32_t gsel = 0;
+  // Deferred mailbox write pass (plain single-GPU stores): a batch's k_m2x
+  // runs fused with the next batch's read pass (k_m21x), or alone when the
+  // table is needed first (flush_m2).  gscal->error: the next batch's
+  // group-slot overflow while the write pass is still to run.
+  bool m2_pending = false;
+  MArgs m2_args{};
+  Scal* gscal = nullptr;
   uint4* msnap = nullptr;    // Q*cm x 1 KiB
   uint4* msnapp = nullptr;   // B x 1 KiB (group snapshots by head position)
   uint4* mpid = nullptr;     // B x 16 B: each sorted position's message id (k_gtx, for k_m1r_c)
@@ -607,7 +616,10 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
     A(vcarry2, nvb2 * kVLineU4);
     const uint64_t QC = (uint64_t)e.Q * e.cm;
     A(mpos, B);
-    A(gtx, (QC + B) * 8);
+    A(gtxb[0], (QC + B) * 8);
+    A(gtxb[1], (QC + B) * 8);
+    e.gtx = e.gtxb[0];
+    A(gscal, 1);
     A(msnap, QC * 64);
     A(msnapp, (uint64_t)B * 64);
     A(mpid, B);
@@ -623,7 +635,8 @@ static int engine_init(gvs_handle* h, Engine& e, uint32_t shard, uint32_t B) {
   GVS_HIP(h, hipMemsetAsync(e.table, 0, e.N * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.mbox, 0, e.R * 1024, s));
   GVS_HIP(h, hipMemsetAsync(e.side, 0, e.R * 16, s));
-  GVS_HIP(h, hipMemsetAsync(e.gtx, 0, ((uint64_t)e.Q * e.cm + B) * 128, s));
+  for (int k = 0; k < 2; ++k) GVS_HIP(h, hipMemsetAsync(e.gtxb[k], 0, ((uint64_t)e.Q * e.cm + B) * 128, s));
+  GVS_HIP(h, hipMemsetAsync(e.gscal, 0, sizeof(Scal), s));
   GVS_HIP(h, hipMemsetAsync(e.rkeys, 0xFF, (uint64_t)B * 8, s));  // null rows until written
   for (int k = 0; k < 2; ++k) {
     GVS_HIP(h, hipMemsetAsync(e.tbuf[k], 0, ((uint64_t)e.W * e.c + B) * 128, s));
@@ -909,6 +922,11 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   e.stamp_run = e.stamp_next++;
   if (e.stamp_next == kNone) e.stamp_next = 1;
   const uint32_t xbase = B - e.X;
+  // this batch's group descriptors; a deferred write pass of the previous
+  // batch still reads the other buffer
+  e.gtx = e.gtxb[e.gsel];
+  e.gsel ^= 1u;
+  const bool fuse = e.m2_pending;
   hipLaunchKernelGGL(k_copy, dim3(B / (4 * kCopyPerWave)), dim3(256), 0, s, d_in, stride, n, B, e.img, e.types,
                      (const uint4*)(e.X ? e.xb2[e.par ^ 1] : nullptr), xbase);
   mark(h, "copy");
@@ -922,7 +940,7 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
   if (int r = sort_keys<Key128, 1>(h, e.s1keys, B)) return r;
   mark(h, "sort_s1");
   {
-    GtxArgs a{e.s1keys, e.ops, e.mpos, e.gtx, e.gtx_agg, e.gtx_carry, e.scal,
+    GtxArgs a{e.s1keys, e.ops, e.mpos, e.gtx, e.gtx_agg, e.gtx_carry, fuse ? e.gscal : e.scal,
               B,        e.Q,   e.logQ, e.cm,  B / kScanT, e.stamp_run};
     a.mpid = e.mpid;
     hipLaunchKernelGGL(k_scan_a<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
@@ -930,10 +948,21 @@ static int phase_a2(gvs_handle* h, Engine& e, const uint4* d_in, uint32_t stride
     hipLaunchKernelGGL(k_scan_c<GtxOp>, dim3(B / kScanT), dim3(kScanT), 0, s, a);
   }
   mark(h, "gtx");
-  if (h->auth)
+  if (h->auth) {
     hipLaunchKernelGGL(k_m1a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + GVS_MA_EXTRA_LDS, s, margs2(h, e));
-  else
+  } else if (fuse) {
+    // the previous batch's write pass and this batch's read pass in one
+    // stream over the mailbox table; then this batch's group-slot overflow
+    // (held apart so that it could not stop the previous batch's write)
+    // joins its error word
+    M21Args fa{e.m2_args, margs2(h, e), &e.gscal->error};
+    hipLaunchKernelGGL(k_m21x, dim3(e.Q), dim3(256), e.Sr * sizeof(uint4) + 2 * (e.cm + 1) * sizeof(GroupM), s,
+                       fa);
+    hipLaunchKernelGGL(k_err_fold, dim3(1), dim3(64), 0, s, e.scal, &e.gscal->error);
+    e.m2_pending = false;
+  } else {
     hipLaunchKernelGGL(k_m1x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM), s, margs2(h, e));
+  }
   {
     M1rArgs a{};
     vscan_fields(a, e);
@@ -1028,6 +1057,11 @@ static void launch_rpass2(gvs_handle* h, Engine& e) {
   }
 }
 
+// The plain single-GPU message store defers each batch's mailbox write pass
+// (DESIGN.md §3 "Fused mailbox passes"); sealed stores (k_m2a) and sharded
+// stores run it at the end of the batch.
+static bool defer_m2(const gvs_handle* h) { return h->mode == kSingle && !h->auth && h->kind == 0; }
+
 static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   hipStream_t s = h->stream;
   const uint32_t B = e.B, nblk = e.nblk;
@@ -1089,6 +1123,8 @@ static int phase_b2(gvs_handle* h, Engine& e, uint32_t n, uint4* d_out) {
   mark(h, "m2r");
   if (h->auth)
     hipLaunchKernelGGL(k_m2a, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + GVS_MA_EXTRA_LDS, s, margs2(h, e));
+  else if (defer_m2(h))  // runs with the next batch's read pass (k_m21x) or alone in flush_m2
+    e.m2_pending = true, e.m2_args = margs2(h, e);
   else
     hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + e.Sr * sizeof(uint4), s,
                        margs2(h, e));
@@ -1243,6 +1279,10 @@ static int run_batch_body(gvs_handle* h, const uint4* d_in, uint32_t n, uint4* d
 // The status of a batch from its (agreed) error word; records the handle's
 // state (poisoned, message).  0: applied.
 static int decode_error(gvs_handle* h, uint32_t e) {
+  // a failed batch leaves no write pass behind: the one it inherited ran in
+  // its k_m21x (the error word was clear then), its own is not to run
+  if (e)
+    for (auto& en : h->eng) en.m2_pending = false;
   if (e & 8u) {
     h->poisoned = true;
     h->err = "integrity failure: a stored row does not match its tag (authenticated storage)";
@@ -1319,6 +1359,28 @@ static int finish(gvs_handle* h) {
   if (int r = decode_error(h, *h->err_pin)) return r;
   advance(h);
   return GVS_OK;
+}
+
+// Run a deferred mailbox write pass on its own (k_m2x), before anything reads
+// the mailbox table or its counters from the host: stats, the raw-region
+// hooks.  Its only late flag is the write pass's own consistency check (error
+// bit 2: the handle is poisoned).
+static int flush_m2(gvs_handle* h) {
+  bool any = false;
+  for (auto& e : h->eng) {
+    if (!e.m2_pending) continue;
+    hipLaunchKernelGGL(k_m2x<false>, dim3(e.Q), dim3(256), (e.cm + 1) * sizeof(GroupM) + e.Sr * sizeof(uint4),
+                       h->stream, e.m2_args);
+    e.m2_pending = false;
+    any = true;
+  }
+  if (!any) return GVS_OK;
+  GVS_HIP(h, hipGetLastError());
+  if (!h->err_pin) GVS_HIP(h, hipHostMalloc((void**)&h->err_pin, sizeof(uint32_t), hipHostMallocDefault));
+  GVS_HIP(h, hipMemcpyAsync(h->err_pin, &h->eng[0].scal->error, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            h->stream));
+  GVS_HIP(h, hipStreamSynchronize(h->stream));
+  return decode_error(h, *h->err_pin);
 }
 
 static int check_epoch(gvs_handle* h) {
@@ -2353,6 +2415,7 @@ int gvs_access(gvs_handle* h, const gvs_request* req, gvs_response* out) {
 
 int gvs_get_stats(gvs_handle* h, gvs_stats* out) {
   if (!h || !out) return GVS_ERR_INVALID_ARG;
+  if (int r = flush_m2(h)) return r;
   std::memset(out, 0, sizeof *out);
   for (auto& e : h->eng) {
     Scal sc{};
@@ -2376,6 +2439,7 @@ int gvs_get_stats(gvs_handle* h, gvs_stats* out) {
 
 int gvs_synchronize(gvs_handle* h) {
   if (!h) return GVS_ERR_INVALID_ARG;
+  if (int r = flush_m2(h)) return r;
   GVS_HIP(h, hipStreamSynchronize(h->stream));
   return GVS_OK;
 }
@@ -2580,6 +2644,7 @@ static int tiles_in(gvs_handle* h, const void* base, uint32_t tr, uint64_t t0, u
 int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset, void* dst,
                  uint64_t bytes) {
   if (!h || !dst) return GVS_ERR_INVALID_ARG;
+  if (int r = flush_m2(h)) return r;
   void* base;
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;
@@ -2599,6 +2664,7 @@ int gvs_dump_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset
 int gvs_store_raw(gvs_handle* h, uint32_t shard, uint32_t region, uint64_t offset,
                   const void* src, uint64_t bytes) {
   if (!h || !src) return GVS_ERR_INVALID_ARG;
+  if (int r = flush_m2(h)) return r;
   void* base;
   uint64_t size;
   if (int r = raw_region(h, shard, region, &base, &size)) return r;

@@ -215,12 +215,14 @@ __device__ inline int find_group_m(const GroupM* g, uint32_t ng, uint32_t cm, ui
 // occupied rows of the partition -> groups, every side entry read; s_keep
 // (LDS, or null) keeps the entries as read, so that a later use does not read
 // them again (sealed stores: ma_prepass, gvs_mauth.h)
+// (s_src, LDS: the partition's side entries as an earlier stage left them,
+// read instead of HBM; k_m21x)
 __device__ inline void side_prepass_m(const MArgs& a, uint32_t q, GroupM* g, uint32_t ng,
                                       int16_t* s_sg, uint8_t* s_occb, uint32_t* s_occ,
-                                      uint4* s_keep = nullptr) {
+                                      uint4* s_keep = nullptr, const uint4* s_src = nullptr) {
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
     const uint64_t row = (uint64_t)q * a.Sr + j;
-    uint4 sd = a.side[row];
+    uint4 sd = s_src ? s_src[j] : a.side[row];
     if (s_keep) s_keep[j] = sd;
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
@@ -890,6 +892,279 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
   // every workgroup adds, zero included: a fixed set of atomics
   if (tid == 0)
     atomicAdd((unsigned long long*)&a.scal->n_mailboxes, (unsigned long long)(int64_t)(int32_t)s_delta);
+}
+
+// ------------------------------------------------------------- k_m21x
+//
+// The write pass of batch t and the read pass of batch t + 1 in one stream
+// over the mailbox table (DESIGN.md §3 "Fused mailbox passes"): every row is
+// read once, rewritten with batch t's results, stored, and then snapshotted
+// for batch t + 1's groups, which saves k_m1x's 1-GiB read per batch.  The
+// work per partition is exactly k_m2x's followed by k_m1x's, on the same
+// fixed schedule (every row read and written once, T slot iterations per
+// wave for each pass, one 1-KiB line per iteration).  Batch t + 1's read
+// prologue needs the side entries after batch t: they follow from batch t's
+// prologue (a touched row takes its group's key and final length, a row whose
+// group ends empty is cleared), computed for every row into the side array in
+// LDS before the stream; the stream stores the same values.
+//
+// w: batch t's write-pass arguments (its group descriptors and results),
+// r: batch t + 1's read-pass arguments.  gerr: batch t + 1's group-slot
+// overflow flag (its k_gtx scan runs before this kernel and must not stop
+// batch t's write pass, whose status was already decided); the read pass of
+// a failed batch t + 1 is skipped (its snapshots are never used).
+struct M21Args {
+  MArgs w, r;
+  const uint32_t* gerr;
+};
+
+__global__ __launch_bounds__(256) void k_m21x(M21Args A) {
+  const MArgs& a = A.w;
+  const MArgs& b = A.r;
+  extern __shared__ uint4 s_dyn[];
+  uint4* s_side = s_dyn;                                           // Sr
+  GroupM* g = reinterpret_cast<GroupM*>(s_dyn + a.Sr);             // cm + 1: batch t
+  GroupM* g1 = g + a.cm + 1;                                       // cm + 1: batch t + 1
+  __shared__ int16_t s_sg[kSrMax];
+  __shared__ uint8_t s_occb[kSrMax];
+  __shared__ uint4 s_wst[4][64];
+  __shared__ int16_t s_place[kSrMax];
+  __shared__ uint8_t s_flag[kSrMax];
+  __shared__ uint16_t s_pfx[kSrMax + 1];
+  __shared__ uint16_t s_gpfx[kGroupMax + 1];
+  __shared__ uint8_t s_gflag[kGroupMax + 1];
+  __shared__ int16_t s_pend[kGroupMax + 1];
+  __shared__ uint8_t s_ld[kGroupMax + 1];
+  __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta, s_tw[kRowWaves];
+  // batch t + 1's read pass
+  __shared__ int16_t s_sg1[kSrMax];
+  __shared__ uint8_t s_occb1[kSrMax];
+  __shared__ uint32_t s_ng1, s_occ1, s_empt1, s_tw1[kRowWaves];
+  __shared__ uint8_t s_tf1[kGroupMax];
+  __shared__ uint16_t s_tp1[kGroupMax + 1];
+  __shared__ int16_t s_tl1[kGroupMax];
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t q = blockIdx.x;
+  if (a.scal->error) return;  // batch t failed (multi-batch calls): neither pass runs
+  const bool rd = *A.gerr == 0u;  // uniform: batch t + 1's read pass runs
+  uint4* part = a.mbox + (uint64_t)q * a.Sr * 64;
+  uint4* side = a.side + (uint64_t)q * a.Sr;
+  uint4 va[kMU], vb[kMU];
+  load_rows(va, part, wave * kMU, a.Sr);
+  // ---- batch t's write prologue (k_m2x)
+  const uint32_t ng = load_groups(a, q, g, &s_ng, true);
+  if (tid == 0) {
+    s_occ = 0;
+    s_delta = 0;
+  }
+  __syncthreads();
+  side_prepass_m(a, q, g, ng, s_sg, s_occb, &s_occ, s_side);
+  __syncthreads();
+  for (uint32_t k = tid; k < a.cm; k += 256) {
+    GroupM& G = g[k];
+    const bool real = k < ng;
+    const GroupFields f = group_fields(G);
+    const uint32_t len = selu32(real & ((int32_t)f.slot >= 0), f.len, 0u);
+    const uint32_t dp = min(G.n_del, len);
+    const uint64_t lenmask = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
+    const uint64_t mask = (((uint64_t)G.mhi << 32) | G.mlo) & lenmask & ~((1ull << dp) - 1ull);
+    const uint32_t nk = len - dp - (uint32_t)__popcll(mask);
+    G.fl = selu32(real, nk + min(G.n_succ, GVS_MAILBOX_SLOTS - nk), 0u);
+    s_gflag[k] = (real & ((int32_t)f.slot < 0) & (G.fl > 0)) ? 1 : 0;
+    s_ld[k] = 0;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j];
+    const bool occ = s_occb[j] != 0;
+    s_flag[j] = (!occ || (k >= 0 && g[k].fl == 0)) ? 1 : 0;
+  }
+  __syncthreads();
+  block_flag_scan(s_flag, a.Sr, s_pfx, s_w);
+  block_flag_scan(s_gflag, a.cm, s_gpfx, s_w);
+  for (uint32_t k = tid; k < a.cm; k += 256)
+    s_pend[s_gflag[k] ? s_gpfx[k] : (uint32_t)kGroupMax] = (int16_t)k;
+  __syncthreads();
+  const uint32_t npend = s_gpfx[a.cm];
+  if (tid == 0 && npend > s_pfx[a.Sr]) atomicOr(&a.scal->error, 2u);
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int16_t cand = s_pend[min((uint32_t)s_pfx[j], (uint32_t)kGroupMax)];
+    s_place[j] = (s_flag[j] && s_pfx[j] < npend) ? cand : (int16_t)-1;
+    const int k = s_sg[j];
+    atomicSub(&s_delta, (k >= 0 && g[k >= 0 ? k : 0].fl == 0) ? 1u : 0u);
+  }
+  if (tid == 0) atomicAdd(&s_delta, npend);
+  if (tid < kRowWaves) s_tw[tid] = 0;
+  __syncthreads();
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j], pl = s_place[j];
+    const int ge = pl >= 0 ? pl : k;
+    s_ld[ge >= 0 ? (uint32_t)ge : (uint32_t)kGroupMax] = 1;
+    atomicAdd(&s_tw[(j / kMU) % kRowWaves], ge >= 0 ? 1u : 0u);
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < a.cm; k += 256) s_gflag[k] = s_ld[k] ? 0 : 1;
+  __syncthreads();
+  block_flag_scan(s_gflag, a.cm, s_gpfx, s_w);
+  for (uint32_t k = tid; k < a.cm; k += 256)
+    if (s_gflag[k]) s_pend[s_gpfx[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t nfree = s_gpfx[a.cm];
+  // ---- the side entries after batch t, every row (what the stream stores):
+  // a touched row its group's key and final length (cleared if it ends
+  // empty), every other row as it was
+  for (uint32_t j = tid; j < a.Sr; j += 256) {
+    const int k = s_sg[j], pl = s_place[j];
+    const int ge = pl >= 0 ? pl : k;
+    const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
+    const uint32_t fl = G.fl;
+    const uint64_t w1 = (G.glo << 23) | ((uint64_t)fl << 1) | 1ull;
+    const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                                              (uint32_t)(w1 >> 32)),
+                           make_uint4(0, 0, 0, 0));
+    s_side[j] = sel4(ge >= 0, nsd, s_side[j]);
+  }
+  __syncthreads();
+  // ---- batch t + 1's read prologue (k_m1x) on those side entries
+  const uint32_t ng1 = load_groups(b, q, g1, &s_ng1, false);
+  if (tid == 0) {
+    s_occ1 = 0;
+    s_empt1 = 0;
+  }
+  __syncthreads();
+  side_prepass_m(b, q, g1, ng1, s_sg1, s_occb1, &s_occ1, nullptr, s_side);
+  __syncthreads();
+  count_empty(g1, ng1, b.cm, &s_empt1);
+  __syncthreads();
+  admit_groups(g1, ng1, b.cm, (b.Sr - s_occ1) + s_empt1);
+  __syncthreads();
+  if (tid < kRowWaves) s_tw1[tid] = 0;
+  __syncthreads();
+  for (uint32_t j = tid; j < b.Sr; j += 256) atomicAdd(&s_tw1[(j / kMU) % kRowWaves], s_sg1[j] >= 0 ? 1u : 0u);
+  for (uint32_t k = tid; k < b.cm; k += 256)
+    s_tf1[k] = ((k < ng1) & ((int32_t)group_fields(g1[k]).slot >= 0)) ? 0 : 1;
+  __syncthreads();
+  block_flag_scan(s_tf1, b.cm, s_tp1, s_w);
+  for (uint32_t k = tid; k < b.cm; k += 256)
+    if (s_tf1[k]) s_tl1[s_tp1[k]] = (int16_t)k;
+  __syncthreads();
+  const uint32_t nfree1 = s_tp1[b.cm];
+  uint32_t d0, dn, e0, en;
+  slot_share(s_tw, a.cm, wave, &d0, &dn);
+  slot_share(s_tw1, b.cm, wave, &e0, &en);
+  const uint32_t nch = a.Sr > wave * kMU ? (a.Sr - wave * kMU + 4 * kMU - 1) / (4 * kMU) : 0u;
+  const uint4* res = a.m2tx + (uint64_t)q * a.cm * kVLineU4;
+  // the dry block: the write pass reads 1 KiB lines 4..7 (k_m2x), the read
+  // pass writes line 1 (k_m1x): no line read and written in one kernel
+  uint4* dry = a.mdry + (uint64_t)q * kMDryU4;
+  uint4* wst = s_wst[wave];
+  // batch t's iteration (k_m2x's step)
+  auto step2 = [&](uint4 (&v)[kMU], uint4& mine, uint32_t bit, uint32_t j0, uint32_t di) {
+    const bool slot_it = bit == 0u;
+    uint4 cur = v[0];
+#pragma unroll
+    for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+    const uint32_t j = j0 + ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u);
+    const bool listed = slot_it && di < nfree;
+    const int k = slot_it ? -1 : s_sg[j], pl = slot_it ? -1 : s_place[j];
+    const int ge = slot_it ? (listed ? (int)s_pend[di] : 0) : (pl >= 0 ? pl : k);
+    const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
+    const uint4* rs = (slot_it && !listed) ? dry + 256 + 64u * min(di - nfree, 3u)
+                                           : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
+    const uint4 app = ld_row<true>(&rs[lane]);
+    const bool matched = pl < 0;
+    const uint32_t len = matched ? G.len : 0u;
+    const uint32_t dp = min(G.n_del, len);
+    const uint64_t mask = ((uint64_t)G.mhi << 32) | G.mlo;
+    uint32_t fl;
+    const uint4 nv = m2_row(cur, matched, len, dp, mask, G.n_succ, app, wst, &fl);
+    const uint64_t w1 = (G.glo << 23) | ((uint64_t)fl << 1) | 1ull;
+    const uint4 nsd = sel4(fl > 0, make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)w1,
+                                              (uint32_t)(w1 >> 32)),
+                           make_uint4(0, 0, 0, 0));
+#pragma unroll
+    for (int uu = 0; uu < kMU; ++uu) v[uu] = sel4((bit >> uu) & 1u, nv, v[uu]);
+    mine = sel4(bit != 0u && lane == ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u), nsd, mine);
+  };
+  // batch t + 1's iteration (k_m1x's step)
+  auto step1 = [&](const uint4 (&v)[kMU], uint32_t bit, uint32_t j0, uint32_t di) {
+    const bool slot_it = bit == 0u;
+    uint4 cur = v[0];
+#pragma unroll
+    for (int uu = 1; uu < kMU; ++uu) cur = sel4((bit >> uu) & 1u, v[uu], cur);
+    const uint32_t u0 = (uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u;
+    const bool listed = slot_it && di < nfree1;
+    const int k = slot_it ? (listed ? (int)s_tl1[di] : 0) : s_sg1[j0 + u0];
+    const GroupM& G = g1[k >= 0 ? (uint32_t)k : 0u];
+    const bool real = !slot_it || (listed && (uint32_t)k < ng1);
+    const uint4 hdr = sel4(real, make_uint4(slot_it ? 0u : G.len, G.fl, G.flags, (uint32_t)G.slot),
+                           make_uint4(0, 0, 0, 0));
+    cur = sel4(lane == 0, hdr, sel4(lane == 1 || slot_it, make_uint4(0, 0, 0, 0), cur));
+    const uint32_t sl = ((q * b.cm + (uint32_t)k) * b.sink_mul) % (b.Q * b.cm);
+    uint4* dst = !listed && slot_it ? dry + 64 : real ? b.msnapp + (uint64_t)G.head * 64 : b.msnap + (uint64_t)sl * 64;
+    st_drop(dst, lane, cur);
+  };
+  uint32_t ci = 0;
+  for (uint32_t j0 = wave * kMU; j0 < a.Sr; j0 += 4 * kMU, ++ci) {
+    if (j0 + 4 * kMU < a.Sr) load_rows(vb, part, j0 + 4 * kMU, a.Sr);
+    uint4 v[kMU];
+    uint32_t mm = 0, m1 = 0;
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) {
+      const bool in = j0 + u < a.Sr;  // wave-uniform
+      v[u] = va[u];
+      mm |= (in && (s_sg[j0 + u] >= 0 || s_place[j0 + u] >= 0)) ? (1u << u) : 0u;
+    }
+    uint4 mine = (lane < (uint32_t)kMU && j0 + lane < a.Sr) ? s_side[j0 + lane] : make_uint4(0, 0, 0, 0);
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
+    const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
+    uint32_t mq = mm;
+    for (uint32_t r = 0; r < nr; ++r) {
+      const uint32_t low = mq & (0u - mq);
+      mq &= mq - 1u;
+      step2(v, mine, low, j0, d0 + dlo + (r - nt));
+    }
+    if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
+#pragma unroll
+    for (int u = 0; u < kMU; ++u)
+      if (j0 + u < a.Sr) st_stream(part, (uint64_t)(j0 + u) * 64 + lane, v[u]);
+    if (rd) {  // batch t + 1 on the rows as just written
+#pragma unroll
+      for (int u = 0; u < kMU; ++u) m1 |= (j0 + u < b.Sr && s_sg1[j0 + u] >= 0) ? (1u << u) : 0u;
+      m1 = __builtin_amdgcn_readfirstlane(m1);
+      const uint32_t nt1 = (uint32_t)__popc(m1), elo = spread_lo(ci, nch, en);
+      const uint32_t nr1 = nt1 + spread_lo(ci + 1, nch, en) - elo;
+      uint32_t mq1 = m1;
+      for (uint32_t r = 0; r < nr1; ++r) {
+        const uint32_t low = mq1 & (0u - mq1);
+        mq1 &= mq1 - 1u;
+        step1(v, low, j0, e0 + elo + (r - nt1));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) va[u] = vb[u];
+  }
+  if (nch == 0) {  // a wave with no rows: its slot iterations of both passes here
+    uint4 v[kMU], mine = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kMU; ++u) v[u] = make_uint4(0, 0, 0, 0);
+    for (uint32_t r = 0; r < dn; ++r) step2(v, mine, 0u, 0u, d0 + r);
+    if (rd)
+      for (uint32_t r = 0; r < en; ++r) step1(v, 0u, 0u, e0 + r);
+  }
+  if (tid == 0)
+    atomicAdd((unsigned long long*)&a.scal->n_mailboxes, (unsigned long long)(int64_t)(int32_t)s_delta);
+}
+
+// after k_m21x: batch t + 1's group-slot overflow joins its error word, and
+// the flag is cleared for the next batch
+__global__ void k_err_fold(Scal* scal, uint32_t* gerr) {
+  if (threadIdx.x == 0) {
+    atomicOr(&scal->error, *gerr);
+    *gerr = 0u;
+  }
 }
 
 }  // namespace gvs

@@ -355,7 +355,14 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
                          const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
                          uint8_t *side_ct, uint8_t tag[16]);
 
-/* Wait for all work on the handle's stream. */
+/* Wait for all work on the handle's stream.  A plain single-GPU store runs
+ * each batch's mailbox write pass together with the next batch's read pass
+ * (one stream over the mailbox table, DESIGN.md §3 "Fused mailbox passes");
+ * the last batch's write pass is still to run when a call returns (its
+ * responses are final).  gvs_synchronize, gvs_get_stats and the test hooks
+ * run it first.  Its one late check (the table's consistency, error bit 2)
+ * then surfaces here or in the next batch, as GVS_ERR_INTERNAL with the
+ * handle poisoned. */
 int gvs_synchronize(gvs_handle *h);
 
 /* Tuning knobs (engine-internal choices that never change results):

@@ -117,6 +117,12 @@ case "$2" in
       python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
   allfinal)  # the GPU suite without counters/timing, the profiling session, then the driver's command, smoke and bench lines
     tests && bash "$0" "$1" prof && bash "$0" "$1" final ;;
+  fusecheck)  # the GPU suite without counters/timing, the store's timing and plain counters, a bench line
+    tests && \
+    step timing_store 600 $PT tests/test_timing.py -k "independent_of_mix and not sealed and not routed" && \
+    step obl_plain 600 $PT tests/test_oblivious.py -k "plain" && \
+    step bench 400 python3 bench.py --no-cpu
+    cp gpurun_out/timing_c3_store*.txt gpurun_out/oblivious_*_plain.txt "$O/" 2>/dev/null ;;
   ttime)  # the GPU suite without counters/timing, then every timing shape with per-test durations
     tests && \
     step timing_all 1000 $PT --durations=0 tests/test_timing.py
