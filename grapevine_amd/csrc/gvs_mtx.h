@@ -913,6 +913,10 @@ __global__ __launch_bounds__(256) void k_m2x(MArgs a) {
 // overflow flag (its k_gtx scan runs before this kernel and must not stop
 // batch t's write pass, whose status was already decided); the read pass of
 // a failed batch t + 1 is skipped (its snapshots are never used).
+#ifndef GVS_DIAG_M21
+#define GVS_DIAG_M21 0  // diagnostic builds only: 1 = no slot iterations, 2 = prologues only
+#endif
+
 struct M21Args {
   MArgs w, r;
   const uint32_t* gerr;
@@ -1050,6 +1054,9 @@ __global__ __launch_bounds__(256) void k_m21x(M21Args A) {
     if (s_tf1[k]) s_tl1[s_tp1[k]] = (int16_t)k;
   __syncthreads();
   const uint32_t nfree1 = s_tp1[b.cm];
+#if GVS_DIAG_M21 == 2
+  return;  // diagnostic builds only: the prologues alone
+#endif
   uint32_t d0, dn, e0, en;
   slot_share(s_tw, a.cm, wave, &d0, &dn);
   slot_share(s_tw1, b.cm, wave, &e0, &en);
@@ -1060,7 +1067,18 @@ __global__ __launch_bounds__(256) void k_m21x(M21Args A) {
   uint4* dry = a.mdry + (uint64_t)q * kMDryU4;
   uint4* wst = s_wst[wave];
   // batch t's iteration (k_m2x's step)
-  auto step2 = [&](uint4 (&v)[kMU], uint4& mine, uint32_t bit, uint32_t j0, uint32_t di) {
+  // the 1-KiB line an iteration appends from: its group's result line, or a
+  // dry line past the list of slots no row takes
+  auto app_src = [&](uint32_t bit, uint32_t j0, uint32_t di) -> const uint4* {
+    const bool slot_it = bit == 0u;
+    const uint32_t j = j0 + ((uint32_t)__builtin_ctz(bit | (1u << 31)) & 31u);
+    const bool listed = slot_it && di < nfree;
+    const int k = slot_it ? -1 : s_sg[j], pl = slot_it ? -1 : s_place[j];
+    const int ge = slot_it ? (listed ? (int)s_pend[di] : 0) : (pl >= 0 ? pl : k);
+    return (slot_it && !listed) ? dry + 256 + 64u * min(di - nfree, 3u)
+                                : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
+  };
+  auto step2 = [&](uint4 (&v)[kMU], uint4& mine, uint32_t bit, uint32_t j0, uint32_t di, uint4 app) {
     const bool slot_it = bit == 0u;
     uint4 cur = v[0];
 #pragma unroll
@@ -1070,9 +1088,6 @@ __global__ __launch_bounds__(256) void k_m21x(M21Args A) {
     const int k = slot_it ? -1 : s_sg[j], pl = slot_it ? -1 : s_place[j];
     const int ge = slot_it ? (listed ? (int)s_pend[di] : 0) : (pl >= 0 ? pl : k);
     const GroupM& G = g[ge >= 0 ? (uint32_t)ge : 0u];
-    const uint4* rs = (slot_it && !listed) ? dry + 256 + 64u * min(di - nfree, 3u)
-                                           : res + (uint64_t)(ge >= 0 ? ge : 0) * kVLineU4 + 8;
-    const uint4 app = ld_row<true>(&rs[lane]);
     const bool matched = pl < 0;
     const uint32_t len = matched ? G.len : 0u;
     const uint32_t dp = min(G.n_del, len);
@@ -1121,16 +1136,17 @@ __global__ __launch_bounds__(256) void k_m21x(M21Args A) {
     const uint32_t nt = (uint32_t)__popc(mm), dlo = spread_lo(ci, nch, dn);
     const uint32_t nr = nt + spread_lo(ci + 1, nch, dn) - dlo;
     uint32_t mq = mm;
-    for (uint32_t r = 0; r < nr; ++r) {
+    for (uint32_t r = 0; r < (GVS_DIAG_M21 == 1 ? 0u : nr); ++r) {
       const uint32_t low = mq & (0u - mq);
       mq &= mq - 1u;
-      step2(v, mine, low, j0, d0 + dlo + (r - nt));
+      const uint32_t di = d0 + dlo + (r - nt);
+      step2(v, mine, low, j0, di, ld_row<true>(&app_src(low, j0, di)[lane]));
     }
     if (lane < (uint32_t)kMU && j0 + lane < a.Sr) side[j0 + lane] = mine;
 #pragma unroll
     for (int u = 0; u < kMU; ++u)
       if (j0 + u < a.Sr) st_stream(part, (uint64_t)(j0 + u) * 64 + lane, v[u]);
-    if (rd) {  // batch t + 1 on the rows as just written
+    if (rd && GVS_DIAG_M21 != 1) {  // batch t + 1 on the rows as just written
 #pragma unroll
       for (int u = 0; u < kMU; ++u) m1 |= (j0 + u < b.Sr && s_sg1[j0 + u] >= 0) ? (1u << u) : 0u;
       m1 = __builtin_amdgcn_readfirstlane(m1);
@@ -1150,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_m21x(M21Args A) {
     uint4 v[kMU], mine = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kMU; ++u) v[u] = make_uint4(0, 0, 0, 0);
-    for (uint32_t r = 0; r < dn; ++r) step2(v, mine, 0u, 0u, d0 + r);
+    for (uint32_t r = 0; r < dn; ++r) step2(v, mine, 0u, 0u, d0 + r, ld_row<true>(&app_src(0u, 0u, d0 + r)[lane]));
     if (rd)
       for (uint32_t r = 0; r < en; ++r) step1(v, 0u, 0u, e0 + r);
   }

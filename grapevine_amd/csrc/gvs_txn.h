@@ -97,43 +97,72 @@ __device__ inline uint32_t line_u32(uint4 x, uint32_t k) {
 template <class V>
 __device__ inline void v_copy(V& d, const V& s) { d = s; }
 
-// s holds kScanT + 1 entries: s[kScanT] is the identity, so that every step
-// combines unconditionally (a branch around a struct assignment puts the
-// struct in scratch)
+// A block's values in LDS word-major: word k of element i at s[k * (kScanT +
+// 1) + i], so that the 64 lanes of a wave touch 64 consecutive words (element-
+// major, a value of 48 words put the lanes of one load on one bank group:
+// Rr1V's scans ran 20-35 us).  kScanT + 1 elements: s[kScanT] is the identity,
+// so that every step combines unconditionally (a branch around a struct
+// assignment puts the struct in scratch).
+template <class V>
+constexpr uint32_t scan_words() {
+  static_assert(sizeof(V) % 4 == 0, "scan values are whole words");
+  return sizeof(V) / 4;
+}
+template <class V>
+__device__ inline void lds_put(uint32_t* s, uint32_t i, const V& v) {
+  uint32_t w[scan_words<V>()];
+  __builtin_memcpy(w, &v, sizeof(V));
+#pragma unroll
+  for (uint32_t k = 0; k < scan_words<V>(); ++k) s[k * (kScanT + 1) + i] = w[k];
+}
+template <class V>
+__device__ inline V lds_get(const uint32_t* s, uint32_t i) {
+  uint32_t w[scan_words<V>()];
+#pragma unroll
+  for (uint32_t k = 0; k < scan_words<V>(); ++k) w[k] = s[k * (kScanT + 1) + i];
+  V v;
+  __builtin_memcpy(&v, w, sizeof(V));
+  return v;
+}
+#define GVS_SCAN_LDS(V, name) __shared__ uint32_t name[(kScanT + 1) * scan_words<V>()]
+
+// exclusive block scan; *total gets the block's total
 template <class Op>
-__device__ inline typename Op::V block_excl(const typename Op::V& x, typename Op::V* s) {
+__device__ inline typename Op::V block_excl(const typename Op::V& x, uint32_t* s, typename Op::V* total = nullptr) {
   using V = typename Op::V;
   const uint32_t t = threadIdx.x;
-  s[t] = x;
-  if (t == 0) s[kScanT] = Op::identity();
+  lds_put<V>(s, t, x);
+  if (t == 0) lds_put<V>(s, kScanT, Op::identity());
   __syncthreads();
   for (uint32_t d = 1; d < kScanT; d <<= 1) {
-    const V y = Op::combine(s[t >= d ? t - d : kScanT], s[t]);
+    const V y = Op::combine(lds_get<V>(s, t >= d ? t - d : kScanT), lds_get<V>(s, t));
     __syncthreads();
-    s[t] = y;
+    lds_put<V>(s, t, y);
     __syncthreads();
   }
-  const V ex = s[t ? t - 1 : kScanT];
+  const V ex = lds_get<V>(s, t ? t - 1 : kScanT);
+  if (total) *total = lds_get<V>(s, kScanT - 1);
   __syncthreads();
-  return ex;  // s[kScanT - 1] still holds the block total
+  return ex;
 }
 
 // Phase-B scans stop when the batch already failed (Op::stop): an abandoned
 // batch must not overwrite the pending final states of the previous one.
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_a(typename Op::Args a) {
-  __shared__ typename Op::V s[kScanT + 1];
+  GVS_SCAN_LDS(typename Op::V, s);
   if (Op::stop(a)) return;
   __shared__ uint4 stage[4 * 64 * 8];  // per-wave record stage (wave_load128)
   const uint32_t p = blockIdx.x * kScanT + threadIdx.x;
-  block_excl<Op>(Op::local(a, p, stage + (threadIdx.x >> 6) * 64 * 8), s);
-  if (threadIdx.x == 0) a.agg[blockIdx.x] = s[kScanT - 1];
+  typename Op::V tot;
+  block_excl<Op>(Op::local(a, p, stage + (threadIdx.x >> 6) * 64 * 8), s, &tot);
+  if (threadIdx.x == 0) a.agg[blockIdx.x] = tot;
 }
 
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_b(typename Op::Args a) {
   using V = typename Op::V;
-  __shared__ V s[kScanT + 1];
+  GVS_SCAN_LDS(V, s);
   if (Op::stop(a)) return;
   const uint32_t t = threadIdx.x, nb = a.nblk;
   const uint32_t per = (nb + kScanT - 1) / kScanT, lo = min(nb, t * per), hi = min(nb, lo + per);
@@ -148,7 +177,7 @@ __global__ __launch_bounds__(kScanT) void k_scan_b(typename Op::Args a) {
 
 template <class Op>
 __global__ __launch_bounds__(kScanT) void k_scan_c(typename Op::Args a) {
-  __shared__ typename Op::V s[kScanT + 1];
+  GVS_SCAN_LDS(typename Op::V, s);
   __shared__ uint4 stage[4 * 64 * 8];  // per-wave record stage (wave_store128)
   if (Op::stop(a)) return;
   const uint32_t p = blockIdx.x * kScanT + threadIdx.x;

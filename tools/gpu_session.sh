@@ -117,6 +117,12 @@ case "$2" in
       python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
   allfinal)  # the GPU suite without counters/timing, the profiling session, then the driver's command, smoke and bench lines
     tests && bash "$0" "$1" prof && bash "$0" "$1" final ;;
+  m21ab)  # the fused mailbox pass: production and the diagnostic builds in ab/ (M21AB="VAR ...")
+    step bench_base 300 python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10
+    for v in ${M21AB:-m21s m21p}; do
+      GVS_LIB_OVERRIDE=ab/libgvstore_$v.so step bench_$v 300 python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10
+    done
+    for f in "$O"/bench_*.log; do echo "$f"; grep '^{"metric"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms_per_step'],3), {k: round(v,3) for k, v in d['stage_ms'].items()})"; done ;;
   fusecheck)  # the GPU suite without counters/timing, the store's timing and plain counters, a bench line
     tests && \
     step timing_store 600 $PT tests/test_timing.py -k "independent_of_mix and not sealed and not routed" && \
