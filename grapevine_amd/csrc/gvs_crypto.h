@@ -9,17 +9,29 @@
 //   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
 //                       (standard CTR, counter in the last two bytes)
 //   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
-//   L_i  = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table & 1),
-//                      leaf i of ct)
-//          message tables (table & 1 = 0: tables 0, 2 and 0x100): 8 leaves
-//          of 128 B; mailbox table (1): 4 leaves of 256 B
 //   H    = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
 //                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
-//   tag  = H ^ L_0 ^ .. ^ L_(n-1)
-// An XOR-MAC with a counter term (Bellare-Guerin-Rogaway's XMACC): H is the
-// PRF of a value that is never sealed twice, (row, e, table), and the L_i are
-// PRFs of index-separated blocks.  The tag binds row, table and epoch, so a
-// replayed, moved or spliced row fails.  The key block of each keyed hash
+//   tag  = H ^ G(ct)
+//   G    = message tables (table & 1 = 0: tables 0, 2 and 0x100): the row
+//          hash (round 6): the layers of UMAC's UHASH-128 (RFC 4418 §5) for
+//          one 1024-byte block, four NH iterations over the row's 256
+//          little-endian words with the key shifted 16 bytes per iteration,
+//          each reduced to 32 bits by the p36 inner product (L3) and padded:
+//            S_t = sum_j ((m[2j] + k[4t+2j]) mod 2^32)((m[2j+1] + k[4t+2j+1]) mod 2^32) mod 2^64
+//            Y_t = ((sum_c chunk_c(S_t) l3k[4t+c]) mod (2^36 - 5)) mod 2^32 ^ l3p[t]
+//          (chunk_c the 16-bit pieces of S_t, most significant first), keys
+//          from BLAKE2b-512(key = mac_key, "gvs-uhash-" | byte j), j < 19;
+//          mailbox table (1): the XOR of its four leaf PRFs
+//            L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(1),
+//                              leaf i of ct, 256 B)
+// The message tables' tag is a Carter-Wegman MAC: H is the PRF of a value
+// that is never sealed twice, (row, e, table), and G an almost-XOR-universal
+// hash of the row (UHASH-128's bound, ~2^-120 per forgery attempt; a store
+// stops at its first bad tag).  NH costs one 32x32->64 multiply-add per 8
+// bytes where BLAKE2b costs ~15 three-source operations: the sealed message
+// pass is bound by VALU issue.  The mailbox table keeps the
+// XOR-MAC with a counter term (Bellare-Guerin-Rogaway's XMACC).  The tag binds
+// row, table and epoch, so a replayed, moved or spliced row fails.  The key block of each keyed hash
 // depends only on (key, person): its state is computed once (SealCtx), so a
 // 128-B leaf costs one compression, a 256-B leaf two and the header one; the
 // header depends on no row data, so the message pass computes it for 64 rows
@@ -250,17 +262,6 @@ __host__ __device__ inline B2State b2_keyed_state(const uint8_t key[32], uint64_
   return s;
 }
 
-// L_i over one 128-byte leaf (m = its 16 little-endian words), from the
-// keyed state of leaf i (message tables)
-__host__ __device__ __attribute__((always_inline)) inline void leaf_prf128(const B2State& k,
-                                                                          const uint64_t m[16],
-                                                                          uint64_t out[2]) {
-  B2State s = k;
-  b2_compress(s, m, 128 + 128, true);
-  out[0] = s.h[0];
-  out[1] = s.h[1];
-}
-
 // L_i over one 256-byte leaf (m = its 32 little-endian words), from the
 // keyed state of leaf i (mailbox table)
 __host__ __device__ __attribute__((always_inline)) inline void leaf_prf(const B2State& k,
@@ -296,12 +297,53 @@ __host__ __device__ __attribute__((always_inline)) inline void header_prf(
   out[1] = s.h[1];
 }
 
+// ------------------------------------------------------- message row hash
+
+constexpr uint32_t kNhWords = 268;            // NH key: 256 words + 3 shifts of 4
+constexpr uint64_t kP36 = (1ull << 36) - 5;
+
+// NH of 16 word pairs w[0..31] against key words k(o + 4t + i) for the four
+// iterations t: s[t] += sum over pairs (mod 2^64).  `k` is any indexable key
+// (LDS, global or host array); o = 32 * leaf for a 128-B leaf of the row.
+template <typename K>
+__host__ __device__ __attribute__((always_inline)) inline void nh_words(const K& k, uint32_t o,
+                                                                       const uint32_t (&w)[32],
+                                                                       uint64_t s[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t a = w[2 * j] + k[o + 4 * t + 2 * j], b = w[2 * j + 1] + k[o + 4 * t + 2 * j + 1];
+      s[t] += (uint64_t)a * (uint64_t)b;  // one v_mad_u64_u32
+    }
+  }
+}
+
+// L3 of the four NH sums: out = G as two little-endian 64-bit words
+__host__ __device__ inline void row_hash_fin(const uint64_t s[4], const uint64_t l3k[16], const uint32_t l3p[4],
+                                             uint64_t out[2]) {
+  uint32_t y[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint64_t acc = 0;  // < 4 * 2^16 * 2^36
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc += ((s[t] >> (48 - 16 * c)) & 0xffffull) * l3k[4 * t + c];
+    uint64_t x = (acc & ((1ull << 36) - 1)) + 5ull * (acc >> 36);  // 2^36 = 5 mod p36
+    x = x >= kP36 ? x - kP36 : x;
+    y[t] = (uint32_t)x ^ l3p[t];
+  }
+  out[0] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
+  out[1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
+}
+
 // Everything a sealing kernel needs, passed by value.
 struct SealCtx {
   AesRk rk;
-  B2State leafk0[8];    // keyed states after the key block: message-table leaves (128 B)
-  B2State leafk1[4];    // mailbox-table leaves (256 B)
+  B2State leafk1[4];    // keyed states after the key block: mailbox-table leaves (256 B)
   B2State headk;        // keyed state of the header PRF
+  const uint32_t* nhk;  // message row hash: the NH key (kNhWords words, device memory)
+  uint64_t l3k[16];     // its L3 keys (< p36)
+  uint32_t l3p[4];      // its L3 pads
   uint32_t epoch;       // rows are read at `epoch`, written at `epoch + 1`
   uint32_t on;          // authenticated-storage mode enabled
 };

@@ -272,6 +272,7 @@ struct gvs_handle {
   bool poisoned = false;     // an integrity failure was seen
   SealCtx sc{};              // storage keys (epoch filled per engine)
   uint32_t* te = nullptr;    // AES table on the device
+  uint32_t* nhk = nullptr;   // message row hash's NH key on the device (sc.nhk)
   uint64_t cutoff = 0;       // expiry sweep: rows with timestamp < cutoff expire
   int kind = 0;              // 0 message store, 1 block store (gvs_oram_*), 2 key-value map (gvs_omap_*)
   int sealed_nw = 0;         // waves per workgroup of the sealed message pass (4, 8, 12; 0: by S)
@@ -489,19 +490,41 @@ static void b2_keyed_short(const uint8_t key[32], const char* msg, uint32_t nn, 
   for (uint32_t i = 0; i < nn; ++i) out[i] = (uint8_t)(s.h[i / 8] >> (8 * (i % 8)));
 }
 
-// storage keys from the config secret: AES key, MAC key state
-static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256]) {
+// storage keys from the config secret: AES key, MAC key
+// states, the message row hash's keys (nh: kNhWords words on the host; the
+// caller puts them in device memory for sc.nhk)
+static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256], uint32_t nh[kNhWords]) {
   uint8_t sb[256], ak[16], mk[32];
   aes_sbox(sb);
   aes_tables(sb, te0);
   b2_keyed_short(secret, "gvs storage aes", 16, ak);
   b2_keyed_short(secret, "gvs storage mac", 32, mk);
   aes_expand(sb, ak, sc.rk);
-  for (uint32_t i = 0; i < 8; ++i)  // message tables: 8 leaves of 128 B
-    sc.leafk0[i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i);
   for (uint32_t i = 0; i < 4; ++i)  // mailbox table: 4 leaves of 256 B
     sc.leafk1[i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i | (1ull << 32));
   sc.headk = b2_keyed_state(mk, kHeadPerson0, 0);
+  // row hash keys: BLAKE2b-512(key = mac_key, "gvs-uhash-" | byte j), j < 19
+  uint8_t kb[19 * 64];
+  for (uint32_t j = 0; j < 19; ++j) {
+    const uint8_t msg[11] = {'g', 'v', 's', '-', 'u', 'h', 'a', 's', 'h', '-', (uint8_t)j};
+    B2State st = b2_init(64, 32, 0, 0);
+    uint64_t m[16];
+    b2_block(mk, 32, m);
+    b2_compress(st, m, 128, false);
+    b2_block(msg, sizeof msg, m);
+    b2_compress(st, m, 128 + sizeof msg, true);
+    for (uint32_t i = 0; i < 64; ++i) kb[64 * j + i] = (uint8_t)(st.h[i / 8] >> (8 * (i % 8)));
+  }
+  auto ld32 = [](const uint8_t* q) {
+    return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+  };
+  for (uint32_t w = 0; w < kNhWords; ++w) nh[w] = ld32(kb + 4 * w);
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint64_t k = ld64(kb + 1072 + 8 * i) & ((1ull << 36) - 1);
+    sc.l3k[i] = k >= kP36 ? k - kP36 : k;
+  }
+  for (uint32_t t = 0; t < 4; ++t) sc.l3p[t] = ld32(kb + 1200 + 4 * t);
+  sc.nhk = nullptr;
   sc.epoch = 0;
   sc.on = 1;
 }
@@ -726,11 +749,15 @@ static int create_common(const gvs_config* cfg, Mode mode, const uint8_t* comm_i
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(GVS_ERR_DEVICE);
   if (h->auth) {
-    uint32_t te0[256];
-    storage_ctx(cfg->secret_key, h->sc, te0);
+    uint32_t te0[256], nh[kNhWords];
+    storage_ctx(cfg->secret_key, h->sc, te0, nh);
     if (int rc = dalloc_t(h, &h->te, 256)) return fail(rc);
     if (hipMemcpy(h->te, te0, sizeof te0, hipMemcpyHostToDevice) != hipSuccess)
       return fail(GVS_ERR_DEVICE);
+    if (int rc = dalloc_t(h, &h->nhk, kNhWords)) return fail(rc);
+    if (hipMemcpy(h->nhk, nh, sizeof nh, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GVS_ERR_DEVICE);
+    h->sc.nhk = h->nhk;
   }
 
   const uint32_t n_eng = mode == kLocal ? h->S : 1u;
@@ -2506,8 +2533,8 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
   const bool known = table <= 2 || table == kPendTable;
   if (!secret || !pt || !ct || !tag || !known || (side_pt && !side_ct)) return GVS_ERR_INVALID_ARG;
   SealCtx sc{};
-  uint32_t te0[256];
-  storage_ctx(secret, sc, te0);
+  uint32_t te0[256], nh[kNhWords];
+  storage_ctx(secret, sc, te0, nh);
   auto xor_block = [&](const uint8_t* src, uint8_t* dst, uint32_t j) {
     const uint4 k = ctr_keystream(sc.rk, te0, table, row, epoch, j);
     const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
@@ -2522,16 +2549,27 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
   }
   uint64_t t[2];
   header_prf(sc.headk, row, epoch, table, sd, t);
-  const uint32_t nl = (table & 1) ? 4 : 8, lb = 1024 / nl;  // leaves, bytes per leaf
-  for (uint32_t i = 0; i < nl; ++i) {
-    uint64_t m[32], l[2];
-    for (uint32_t k = 0; k < lb / 8; ++k) m[k] = ld64(ct + lb * i + 8 * k);
-    if (table & 1)
+  if (table & 1) {  // mailbox rows: 4 leaf PRFs of 256 B
+    for (uint32_t i = 0; i < 4; ++i) {
+      uint64_t m[32], l[2];
+      for (uint32_t k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
       leaf_prf(sc.leafk1[i], m, l);
-    else
-      leaf_prf128(sc.leafk0[i], m, l);
-    t[0] ^= l[0];
-    t[1] ^= l[1];
+      t[0] ^= l[0];
+      t[1] ^= l[1];
+    }
+  } else {  // message tables: the row hash, leaf by leaf as the kernels do
+    uint64_t sum[4] = {0, 0, 0, 0}, g[2];
+    for (uint32_t i = 0; i < 8; ++i) {
+      uint32_t w[32];
+      for (uint32_t k = 0; k < 32; ++k) {
+        const uint8_t* q = ct + 128 * i + 4 * k;
+        w[k] = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+      }
+      nh_words(nh, 32 * i, w, sum);
+    }
+    row_hash_fin(sum, sc.l3k, sc.l3p, g);
+    t[0] ^= g[0];
+    t[1] ^= g[1];
   }
   for (int b = 0; b < 16; ++b) tag[b] = (uint8_t)(t[b / 8] >> (8 * (b % 8)));
   return GVS_OK;
@@ -2546,7 +2584,8 @@ int gvs_dump_messages(gvs_handle* h, void* host_dst, uint64_t bytes) {
   uint8_t* dst = (uint8_t*)host_dst;
   std::vector<uint32_t> te0(256);
   SealCtx sc{};
-  if (h->auth) storage_ctx(h->cfg.secret_key, sc, te0.data());
+  uint32_t nh_unused[kNhWords];
+  if (h->auth) storage_ctx(h->cfg.secret_key, sc, te0.data(), nh_unused);
   for (const auto& e : h->eng) {
     GVS_HIP(h, hipMemcpyAsync(phys.data(), e.table, phys.size(), hipMemcpyDeviceToHost, h->stream));
     GVS_HIP(h, hipStreamSynchronize(h->stream));
@@ -2790,11 +2829,15 @@ static int kv_create(const gvs_oram_config* cfg, int kind, gvs_handle** out) {
   for (auto& ev : h->ev)
     if (hipEventCreate(&ev) != hipSuccess) return fail(GVS_ERR_DEVICE);
   if (h->auth) {
-    uint32_t te0[256];
-    storage_ctx(cfg->secret_key, h->sc, te0);
+    uint32_t te0[256], nh[kNhWords];
+    storage_ctx(cfg->secret_key, h->sc, te0, nh);
     if (int rc = dalloc_t(h, &h->te, 256)) return fail(rc);
     if (hipMemcpy(h->te, te0, sizeof te0, hipMemcpyHostToDevice) != hipSuccess)
       return fail(GVS_ERR_DEVICE);
+    if (int rc = dalloc_t(h, &h->nhk, kNhWords)) return fail(rc);
+    if (hipMemcpy(h->nhk, nh, sizeof nh, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GVS_ERR_DEVICE);
+    h->sc.nhk = h->nhk;
   }
   h->eng.resize(1);
   Engine& e = h->eng[0];

@@ -162,7 +162,7 @@ struct OgtOp {
     return null ? a.W : (a.logW ? (uint32_t)(hi >> (64 - a.logW)) : 0u);
   }
   __device__ static bool same_key(uint4 x, uint4 y) {
-    return x.x == y.x && x.y == y.y && (x.z & ~kSeqMask) == (y.z & ~kSeqMask) && x.w == y.w;
+    return (x.x == y.x) & (x.y == y.y) & ((x.z & ~kSeqMask) == (y.z & ~kSeqMask)) & (x.w == y.w);
   }
   __device__ static V local(const Args& a, uint32_t p, uint4*) {
     const uint4 r = rec0(a, p), h = hash(a, p);
@@ -174,15 +174,15 @@ struct OgtOp {
     }
     const bool pnull = rp.w != 0u;
     const uint32_t q = part(a, h, null), pq = p ? part(a, hp, pnull) : ~0u;
-    const bool head = !null && (p == 0 || pnull || !same_key(h, hp));
+    const bool head = !null & ((p == 0) | pnull | !same_key(h, hp));
     // own transform: READ id, WRITE const(1), REMOVE const(0), INSERT ifabsent
     const uint32_t kind = r.x;
     uint32_t fk = kTId, fe = 0;
-    fk = selu32(kind == KV_WRITE || kind == KV_REMOVE, kTConst, fk);
+    fk = selu32((kind == KV_WRITE) | (kind == KV_REMOVE), kTConst, fk);
     fe = selu32(kind == KV_WRITE, 1u, fe);
     fk = selu32(kind == KV_INSERT, kTIfAbsent, fk);
-    return V{(uint32_t)(p == 0 || q != pq), head ? 1u : 0u, head || null ? 1u : 0u, fk, fe,
-             (kind == KV_WRITE || kind == KV_INSERT) ? 1u : 0u, p, 0u};
+    return V{(uint32_t)((p == 0) | (q != pq)), head ? 1u : 0u, (head | null) ? 1u : 0u, fk, fe,
+             ((kind == KV_WRITE) | (kind == KV_INSERT)) ? 1u : 0u, p, 0u};
   }
   __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
     const uint4 r = rec0(a, p), h = hash(a, p);
@@ -192,7 +192,7 @@ struct OgtOp {
       hn = hash(a, p + 1);
       rn = rec0(a, p + 1);
     }
-    const bool last = !null && (p + 1 == a.B || rn.w != 0u || !same_key(h, hn));
+    const bool last = !null & ((p + 1 == a.B) | (rn.w != 0u) | !same_key(h, hn));
     const V in = combine(ex, loc);
     const bool head = loc.gcnt != 0u;
     const uint32_t before = loc.preset ? 0u : ex.gcnt;
@@ -257,11 +257,17 @@ __device__ inline int find_group_o(const GroupO* g, uint32_t ng, uint32_t c, uin
   for (uint32_t step = top; step > 0; step >>= 1) {
     const uint32_t t = pos + step;
     const GroupO& G = g[min(t - 1, c - 1)];
-    const bool lt = t <= ng && (G.hi < hi || (G.hi == hi && G.lo < lo));
+    // both words read at every step, bitwise (no short-circuit branch that
+    // skips the compare by the data; find_group_m's rule)
+    uint64_t ghi = G.hi, glo = G.lo;
+    asm volatile("" : "+v"(ghi), "+v"(glo));
+    const bool lt = (t <= ng) & ((ghi < hi) | ((ghi == hi) & (glo < lo)));
     pos = lt ? t : pos;
   }
   const GroupO& G = g[min(pos, c - 1)];
-  return (pos < ng && G.hi == hi && G.lo == lo) ? (int)pos : -1;
+  uint64_t ghi = G.hi, glo = G.lo;
+  asm volatile("" : "+v"(ghi), "+v"(glo));
+  return ((pos < ng) & (ghi == hi) & (glo == lo)) ? (int)pos : -1;
 }
 
 template <bool AUTH>
@@ -347,8 +353,12 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const bool used = nz4(key);
     const int k = find_group_o(g, ng, a.c, u4lo(h), u4hi(h) & kOHashMask);
     const GroupO& G = g[k >= 0 ? k : 0];
-    const bool match = used && k >= 0 && key.x == G.key[0] && key.y == G.key[1] && key.z == G.key[2] &&
-                       key.w == G.key[3];
+    // bitwise: a short-circuit && skipped the key compares (code) for rows
+    // without a hash match, i.e. by how many keys the batch misses; the
+    // instruction fetch showed in FETCH_SIZE (+20-40 KiB under the miss and
+    // insert-of-new-key mixes, profiles/r06f_oblivious_FETCH_SIZE_omap.txt)
+    const bool match = used & (k >= 0) & (key.x == G.key[0]) & (key.y == G.key[1]) & (key.z == G.key[2]) &
+                       (key.w == G.key[3]);
     const uint32_t kk = match ? (uint32_t)k : kG;  // sink entry otherwise
     g[kk].row = (int32_t)j;
     g[kk].e0 = 1u;
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   __syncthreads();
   for (uint32_t k = tid; k < a.c; k += 256) {
     const GroupO& G = g[k];
-    s_need[k] = (k < ng && !G.e0 && G.cr) ? 1 : 0;
+    s_need[k] = ((k < ng) & !G.e0 & (G.cr != 0u)) ? 1 : 0;
   }
   __syncthreads();
   block_flag_scan(s_free, a.S, s_fpfx, s_w);
@@ -366,11 +376,11 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
   const uint32_t nfree = s_fpfx[a.S], nneed = s_npfx[a.c];
   const uint32_t nadm = min(nfree, nneed);
   for (uint32_t k = tid; k < a.c; k += 256)  // admitted groups in order; the rest write the sink
-    s_pend[(s_need[k] && s_npfx[k] < nadm) ? s_npfx[k] : kG] = (int16_t)k;
+    s_pend[((s_need[k] != 0) & (s_npfx[k] < nadm)) ? s_npfx[k] : kG] = (int16_t)k;
   __syncthreads();
   // the r-th free row takes the r-th admitted group
   for (uint32_t j = tid; j < a.S; j += 256) {
-    const bool take = s_free[j] && s_fpfx[j] < nadm;
+    const bool take = (s_free[j] != 0) & (s_fpfx[j] < nadm);
     const int16_t k = s_pend[min((uint32_t)s_fpfx[j], kG)];
     const uint32_t kk = take ? (uint32_t)k : kG;
     g[kk].row = (int32_t)j;
@@ -387,7 +397,11 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const int16_t m = s_m[j];
     const uint32_t k = (uint32_t)(m & 0x3fff);
     const GroupO& G = g[m >= 0 ? k : 0u];
-    const uint32_t efin = G.fk == kTId ? G.e0 : (G.fk == kTConst ? G.fe : 1u);
+    // every field read, then selected (a ternary over fields compiled to a
+    // branch per row on its group's transform kind)
+    uint32_t gfk = G.fk, ge0 = G.e0, gfe = G.fe;
+    asm volatile("" : "+v"(gfk), "+v"(ge0), "+v"(gfe));
+    const uint32_t efin = selu32(gfk == kTId, ge0, selu32(gfk == kTConst, gfe, 1u));
     uint4 key = dkey[it], h = dh[it];
     const uint4 gk = make_uint4(G.key[0], G.key[1], G.key[2], G.key[3]);
     const uint4 gh = make_uint4((uint32_t)G.hi, (uint32_t)(G.hi >> 32), (uint32_t)G.lo, (uint32_t)(G.lo >> 32));
@@ -409,9 +423,11 @@ __global__ __launch_bounds__(256) void k_okey(OkeyArgs a) {
     const uint32_t k = min(k0 + (lane >> 3), a.c - 1u);
     const GroupO& G = g[k];
     const bool real = k < ng;
-    const bool ovf = real && s_need[k] && s_npfx[k] >= nadm;
-    const uint64_t prow = G.row >= 0 ? (uint64_t)w * a.S + (uint32_t)G.row : ~0ull;
-    const uint64_t idx = real ? G.head : (uint64_t)a.B + (uint64_t)w * a.c + k;
+    const bool ovf = real & (s_need[k] != 0) & (s_npfx[k] >= nadm);
+    uint32_t grow = (uint32_t)G.row, ghead = G.head;  // read whatever `real` is, then selected
+    asm volatile("" : "+v"(grow), "+v"(ghead));
+    const uint64_t prow = (int32_t)grow >= 0 ? (uint64_t)w * a.S + grow : ~0ull;
+    const uint64_t idx = real ? ghead : (uint64_t)a.B + (uint64_t)w * a.c + k;
     const uint4 rec0 = make_uint4((uint32_t)prow, (uint32_t)(prow >> 32), (G.e0 ? 1u : 0u) | (ovf ? 2u : 0u), 0u);
     if (k0 + (lane >> 3) < a.c) st_drop(a.ogp, idx * 8 + (lane & 7u), sel4((lane & 7u) == 0u, rec0, make_uint4(0, 0, 0, 0)));
   }
@@ -471,7 +487,7 @@ struct OrowOp {
     const uint4 op = a.opos[p];
     const uint4 g = a.ogp[(uint64_t)p * 8];  // meaningful at heads only; read at every position
     const bool head = op.x & kPosHead, null = op.x & kPosNull;
-    return V{(head || null) ? 1u : 0u, head ? g.x : ~0u, head ? g.y : ~0u, head ? g.z : 0u};
+    return V{(head | null) ? 1u : 0u, head ? g.x : ~0u, head ? g.y : ~0u, head ? g.z : 0u};
   }
   __device__ static void emit(const Args& a, uint32_t p, const V& ex, const V& loc, uint4* stage) {
     const V in = combine(ex, loc);
@@ -480,7 +496,7 @@ struct OrowOp {
     const uint32_t seq = op.x & kSeqMask;
     const bool null = op.x & kPosNull;
     const uint64_t prow = ((uint64_t)in.row_hi << 32) | in.row_lo;
-    const bool has_row = !null && prow != ~0ull;
+    const bool has_row = !null & (prow != ~0ull);
     a.rkeys[p] = r_key(has_row ? prow : kRNullRow, 0u, seq);
     uint4 rec[8];
     rec[0] = make_uint4(r.x, null ? 0u : (in.flags & 1u), null ? 0u : (in.flags >> 1) & 1u, r.y);

@@ -409,42 +409,58 @@ __device__ inline void wave_tags(const SealCtx& c, uint32_t table, uint64_t row0
   const uint32_t lane = lane_id();
   if constexpr (NL == 8) {
     static_assert(U == 8 || U == 16, "8 or 16 rows of 8 leaves");
+    // the row hash (gvs_crypto.h): lane L's leaf L & 7 against its window of
+    // the NH key (global, read once per call), the sums added over the row's
+    // 8 lanes, then L3 on each lane's row
     const uint32_t leaf = lane & 7;
-    B2State k = c.leafk0[0];
+    uint32_t k[44];
+    const uint4* kp = reinterpret_cast<const uint4*>(c.nhk + 32u * leaf);
 #pragma unroll
-    for (uint32_t i = 1; i < 8; ++i) k = b2_sel(leaf == i, c.leafk0[i], k);
-    uint64_t acc[U / 8][2];
+    for (int q = 0; q < 11; ++q) {
+      const uint4 x = kp[q];
+      k[4 * q] = x.x;
+      k[4 * q + 1] = x.y;
+      k[4 * q + 2] = x.z;
+      k[4 * q + 3] = x.w;
+    }
+    uint64_t acc[U / 8][4];
 #pragma unroll
     for (int set = 0; set < U / 8; ++set) {
       const uint32_t ur = (lane >> 3) + 8u * (uint32_t)set;
       const uint4* seg = st + (ur * 4 + (leaf >> 1)) * kSegU4 + (leaf & 1) * 8;
-      uint64_t m[16];
+      uint32_t w[32];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint4 x = seg[q];
-        m[2 * q] = u4lo(x);
-        m[2 * q + 1] = u4hi(x);
+        w[4 * q] = x.x;
+        w[4 * q + 1] = x.y;
+        w[4 * q + 2] = x.z;
+        w[4 * q + 3] = x.w;
       }
-      uint64_t r[2];
-      leaf_prf128(k, m, r);
+      uint64_t sm[4] = {0, 0, 0, 0};
+      nh_words(k, 0u, w, sm);
 #pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        r[w] ^= shfl_u64(r[w], (int)(lane ^ 1u));
-        r[w] ^= shfl_u64(r[w], (int)(lane ^ 2u));
-        r[w] ^= shfl_u64(r[w], (int)(lane ^ 4u));
-        acc[set][w] = r[w];
+      for (int t = 0; t < 4; ++t) {
+        sm[t] += shfl_u64(sm[t], (int)(lane ^ 1u));
+        sm[t] += shfl_u64(sm[t], (int)(lane ^ 2u));
+        sm[t] += shfl_u64(sm[t], (int)(lane ^ 4u));
+        acc[set][t] = sm[t];
       }
     }
     const uint32_t row = (lane >> 2) % (uint32_t)U;
     const int src = (int)(8u * (row & 7u));
+    uint64_t sm[4], g[2];
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
+    for (int t = 0; t < 4; ++t) {
       // both shuffles in every lane (a shuffle under a divergent branch would
       // read lanes that are switched off), then a per-lane select
-      const uint64_t lo = shfl_u64(acc[0][w], src);
-      const uint64_t hi = shfl_u64(acc[U / 8 - 1][w], src);
-      out[w] = (U == 16 && row >= 8 ? hi : lo) ^ hdr[w];
+      const uint64_t lo = shfl_u64(acc[0][t], src);
+      const uint64_t hi = shfl_u64(acc[U / 8 - 1][t], src);
+      sm[t] = U == 16 && row >= 8 ? hi : lo;
     }
+    row_hash_fin(sm, c.l3k, c.l3p, g);
+    out[0] = g[0] ^ hdr[0];
+    out[1] = g[1] ^ hdr[1];
     (void)table, (void)row0, (void)epoch, (void)with_side, (void)htab;
     return;
   } else {

@@ -112,25 +112,41 @@ __device__ inline void leaf_words(const uint4 (&v)[8], uint64_t (&m)[16]) {
 }
 
 // Tag of the lane's row (leaf-major: lane L holds leaf L & 7 of row L >> 3):
-// its leaf PRF, the XOR over the row's 8 lanes, then the header H.  The 8
-// leaf keys' states sit in LDS (s_lk, 8 x 128 B): each lane reads its own
-// instead of selecting among all eight, which held them in registers.
-__device__ inline void lm_tag(const uint64_t* s_lk, const uint4 (&v)[8], const uint64_t hdr[2], uint64_t out[2]) {
+// the row hash (gvs_crypto.h): NH of the lane's 32 words against its leaf's
+// window of the key (s_nh in LDS: words 32 (L & 7) .. + 43), the four sums
+// added over the row's 8 lanes, L3, then the header H.
+__device__ inline void lm_tag(const uint32_t* s_nh, const SealCtx& c, const uint4 (&v)[8], const uint64_t hdr[2],
+                              uint64_t out[2]) {
   const uint32_t leaf = lane_id() & 7u;
-  B2State k;
+  uint32_t w[32], k[44];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) k.h[i] = s_lk[leaf * 8 + i];
-  uint64_t m[16];
-  leaf_words(v, m);
-  uint64_t r[2];
-  leaf_prf128(k, m, r);
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 1u));
-    r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 2u));
-    r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 4u));
-    out[w] = r[w] ^ hdr[w];
+  for (int q = 0; q < 8; ++q) {
+    w[4 * q] = v[q].x;
+    w[4 * q + 1] = v[q].y;
+    w[4 * q + 2] = v[q].z;
+    w[4 * q + 3] = v[q].w;
   }
+  const uint4* kp = reinterpret_cast<const uint4*>(s_nh + 32u * leaf);
+#pragma unroll
+  for (int q = 0; q < 11; ++q) {
+    const uint4 x = kp[q];
+    k[4 * q] = x.x;
+    k[4 * q + 1] = x.y;
+    k[4 * q + 2] = x.z;
+    k[4 * q + 3] = x.w;
+  }
+  uint64_t sm[4] = {0, 0, 0, 0};
+  nh_words(k, 0u, w, sm);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    sm[t] += shfl_u64(sm[t], (int)(lane_id() ^ 1u));
+    sm[t] += shfl_u64(sm[t], (int)(lane_id() ^ 2u));
+    sm[t] += shfl_u64(sm[t], (int)(lane_id() ^ 4u));
+  }
+  uint64_t g[2];
+  row_hash_fin(sm, c.l3k, c.l3p, g);
+  out[0] = g[0] ^ hdr[0];
+  out[1] = g[1] ^ hdr[1];
 }
 
 // A value the compiler must treat as unknown where this is called: the loop
@@ -197,7 +213,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
   __shared__ uint4 s_xp[kXepMax * 3];
   __shared__ uint4 s_xx[kXepMax];
   __shared__ uint32_t s_xc[NW];
-  __shared__ uint64_t s_lk[8 * 8];              // the message leaves' key states (leafk0)
+  __shared__ __attribute__((aligned(16))) uint32_t s_nh[kNhWords];  // the row hash's NH key
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t w = blockIdx.x;
   if (a.scal->error) return;
@@ -205,7 +221,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
     load_te2(s_lds, a.te);
   else
     load_te(s_lds, a.te);
-  if (tid < 64) s_lk[tid] = a.sc.leafk0[tid >> 3].h[tid & 7u];
+  for (uint32_t o = tid; o < kNhWords; o += 64 * NW) s_nh[o] = a.sc.nhk[o];
   const uint32_t nwd = a.S / 32u;
   for (uint32_t o = tid; o < nwd; o += 64 * NW) {
     s_pbm[o] = 0u;
@@ -308,7 +324,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         {
           const uint64_t hr[2] = {shfl_u64(hh[0], (int)rr), shfl_u64(hh[1], (int)rr)};
           uint64_t tg[2];
-          lm_tag(s_lk, v, hr, tg);
+          lm_tag(s_nh, a.sc, v, hr, tg);
           const uint4 want = shfl4(tl, (int)u);
           if (__ballot((u4lo(want) != tg[0]) | (u4hi(want) != tg[1])) && lane == 0)
             atomicOr(&a.scal->error, 8u);  // integrity failure: the batch and the handle are dead
@@ -346,7 +362,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
           lm_ctr(a.sc, te, row, opaque(a.sc.epoch + 1u), v);
           const uint64_t hw[2] = {shfl_u64(hh[0], (int)(32u + rr)), shfl_u64(hh[1], (int)(32u + rr))};
           uint64_t tg[2];
-          lm_tag(s_lk, v, hw, tg);
+          lm_tag(s_nh, a.sc, v, hw, tg);
           // lane r < 8 writes row r's tag: the 8 rows' tags are one whole line
           const uint64_t t0 = shfl_u64(tg[0], (int)(8u * (lane & 7u))), t1 = shfl_u64(tg[1], (int)(8u * (lane & 7u)));
           if (lane < 8u)

@@ -89,6 +89,8 @@ def lib():
         L.gvo_omap_size.restype = u64
         L.gvo_omap_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.gvo_seal_row.argtypes = [cp, u32, u64, u32, cp, cp, cp, cp, cp]
+        L.gvo_uhash_keys.argtypes = [cp, vp, vp, vp]
+        L.gvo_row_hash.argtypes = [vp, vp, vp, cp, cp]
         L.gvo_id_encode_shard.argtypes = [ctypes.c_char_p, u32, u32, u64, ctypes.c_char_p]
         L.gvo_id_decode_shard.argtypes = [ctypes.c_char_p, ctypes.c_char_p, u64, u32,
                                           ctypes.POINTER(u32), ctypes.POINTER(u32),
@@ -224,6 +226,20 @@ def seal_row(secret32: bytes, table: int, row: int, epoch: int, pt: bytes, side_
                     ctypes.create_string_buffer(16))
     lib().gvo_seal_row(secret32, table, row, epoch, pt, side_pt, ct, sct if side_pt else None, tag)
     return ct.raw, (sct.raw if side_pt else None), tag.raw
+
+
+def uhash_keys(secret32: bytes):
+    """-> (nh: 268 u32, l3k: 16 u64, l3p: 4 u32), the message tables' row-hash keys"""
+    nh, l3k, l3p = np.zeros(268, np.uint32), np.zeros(16, np.uint64), np.zeros(4, np.uint32)
+    lib().gvo_uhash_keys(secret32, nh.ctypes.data, l3k.ctypes.data, l3p.ctypes.data)
+    return nh, l3k, l3p
+
+
+def row_hash(keys, ct: bytes) -> bytes:
+    nh, l3k, l3p = keys
+    out = ctypes.create_string_buffer(16)
+    lib().gvo_row_hash(nh.ctypes.data, l3k.ctypes.data, l3p.ctypes.data, ct, out)
+    return out.raw
 
 
 def identity(i: int) -> bytes:

@@ -112,6 +112,9 @@ void gvo_aes128_encrypt(const uint8_t rk[176], const uint8_t in[16], uint8_t out
 void gvo_blake2b(const uint8_t *key, size_t keylen, const uint8_t *person, const uint8_t *msg,
                  size_t len, uint8_t *out, size_t outlen);
 void gvo_storage_keys(const uint8_t secret[32], uint8_t aes_key[16], uint8_t mac_key[32]);
+void gvo_uhash_keys(const uint8_t secret[32], uint32_t nh[268], uint64_t l3k[16], uint32_t l3p[4]);
+void gvo_row_hash(const uint32_t nh[268], const uint64_t l3k[16], const uint32_t l3p[4],
+                  const uint8_t ct[1024], uint8_t out[16]);
 void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32_t epoch,
                   const uint8_t pt[1024], const uint8_t *side_pt, uint8_t ct[1024],
                   uint8_t *side_ct, uint8_t tag[16]);

@@ -225,11 +225,66 @@ static void put_le(uint8_t *p, uint64_t v, int n) {
   for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
 }
 
-/* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ L_0 ^ .. ^ L_(n-1) with
- *   L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(table & 1), leaf i)
- *   (message tables, table & 1 = 0: n = 8 leaves of 128 B; mailbox table: n = 4 of 256 B)
+/* Row-hash keys of the message tables (round 6): 1216 bytes, blocks j = 0..18
+ * of BLAKE2b-512(key = mac_key, "gvs-uhash-" | byte j).  Words 0..267 are the
+ * NH key (little-endian u32), then 16 L3 keys (le64 mod 2^36, minus p36 when
+ * at least p36 = 2^36 - 5) and 4 L3 pads (le32). */
+#define GVO_P36 ((1ull << 36) - 5)
+void gvo_uhash_keys(const uint8_t secret[32], uint32_t nh[268], uint64_t l3k[16], uint32_t l3p[4]) {
+  uint8_t ak[16], mk[32], kb[19 * 64];
+  gvo_storage_keys(secret, ak, mk);
+  for (int j = 0; j < 19; ++j) {
+    uint8_t msg[11] = {'g', 'v', 's', '-', 'u', 'h', 'a', 's', 'h', '-', (uint8_t)j};
+    gvo_blake2b(mk, 32, NULL, msg, sizeof msg, kb + 64 * j, 64);
+  }
+  for (int w = 0; w < 268; ++w)
+    nh[w] = (uint32_t)kb[4 * w] | (uint32_t)kb[4 * w + 1] << 8 | (uint32_t)kb[4 * w + 2] << 16 |
+            (uint32_t)kb[4 * w + 3] << 24;
+  for (int i = 0; i < 16; ++i) {
+    uint64_t k = le64(kb + 1072 + 8 * i) & ((1ull << 36) - 1);
+    l3k[i] = k >= GVO_P36 ? k - GVO_P36 : k;
+  }
+  for (int t = 0; t < 4; ++t) {
+    const uint8_t *q = kb + 1200 + 4 * t;
+    l3p[t] = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+  }
+}
+
+/* G(ct), the 128-bit hash of a 1024-byte message-table ciphertext: the
+ * layers of UMAC's UHASH-128 (RFC 4418 §5) for a message of one 1024-byte
+ * block, four iterations t with the NH key shifted by 4 words (16 bytes) each:
+ *   S_t = sum_j ((m[2j] + k[4t + 2j]) mod 2^32) * ((m[2j+1] + k[4t + 2j+1]) mod 2^32)
+ *         mod 2^64 over the 256 little-endian words m of the ciphertext (NH);
+ *   Y_t = ((sum_c chunk_c(S_t) * l3k[4t + c]) mod p36) mod 2^32, xor l3p[t]
+ *         with chunk_c the 16-bit pieces of S_t, most significant first (L3;
+ *         L2 of a one-block message is the identity, its upper 64 bits zero);
+ *   G = le32(Y_0) | le32(Y_1) | le32(Y_2) | le32(Y_3). */
+void gvo_row_hash(const uint32_t nh[268], const uint64_t l3k[16], const uint32_t l3p[4],
+                  const uint8_t ct[1024], uint8_t out[16]) {
+  uint32_t m[256];
+  for (int w = 0; w < 256; ++w)
+    m[w] = (uint32_t)ct[4 * w] | (uint32_t)ct[4 * w + 1] << 8 | (uint32_t)ct[4 * w + 2] << 16 |
+           (uint32_t)ct[4 * w + 3] << 24;
+  for (int t = 0; t < 4; ++t) {
+    uint64_t s = 0;
+    for (int j = 0; j < 128; ++j)
+      s += (uint64_t)(uint32_t)(m[2 * j] + nh[4 * t + 2 * j]) * (uint64_t)(uint32_t)(m[2 * j + 1] + nh[4 * t + 2 * j + 1]);
+    uint64_t y = 0;
+    for (int c = 0; c < 4; ++c) {
+      const uint64_t chunk = (s >> (48 - 16 * c)) & 0xffffu;
+      y = (y + chunk * l3k[4 * t + c]) % GVO_P36;
+    }
+    put_le(out + 4 * t, (uint32_t)y ^ l3p[t], 4);
+  }
+}
+
+/* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ G, with
  *   H   = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
  *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
+ *   G   = gvo_row_hash(ct) for the message tables (table & 1 = 0: a
+ *         Carter-Wegman MAC, H the PRF of a nonce never sealed twice);
+ *         for the mailbox table the XOR of its 4 leaf PRFs
+ *         L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(1), leaf i of 256 B)
  * table: 0 message rows, 1 mailbox rows, 2 pending final states (P, by
  * position, side = target row), 0x100 a message row whose final state is
  * pending in P (header only: its keystream and leaves are table 0's; the CTR
@@ -263,8 +318,17 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   put_le(hdr + 12, table, 4);
   if (side_pt) memcpy(hdr + 16, side_ct, 16);
   gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
-  /* message tables (table & 1 = 0): 8 leaves of 128 B; mailbox table: 4 of 256 B */
-  const uint32_t nl = (table & 1) ? 4 : 8, lb = 1024 / nl;
+  if (!(table & 1)) { /* message tables: the row hash */
+    uint32_t nh[268], l3p[4];
+    uint64_t l3k[16];
+    uint8_t g[16];
+    gvo_uhash_keys(secret, nh, l3k, l3p);
+    gvo_row_hash(nh, l3k, l3p, ct, g);
+    for (int k = 0; k < 16; ++k) tag[k] ^= g[k];
+    return;
+  }
+  /* mailbox table: 4 leaves of 256 B */
+  const uint32_t nl = 4, lb = 1024 / nl;
   for (uint32_t i = 0; i < nl; ++i) {
     uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'}, l[16];
     put_le(person + 8, i, 4);

@@ -7,7 +7,14 @@ Three independent implementations must agree:
   * the product library's host-side implementation (gvs_storage_seal_row,
     the same gvs_crypto.h code the gfx950 kernels run).
 Known-answer vectors: FIPS-197 Appendix C.1, SP 800-38A F.5.1, RFC 7693
-Appendix A.  Tag: H ^ L_0 ^ .. ^ L_3 (XOR-MAC with a counter term, gvs_crypto.h)."""
+Appendix A.  Tag: H ^ G, H the header PRF; G the row hash of the message
+tables (UHASH-128 layers: NH, the one-block L2, the p36 L3; restated below in
+Python from its definition) or, for the mailbox table, the XOR of its four leaf
+PRFs (gvs_crypto.h).  The row hash has no published vector of its own (UMAC's
+are for its full byte layout and the AES-based key derivation): the Python and
+C restatements and the library's host code are checked against each other, and
+its properties (every word and every tag bit depend on the data, key
+separation, linearity of NH) are checked below."""
 import ctypes
 import hashlib
 import shutil
@@ -39,6 +46,41 @@ def counter_block(table, row, epoch, j):
             + j.to_bytes(2, "big"))
 
 
+P36 = (1 << 36) - 5
+
+
+def py_uhash_keys(secret):
+    """The row hash's keys from BLAKE2b-512(key = mac_key, "gvs-uhash-" | j)."""
+    _, mk = py_keys(secret)
+    kb = b"".join(hashlib.blake2b(b"gvs-uhash-" + bytes([j]), key=mk, digest_size=64).digest()
+                  for j in range(19))
+    nh = [int.from_bytes(kb[4 * w:4 * w + 4], "little") for w in range(268)]
+    l3k = []
+    for i in range(16):
+        k = int.from_bytes(kb[1072 + 8 * i:1080 + 8 * i], "little") & ((1 << 36) - 1)
+        l3k.append(k - P36 if k >= P36 else k)
+    l3p = [int.from_bytes(kb[1200 + 4 * t:1204 + 4 * t], "little") for t in range(4)]
+    return nh, l3k, l3p
+
+
+def py_row_hash(keys, ct):
+    """NH over the row's 256 little-endian words, key shifted 4 words per
+    iteration; L3: the 16-bit chunks of S_t (most significant first) against
+    l3k mod p36, mod 2^32, xor l3p."""
+    nh, l3k, l3p = keys
+    m = [int.from_bytes(ct[4 * w:4 * w + 4], "little") for w in range(256)]
+    out = b""
+    for t in range(4):
+        s = 0
+        for j in range(128):
+            a = (m[2 * j] + nh[4 * t + 2 * j]) & 0xFFFFFFFF
+            b = (m[2 * j + 1] + nh[4 * t + 2 * j + 1]) & 0xFFFFFFFF
+            s = (s + a * b) & ((1 << 64) - 1)
+        y = sum(((s >> (48 - 16 * c)) & 0xFFFF) * l3k[4 * t + c] for c in range(4)) % P36
+        out += ((y & 0xFFFFFFFF) ^ l3p[t]).to_bytes(4, "little")
+    return out
+
+
 def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
     """Reference sealing of many rows at once (one openssl call)."""
     ak, mk = py_keys(secret)
@@ -53,12 +95,13 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
         hdr += sct if sct is not None else bytes(16)
         tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
                                              person=b"gvs-head" + bytes(8)).digest(), "little")
-        nl = 4 if table & 1 else 8  # mailbox rows: 4 leaves of 256 B; message tables: 8 of 128 B
-        lb = 1024 // nl
-        for i in range(nl):
-            person = b"gvs-leaf" + i.to_bytes(4, "little") + (table & 1).to_bytes(4, "little")
-            tag ^= int.from_bytes(hashlib.blake2b(ct[lb * i:lb * i + lb], key=mk, digest_size=16,
-                                                  person=person).digest(), "little")
+        if table & 1:  # mailbox rows: 4 leaf PRFs of 256 B
+            for i in range(4):
+                person = b"gvs-leaf" + i.to_bytes(4, "little") + (1).to_bytes(4, "little")
+                tag ^= int.from_bytes(hashlib.blake2b(ct[256 * i:256 * i + 256], key=mk, digest_size=16,
+                                                      person=person).digest(), "little")
+        else:  # message tables: the row hash
+            tag ^= int.from_bytes(py_row_hash(py_uhash_keys(secret), ct), "little")
         out.append((ct, sct, tag.to_bytes(16, "little")))
     return out
 
@@ -148,3 +191,35 @@ def test_library_host_sealing_matches_oracle(table):
         pt = rng.bytes(1024)
         side = rng.bytes(16) if has_side(table) else None
         assert library_seal(table, row, 9, pt, side) == ffi.seal_row(SECRET, table, row, 9, pt, side)
+
+
+def test_row_hash_c_matches_python():
+    keys_c, keys_py = ffi.uhash_keys(SECRET), py_uhash_keys(SECRET)
+    assert list(keys_c[0]) == keys_py[0] and list(keys_c[1]) == keys_py[1] and list(keys_c[2]) == keys_py[2]
+    assert all(k < P36 for k in keys_py[1])
+    rng = np.random.default_rng(11)
+    for ct in (bytes(1024), b"\xff" * 1024, rng.bytes(1024), rng.bytes(1024)):
+        assert ffi.row_hash(keys_c, ct) == py_row_hash(keys_py, ct)
+
+
+def test_row_hash_properties():
+    """Every 4-byte word of the row and every tag word depend on the data;
+    other secrets give other keys; NH is linear in the key offset as stated
+    (the Toeplitz shift: iteration t reads key words 4t .. 4t + 255)."""
+    keys = ffi.uhash_keys(SECRET)
+    rng = np.random.default_rng(12)
+    ct = bytearray(rng.bytes(1024))
+    g0 = ffi.row_hash(keys, bytes(ct))
+    for w in range(0, 256, 17):
+        c2 = bytearray(ct)
+        c2[4 * w] ^= 1
+        g1 = ffi.row_hash(keys, bytes(c2))
+        assert all(g0[4 * t:4 * t + 4] != g1[4 * t:4 * t + 4] for t in range(4)), w
+    other = ffi.uhash_keys(bytes(31) + b"\x01")
+    assert ffi.row_hash(other, bytes(ct)) != g0
+    nh, l3k, l3p = keys
+    shifted = (np.concatenate([nh[4:], np.zeros(4, np.uint32)]), l3k.copy(), l3p.copy())
+    # iteration 1 of the original keys is iteration 0 of keys shifted by 4 words, given its L3 keys
+    shifted[1][0:4] = l3k[4:8]
+    shifted[2][0] = l3p[1]
+    assert ffi.row_hash(shifted, bytes(ct))[0:4] == g0[4:8]

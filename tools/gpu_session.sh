@@ -117,6 +117,11 @@ case "$2" in
       python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0 ;;
   allfinal)  # the GPU suite without counters/timing, the profiling session, then the driver's command, smoke and bench lines
     tests && bash "$0" "$1" prof && bash "$0" "$1" final ;;
+  sealmac)  # the GPU suite without counters/timing, the map and sealed counter shapes, the sealed bench line
+    tests && \
+    step obl_map 900 $PT tests/test_oblivious.py -k "omap or (auth and not oram)" && \
+    step bench_auth 400 python3 bench.py --auth --no-cpu --steps 5 --host-steps 0 --wire-steps 0
+    cp gpurun_out/oblivious_*omap*.txt gpurun_out/oblivious_*_auth.txt "$O/" 2>/dev/null ;;
   m21ab)  # the fused mailbox pass: production and the diagnostic builds in ab/ (M21AB="VAR ...")
     step bench_base 300 python3 bench.py --no-cpu --host-steps 0 --wire-steps 0 --steps 10
     for v in ${M21AB:-m21s m21p}; do
