@@ -9,7 +9,10 @@
 //   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
 //                       (standard CTR, counter in the last two bytes)
 //   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
-//   H    = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+//   H    = message tables: AES-128_kh(le64(row) | le32(e) | le32(table)),
+//          then AES-128_kh of that ^ side_ct for table 2 (head_aes;
+//          kh = BLAKE2b-128(key = secret, "gvs storage head"));
+//          mailbox table: BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
 //                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
 //   tag  = H ^ G(ct)
 //   G    = message tables (table & 1 = 0: tables 0, 2 and 0x100): the row
@@ -121,6 +124,23 @@ __host__ __device__ inline uint4 ctr_keystream(const AesRk& rk, const Tab& te0, 
   aes128_encrypt_words(rk, te0, bswap32((uint32_t)row), bswap32((uint32_t)(row >> 32)),
                        bswap32(epoch), (table << 24) | j, o);
   return make_uint4(bswap32(o[0]), bswap32(o[1]), bswap32(o[2]), bswap32(o[3]));
+}
+
+// H of a message-table row (table & 1 = 0): AES-128 under kh of the nonce
+// le64(row) | le32(epoch) | le32(table), and for the tables with a side entry
+// (P, table 2) AES again of that XOR the side ciphertext: a PRF of a fixed-
+// length input per table.  out = H as two little-endian 64-bit words.
+template <typename Tab>
+__host__ __device__ inline void head_aes(const AesRk& rkh, const Tab& te0, uint64_t row, uint32_t epoch,
+                                         uint32_t table, const uint64_t* side, uint64_t out[2]) {
+  uint32_t o[4];
+  aes128_encrypt_words(rkh, te0, bswap32((uint32_t)row), bswap32((uint32_t)(row >> 32)), bswap32(epoch),
+                       bswap32(table), o);
+  if (side)
+    aes128_encrypt_words(rkh, te0, o[0] ^ bswap32((uint32_t)side[0]), o[1] ^ bswap32((uint32_t)(side[0] >> 32)),
+                         o[2] ^ bswap32((uint32_t)side[1]), o[3] ^ bswap32((uint32_t)(side[1] >> 32)), o);
+  out[0] = (uint64_t)bswap32(o[0]) | ((uint64_t)bswap32(o[1]) << 32);
+  out[1] = (uint64_t)bswap32(o[2]) | ((uint64_t)bswap32(o[3]) << 32);
 }
 
 // --------------------------------------------------------------- BLAKE2b
@@ -339,6 +359,7 @@ __host__ __device__ inline void row_hash_fin(const uint64_t s[4], const uint64_t
 // Everything a sealing kernel needs, passed by value.
 struct SealCtx {
   AesRk rk;
+  AesRk rkh;            // message tables' header PRF (head_aes)
   B2State leafk1[4];    // keyed states after the key block: mailbox-table leaves (256 B)
   B2State headk;        // keyed state of the header PRF
   const uint32_t* nhk;  // message row hash: the NH key (kNhWords words, device memory)

@@ -500,6 +500,9 @@ static void storage_ctx(const uint8_t secret[32], SealCtx& sc, uint32_t te0[256]
   b2_keyed_short(secret, "gvs storage aes", 16, ak);
   b2_keyed_short(secret, "gvs storage mac", 32, mk);
   aes_expand(sb, ak, sc.rk);
+  uint8_t kh[16];
+  b2_keyed_short(secret, "gvs storage head", 16, kh);
+  aes_expand(sb, kh, sc.rkh);
   for (uint32_t i = 0; i < 4; ++i)  // mailbox table: 4 leaves of 256 B
     sc.leafk1[i] = b2_keyed_state(mk, kLeafPerson0, (uint64_t)i | (1ull << 32));
   sc.headk = b2_keyed_state(mk, kHeadPerson0, 0);
@@ -2548,7 +2551,10 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
     sd[1] = ld64(side_ct + 8);
   }
   uint64_t t[2];
-  header_prf(sc.headk, row, epoch, table, sd, t);
+  if (table & 1)
+    header_prf(sc.headk, row, epoch, table, sd, t);
+  else
+    head_aes(sc.rkh, te0, row, epoch, table, side_pt ? sd : nullptr, t);
   if (table & 1) {  // mailbox rows: 4 leaf PRFs of 256 B
     for (uint32_t i = 0; i < 4; ++i) {
       uint64_t m[32], l[2];

@@ -615,7 +615,10 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
       sd[0] = u4lo(x);
       sd[1] = u4hi(x);
     }
-    header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);  // one-time: no amortising
+    if (side)  // one-time: no amortising
+      header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);
+    else  // message tables (gvs_crypto.h head_aes)
+      head_aes(c.rkh, lds_te(s_te), r0 + ((lane >> 2) % U), 0u, table, nullptr, hdr);
     if (side)
       wave_seal<U, 4>(c, s_te, table, r0, 0u, v, tags, true, st, hdr);
     else  // message tables: 8 leaves of 128 B

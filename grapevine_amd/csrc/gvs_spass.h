@@ -307,8 +307,18 @@ __global__ __launch_bounds__(64 * NW, 1) void k_spass(R2Args a) {
         const bool wr = lane >= 32u;
         const uint32_t bits = wr ? cbits : pbits;
         const uint32_t tab = ((bits >> r) & 1u) ? kPendTable : 0u;
-        const uint64_t z[2] = {0, 0};
-        header_prf(opaque(a.sc.headk), rowbase + g * 32u + r, opaque(a.sc.epoch + (wr ? 1u : 0u)), tab, z, hh);
+        // H = AES-128_kh(le64(row) | le32(epoch) | le32(table)) (gvs_crypto.h
+        // head_aes), one block per lane on the two LDS tables
+        const uint64_t row = rowbase + g * 32u + r;
+        const uint32_t ep = opaque(a.sc.epoch + (wr ? 1u : 0u));
+        uint32_t hs[1][4] = {{bswap32((uint32_t)row) ^ a.sc.rkh.w[0], bswap32((uint32_t)(row >> 32)) ^ a.sc.rkh.w[1],
+                              bswap32(ep) ^ a.sc.rkh.w[2], bswap32(tab) ^ a.sc.rkh.w[3]}};
+        if (GVS_SP_DUAL)
+          aes128_rounds_n2<1, 1>(a.sc.rkh, te, hs);
+        else
+          aes128_rounds_n<1, 1>(a.sc.rkh, te, hs);
+        hh[0] = (uint64_t)bswap32(hs[0][0]) | ((uint64_t)bswap32(hs[0][1]) << 32);
+        hh[1] = (uint64_t)bswap32(hs[0][2]) | ((uint64_t)bswap32(hs[0][3]) << 32);
       }
 #pragma unroll 1
       for (uint32_t jj = 0; jj < 4; ++jj) {

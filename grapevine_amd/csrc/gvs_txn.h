@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256) void k_pseal(PsealArgs a) {
   const uint4 x = st[U * 4 * kSegU4 + ur];
   const uint64_t sdv[2] = {u4lo(x), u4hi(x)};
   uint64_t hdr[2];
-  header_prf(a.sc.headk, p0 + ur, a.ep, 2u, sdv, hdr);
+  head_aes(a.sc.rkh, lds_te(s_te), p0 + ur, a.ep, 2u, sdv, hdr);  // table 2: its side ciphertext bound in
   bool ok = true;
   if (SEAL) {
     wave_seal<U, 8>(a.sc, s_te, 2u, p0, a.ep, v, a.ptag, true, st, hdr);

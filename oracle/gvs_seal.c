@@ -279,7 +279,9 @@ void gvo_row_hash(const uint32_t nh[268], const uint64_t l3k[16], const uint32_t
 }
 
 /* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ G, with
- *   H   = BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+ *   H   = message tables (table & 1 = 0): AES-128_kh(le64(row) | le32(epoch) | le32(table)),
+ *         for table 2 (side entry) AES-128_kh(that ^ side ct);
+ *         mailbox table: BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
  *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
  *   G   = gvo_row_hash(ct) for the message tables (table & 1 = 0: a
  *         Carter-Wegman MAC, H the PRF of a nonce never sealed twice);
@@ -317,7 +319,23 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   put_le(hdr + 8, epoch, 4);
   put_le(hdr + 12, table, 4);
   if (side_pt) memcpy(hdr + 16, side_ct, 16);
-  gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
+  if (!(table & 1)) {
+    /* message tables: H = AES_kh(nonce), or AES_kh(AES_kh(nonce) ^ side ct)
+     * for the tables with a side entry (P, table 2): a PRF of a fixed-length
+     * input per table, kh = BLAKE2b-128(key = secret, "gvs storage head") */
+    static const char hk[] = "gvs storage head";
+    uint8_t kh[16], rkh[176];
+    gvo_blake2b(secret, 32, NULL, (const uint8_t *)hk, sizeof hk - 1, kh, 16);
+    gvo_aes128_expand(kh, rkh);
+    gvo_aes128_encrypt(rkh, hdr, tag);
+    if (side_pt) {
+      uint8_t x[16];
+      for (int k = 0; k < 16; ++k) x[k] = (uint8_t)(tag[k] ^ side_ct[k]);
+      gvo_aes128_encrypt(rkh, x, tag);
+    }
+  } else {
+    gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
+  }
   if (!(table & 1)) { /* message tables: the row hash */
     uint32_t nh[268], l3p[4];
     uint64_t l3k[16];

@@ -149,3 +149,23 @@ def test_interleaved_one_stalled_batch_is_dropped():
     stall = {("main", 3, 0): 25.0}
     lines, bad, mdb = tt.evaluate_interleaved(_interleaved(stall), "rud")
     assert not bad, bad
+
+
+# ---- the counter test's fresh-process rule (tests/test_oblivious.py)
+
+def test_counter_rerun_candidates():
+    mixes = ["main", "rud", "deletes", "hot_next", "main#2"]
+    one = [("k_spass", "rud", "batch", 16.4, 3.9, 0, 1), ("k_spass", "rud", "bias", 2.7, 0.6)]
+    assert ob.rerun_candidates(one, mixes) == ["rud"]
+    assert ob.rerun_candidates(one, mixes, fresh=("rud",)) == []
+    # most mixes biased the same way on one kernel: the reference is the suspect
+    ref = [("k", m, "bias", -3.0, 1.0) for m in ("rud", "deletes", "hot_next")]
+    assert ob.rerun_candidates(ref, mixes) == ["main"]
+
+
+def test_counter_evaluation_flags_a_one_batch_excursion():
+    per = {"main": _proc(_pre([10] * ob.N_MEAS)), "rud": _proc(_pre([10] * ob.N_MEAS)),
+           "main#2": _proc(_pre([10] * ob.N_MEAS))}
+    per["rud"][3 + 2] = [("k", 1, 1, 100.0 + 16.0, 10.0)]
+    lines, bad = ob.evaluate_counters(per)
+    assert ("k", "rud", "batch") == bad[0][:3] and bad[0][5] == 2

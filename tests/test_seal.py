@@ -7,7 +7,8 @@ Three independent implementations must agree:
   * the product library's host-side implementation (gvs_storage_seal_row,
     the same gvs_crypto.h code the gfx950 kernels run).
 Known-answer vectors: FIPS-197 Appendix C.1, SP 800-38A F.5.1, RFC 7693
-Appendix A.  Tag: H ^ G, H the header PRF; G the row hash of the message
+Appendix A.  Tag: H ^ G, H the header PRF (AES-128 of the row's nonce for the
+message tables, keyed BLAKE2b for the mailbox table); G the row hash of the message
 tables (UHASH-128 layers: NH, the one-block L2, the p36 L3; restated below in
 Python from its definition) or, for the mailbox table, the XOR of its four leaf
 PRFs (gvs_crypto.h).  The row hash has no published vector of its own (UMAC's
@@ -92,9 +93,16 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
         ct = bytes(np.frombuffer(pts[k], np.uint8) ^ ks[k, :1024])
         sct = bytes(np.frombuffer(side_pts[k], np.uint8) ^ ks[k, 1024:]) if side_pts is not None else None
         hdr = r.to_bytes(8, "little") + epoch.to_bytes(4, "little") + table.to_bytes(4, "little")
-        hdr += sct if sct is not None else bytes(16)
-        tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
-                                             person=b"gvs-head" + bytes(8)).digest(), "little")
+        if table & 1:
+            hdr += sct if sct is not None else bytes(16)
+            tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
+                                                 person=b"gvs-head" + bytes(8)).digest(), "little")
+        else:  # message tables: AES-128 under kh of the nonce (then of it ^ side ct)
+            kh = hashlib.blake2b(b"gvs storage head", key=secret, digest_size=16).digest()
+            h = openssl_ecb(kh, hdr)
+            if sct is not None:
+                h = openssl_ecb(kh, bytes(a ^ b for a, b in zip(h, sct)))
+            tag = int.from_bytes(h, "little")
         if table & 1:  # mailbox rows: 4 leaf PRFs of 256 B
             for i in range(4):
                 person = b"gvs-leaf" + i.to_bytes(4, "little") + (1).to_bytes(4, "little")
