@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--routed", action="store_true",
                    help="N=1: use the sharded store's routed path (one shard over RCCL)")
     p.add_argument("--auth", action="store_true",
-                   help="authenticated storage (AES-CTR + BLAKE2b sealed rows, BASELINE config 5 mode)")
+                   help="authenticated storage (AES-CTR sealed rows with a MAC per row, BASELINE config 5 mode)")
     p.add_argument("--sealed-waves", type=int, default=0, choices=(0, 4, 8, 12),
                    help="--auth: waves per workgroup of the sealed message pass (0: the store's choice)")
     p.add_argument("--mailbox-slots", type=int, default=256,
@@ -724,7 +724,7 @@ def main():
                     "kernel": "k_rpass2s (fixed-schedule message-table pass)",
                     "txn_slots": c, "alg_bytes_per_launch": alg_bytes, "kernel_ms": rpass_ms}
         if a.auth:
-            # sealed rows: the pass is bound by vector-ALU issue (AES + BLAKE2b),
+            # sealed rows: the pass is bound by vector-ALU issue (AES + the row MAC),
             # DESIGN.md §8; SQ_INSTS_VALU per launch from a --pmc pass
             # (tools/valu_from_pmc.py) over the HIP-event kernel time
             insts = None
@@ -789,7 +789,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded on device): 75% prefill, 25/25/25/25 CRUD mix, 50% next-message reads/deletes",
-            "config": {"workload": (f"C5 storage mode (AES-128-CTR + BLAKE2b sealed rows): " if a.auth else "C3: ")
+            "config": {"workload": (f"C5 storage mode (AES-128-CTR sealed rows, AES + NH/UHASH-128 MAC on message rows, BLAKE2b on mailbox rows): " if a.auth else "C3: ")
                        + f"2^{a.log2n} message capacity per GPU, {B}-request batches",
                        "msg_capacity": N, "batch": B,
                        "mailboxes": cfg.mailbox_partitions * cfg.mailbox_partition_slots,

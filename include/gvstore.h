@@ -90,7 +90,7 @@ extern "C" {
                                         secret_key before it could wrap */
 
 /* gvs_config.flags */
-#define GVS_FLAG_AUTH_STORAGE 1u /* AES-CTR + BLAKE2b sealed tables */
+#define GVS_FLAG_AUTH_STORAGE 1u /* AES-CTR sealed tables, a MAC per row */
 
 /* ---- records ------------------------------------------------------------- */
 

@@ -161,6 +161,12 @@ def test_counter_rerun_candidates():
     # most mixes biased the same way on one kernel: the reference is the suspect
     ref = [("k", m, "bias", -3.0, 1.0) for m in ("rud", "deletes", "hot_next")]
     assert ob.rerun_candidates(ref, mixes) == ["main"]
+    # ... and once main has been run again, the violating mixes are
+    assert ob.rerun_candidates(ref, mixes, fresh=("main",)) == ["rud", "deletes", "hot_next"]
+    # one process failing every launch of a repeated kernel is that process
+    rep = [("k_bitonic_tile", "hot_next", "bias", 0.33, 0.25)] * 6 + \
+        [("k_copy", "hot_next", "batch", 7.5, 2.56, 3, 4)]
+    assert ob.rerun_candidates(rep, mixes) == ["hot_next"]
 
 
 def test_counter_evaluation_flags_a_one_batch_excursion():

@@ -405,10 +405,14 @@ def rerun_candidates(bad, mixes, fresh=()):
     kernel's bias in the same direction.  Processes already run again are not
     candidates: their violations stand."""
     others = [m for m in mixes if m != "main"]
-    for k in {v[0] for v in bad if v[2] == "bias"}:
-        signs = [math.copysign(1, v[3]) for v in bad if v[0] == k and v[2] == "bias"]
-        if len(signs) > len(others) / 2 and abs(sum(signs)) == len(signs):
-            return [m for m in ["main"] if m not in fresh]
+    if "main" not in fresh:
+        for k in {v[0] for v in bad if v[2] == "bias"}:
+            # one vote per mix: a kernel name launched several times per batch
+            # (the sort stages) must not outvote the other mixes (r06i: six
+            # k_bitonic_tile launches of one hot_next process re-ran main)
+            signs = {v[1]: math.copysign(1, v[3]) for v in bad if v[0] == k and v[2] == "bias"}
+            if len(signs) > len(others) / 2 and abs(sum(signs.values())) == len(signs):
+                return ["main"]
     return [m for m in dict.fromkeys(v[1] for v in bad) if m not in fresh]
 
 
