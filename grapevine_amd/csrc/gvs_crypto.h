@@ -12,11 +12,11 @@
 //   H    = message tables: AES-128_kh(le64(row) | le32(e) | le32(table)),
 //          then AES-128_kh of that ^ side_ct for table 2 (head_aes;
 //          kh = BLAKE2b-128(key = secret, "gvs storage head"));
-//          mailbox table: BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+//          mailbox and map directory (1, 3): BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
 //                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
 //   tag  = H ^ G(ct)
-//   G    = message tables (table & 1 = 0: tables 0, 2 and 0x100): the row
-//          hash (round 6): the layers of UMAC's UHASH-128 (RFC 4418 §5) for
+//   G    = every table but the map directory (tables 0, 1, 2 and 0x100): the
+//          row hash (round 6): the layers of UMAC's UHASH-128 (RFC 4418 §5) for
 //          one 1024-byte block, four NH iterations over the row's 256
 //          little-endian words with the key shifted 16 bytes per iteration,
 //          each reduced to 32 bits by the p36 inner product (L3) and padded:
@@ -24,15 +24,15 @@
 //            Y_t = ((sum_c chunk_c(S_t) l3k[4t+c]) mod (2^36 - 5)) mod 2^32 ^ l3p[t]
 //          (chunk_c the 16-bit pieces of S_t, most significant first), keys
 //          from BLAKE2b-512(key = mac_key, "gvs-uhash-" | byte j), j < 19;
-//          mailbox table (1): the XOR of its four leaf PRFs
+//          map directory (3): the XOR of its four leaf PRFs
 //            L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(1),
 //                              leaf i of ct, 256 B)
-// The message tables' tag is a Carter-Wegman MAC: H is the PRF of a value
+// The row-hash tables' tag is a Carter-Wegman MAC: H is the PRF of a value
 // that is never sealed twice, (row, e, table), and G an almost-XOR-universal
 // hash of the row (UHASH-128's bound, ~2^-120 per forgery attempt; a store
 // stops at its first bad tag).  NH costs one 32x32->64 multiply-add per 8
 // bytes where BLAKE2b costs ~15 three-source operations: the sealed message
-// pass is bound by VALU issue.  The mailbox table keeps the
+// pass is bound by VALU issue.  The map directory keeps the
 // XOR-MAC with a counter term (Bellare-Guerin-Rogaway's XMACC).  The tag binds
 // row, table and epoch, so a replayed, moved or spliced row fails.  The key block of each keyed hash
 // depends only on (key, person): its state is computed once (SealCtx), so a
@@ -360,9 +360,9 @@ __host__ __device__ inline void row_hash_fin(const uint64_t s[4], const uint64_t
 struct SealCtx {
   AesRk rk;
   AesRk rkh;            // message tables' header PRF (head_aes)
-  B2State leafk1[4];    // keyed states after the key block: mailbox-table leaves (256 B)
+  B2State leafk1[4];    // keyed states after the key block: map-directory leaves (256 B)
   B2State headk;        // keyed state of the header PRF
-  const uint32_t* nhk;  // message row hash: the NH key (kNhWords words, device memory)
+  const uint32_t* nhk;  // the row hash's NH key (kNhWords words, device memory)
   uint64_t l3k[16];     // its L3 keys (< p36)
   uint32_t l3p[4];      // its L3 pads
   uint32_t epoch;       // rows are read at `epoch`, written at `epoch + 1`

@@ -2555,15 +2555,7 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
     header_prf(sc.headk, row, epoch, table, sd, t);
   else
     head_aes(sc.rkh, te0, row, epoch, table, side_pt ? sd : nullptr, t);
-  if (table & 1) {  // mailbox rows: 4 leaf PRFs of 256 B
-    for (uint32_t i = 0; i < 4; ++i) {
-      uint64_t m[32], l[2];
-      for (uint32_t k = 0; k < 32; ++k) m[k] = ld64(ct + 256 * i + 8 * k);
-      leaf_prf(sc.leafk1[i], m, l);
-      t[0] ^= l[0];
-      t[1] ^= l[1];
-    }
-  } else {  // message tables: the row hash, leaf by leaf as the kernels do
+  {  // the row hash (every table this function seals), leaf by leaf as the kernels do
     uint64_t sum[4] = {0, 0, 0, 0}, g[2];
     for (uint32_t i = 0; i < 8; ++i) {
       uint32_t w[32];

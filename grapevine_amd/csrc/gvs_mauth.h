@@ -10,7 +10,8 @@
 // time per row.  Here, as in the sealed message pass (gvs_spass.h):
 //   * a sealed mailbox table is stored in 16-row tiles (mtile_unit): the 16
 //     coalesced 1-KiB loads of a chunk leave leaf L & 3 (256 B) of row L >> 2
-//     in lane L's registers, so the leaf hashes and the CTR keystream
+//     in lane L's registers, so the row hash (NH over the leaf, the sums added
+//     over the row's four lanes; BLAKE2b leaf PRFs until round 6) and the CTR keystream
 //     (blocks 16 (L & 3) .. + 15 of the lane's row) work on registers;
 //   * the header PRFs are computed one row per thread for the partition at
 //     once: the read headers in the prepass (with the side entries' keystream
@@ -37,48 +38,52 @@ __device__ inline uint4* hole(uint32_t* s_te, uint32_t i) {
 }
 // hole slots: [0, 256) the waves' row buffers (64 each); then per row of the
 // partition: read header, side plaintext, side keystream at the write epoch
-// (the write pass turns it into the new side ciphertext), write leaf sum
+// (the write pass turns it into the new side ciphertext), write row hash G
 constexpr uint32_t kHoWst = 0, kHoHr = 256, kHoSide = kHoHr + kSrAuth, kHoKsw = kHoSide + kSrAuth,
                    kHoLsum = kHoKsw + kSrAuth;
 static_assert(kHoLsum + kSrAuth <= 2048, "the holes hold 2048 slots");
 
-// the 4 mailbox leaf keys' states in LDS (lane L reads leaf L & 3's)
-__device__ inline B2State leaf_key(const uint64_t* s_lk) {
-  B2State k;
-  const uint32_t leaf = lane_id() & 3u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) k.h[i] = s_lk[leaf * 8 + i];
-  return k;
+// The row hash's NH key (gvs_crypto.h) in LDS as four leaf windows: leaf l
+// needs key words 64 l .. 64 l + 75 (its 64 words and three 4-word shifts),
+// kept at s_nk + 76 l.  A stride of 76 words puts the four windows' 16-B reads
+// of one instruction in different banks (64 words would put them all in one).
+constexpr uint32_t kMNkWin = 76;
+__device__ inline void load_nk(uint32_t* s_nk, const uint32_t* nhk) {
+  for (uint32_t i = threadIdx.x; i < 4u * kMNkWin; i += blockDim.x)
+    s_nk[i] = nhk[64u * (i / kMNkWin) + i % kMNkWin];
 }
 
-// XOR of the row's four leaf PRFs (lanes 4u .. 4u + 3) over the lane's 256-B
-// leaf, in every lane of the row.  The leaf's two compressions share one copy
-// of the code: the halves of v are swapped between them (and back after).
-__device__ inline void leaf_sum4(const uint64_t* s_lk, uint4 (&v)[kMA], uint64_t r[2]) {
-  B2State k = leaf_key(s_lk);
-#pragma unroll 1
-  for (uint32_t blk = 0; blk < 2; ++blk) {
-    uint64_t m[16];
+// G of the lane's row (the row hash, gvs_crypto.h) in every lane of the row:
+// NH of the lane's 256-B leaf (lane L: leaf L & 3 of row L >> 2, v[i] its
+// words 4i .. 4i + 3) against the leaf's key window, the four sums added over
+// the row's four lanes, then L3.  Word pairs (4i, 4i + 1) and (4i + 2, 4i + 3)
+// meet key words 4(i + t) .. 4(i + t) + 3 of the window in iteration t: a
+// sliding window of four 16-B key reads.
+__device__ inline void mrow_hash(const uint32_t* s_nk, const SealCtx& c, const uint4 (&v)[kMA], uint64_t r[2]) {
+  const uint4* kp = reinterpret_cast<const uint4*>(s_nk + kMNkWin * (lane_id() & 3u));
+  uint64_t s[4] = {0, 0, 0, 0};
+  uint4 k0 = kp[0], k1 = kp[1], k2 = kp[2];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      m[2 * q] = u4lo(v[q]);
-      m[2 * q + 1] = u4hi(v[q]);
+  for (int i = 0; i < kMA; ++i) {
+    const uint4 k3 = kp[i + 3];
+    const uint4 kk[4] = {k0, k1, k2, k3};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t a0 = v[i].x + kk[t].x, b0 = v[i].y + kk[t].y;
+      const uint32_t a1 = v[i].z + kk[t].z, b1 = v[i].w + kk[t].w;
+      s[t] += (uint64_t)a0 * (uint64_t)b0;  // v_mad_u64_u32
+      s[t] += (uint64_t)a1 * (uint64_t)b1;
     }
-    b2_compress(k, m, 128u + 128u * (blk + 1u), blk == 1u);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 x = v[q];
-      v[q] = v[q + 8];
-      v[q + 8] = x;
-    }
+    k0 = k1;
+    k1 = k2;
+    k2 = k3;
   }
-  r[0] = k.h[0];
-  r[1] = k.h[1];
 #pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 1u));
-    r[w] ^= shfl_u64(r[w], (int)(lane_id() ^ 2u));
+  for (int t = 0; t < 4; ++t) {
+    s[t] += shfl_u64(s[t], (int)(lane_id() ^ 1u));
+    s[t] += shfl_u64(s[t], (int)(lane_id() ^ 2u));
   }
+  row_hash_fin(s, c.l3k, c.l3p, r);
 }
 
 // XOR the keystream of (mailbox table, row, epoch) blocks 16 (L & 3) .. + 15
@@ -192,12 +197,12 @@ __device__ inline void ma_prepass(const MArgs& a, uint32_t q, GroupM* g, uint32_
 
 // Verify and decrypt the chunk at the read epoch (rows j0 .. j0 + 15 of
 // partition q): a tag mismatch fails the batch and the handle for good.
-__device__ inline void ma_unseal(const MArgs& a, uint32_t* s_te, const uint64_t* s_lk, uint32_t q, uint32_t j0,
+__device__ inline void ma_unseal(const MArgs& a, uint32_t* s_te, const uint32_t* s_nk, uint32_t q, uint32_t j0,
                                  uint4 (&v)[kMA]) {
   const uint32_t lane = lane_id(), u = lane >> 2;
   const uint64_t row = (uint64_t)q * a.Sr + j0 + u;
   uint64_t ls[2];
-  leaf_sum4(s_lk, v, ls);
+  mrow_hash(s_nk, a.sc, v, ls);
   const uint4 hr = *hole(s_te, kHoHr + j0 + u);
   const uint4 want = a.btag[row];  // 16 rows' tags: two whole lines
   const bool bad = (u4lo(want) != (ls[0] ^ u4lo(hr))) | (u4hi(want) != (ls[1] ^ u4hi(hr)));
@@ -218,13 +223,13 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   __shared__ uint8_t s_tf[kGroupMax];
   __shared__ uint16_t s_tp[kGroupMax + 1];
   __shared__ int16_t s_tl[kGroupMax];
-  __shared__ uint64_t s_lk[4 * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t s_nk[4 * kMNkWin];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   load_te(s_te, a.te);
-  if (tid < 32) s_lk[tid] = a.sc.leafk1[tid >> 3].h[tid & 7u];
+  load_nk(s_nk, a.sc.nhk);
   const uint32_t ng = load_groups(a, q, g, &s_ng, false);
   if (tid == 0) {
     s_occ = 0;
@@ -273,7 +278,7 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   for (uint32_t j0 = wave * kMA; j0 < a.Sr; j0 += kRowWaves * kMA, ++ci) {
     uint4 v[kMA];
     ma_load(v, a.mbox, ((uint64_t)q * a.Sr + j0) / kMA);
-    ma_unseal(a, s_te, s_lk, q, j0, v);
+    ma_unseal(a, s_te, s_nk, q, j0, v);
     uint32_t mm = 0;
 #pragma unroll
     for (int u = 0; u < kMA; ++u) mm |= (s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
@@ -316,13 +321,13 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   __shared__ int16_t s_pend[kGroupMax + 1];
   __shared__ uint8_t s_ld[kGroupMax + 1];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta, s_tw[kRowWaves];
-  __shared__ uint64_t s_lk[4 * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t s_nk[4 * kMNkWin];
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   load_te(s_te, a.te);
-  if (tid < 32) s_lk[tid] = a.sc.leafk1[tid >> 3].h[tid & 7u];
+  load_nk(s_nk, a.sc.nhk);
   uint4* side = a.side + (uint64_t)q * a.Sr;
   const uint32_t ng = load_groups(a, q, g, &s_ng, true);
   if (tid == 0) {
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
     const uint32_t u = ln >> 2;
     const uint64_t row = (uint64_t)q * a.Sr + j0 + u;
     // four jobs, one copy of each crypto step: 0 verify, 1 decrypt and the
-    // mailbox steps, 2 re-encrypt, 3 the new leaf sums and the stores.  The
+    // mailbox steps, 2 re-encrypt, 3 the new row hashes and the stores.  The
     // unrolled sequence (220 KB of code; k_m1a's 112 KB) made the read pass's
     // FETCH_SIZE follow the request mix by 17-30 KiB under the all-miss and
     // hot mixes (profiles/r05e_*, r05h_*), where the rolled form is flat
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
       if (job == 0u) ma_load(v, a.mbox, t);
       if (job == 0u || job == 3u) {
         uint64_t ls[2];
-        leaf_sum4(s_lk, v, ls);
+        mrow_hash(s_nk, a.sc, v, ls);
         if (job == 0u) {  // the read tag: H at the read epoch (prepass) over the old side ciphertext
           const uint4 hr = *hole(s_te, kHoHr + j0 + u);
           const uint4 want = a.btag[row];  // 16 rows' tags: two whole lines

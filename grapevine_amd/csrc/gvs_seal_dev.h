@@ -389,16 +389,16 @@ __device__ inline B2State b2_sel(bool c, const B2State& a, const B2State& b) {
 
 // Tag of row row0 + (lane >> 2) % U, over the ciphertext rows already in the
 // stage: tag = H ^ L_0 ^ .. ^ L_(NL-1) (gvs_crypto.h).
-//  * NL = 4 (mailbox rows, 256-B leaves): lane L computes leaf L & 3 of row
+//  * NL = 4 (map directory rows, 256-B leaves): lane L computes leaf L & 3 of row
 //    (L >> 2) % U; the quad XORs its four leaves by shuffles.
 //    - U <= 8 (side entries staged at st[U*4*kSegU4 + u]): lanes 32 + u
 //      compute H of row u in the same instructions (their first compression
 //      takes the header block instead of leaf data), so the header costs no
 //      extra time.  htab: the header's table field in this lane's header row.
 //    - U = 16: every lane hashes a leaf; `hdr` is H of the lane's row.
-//  * NL = 8 (message tables, 128-B leaves, one compression each): lane L
+//  * NL = 8 (the row hash: message and mailbox tables, 128-B leaves): lane L
 //    computes leaf L & 7 of row L >> 3 (U = 8), or of rows L >> 3 and
-//    (L >> 3) + 8 (U = 16); the 8 lanes of a row XOR their leaves, and every
+//    (L >> 3) + 8 (U = 16); the 8 lanes of a row add their NH sums, and every
 //    lane then takes its row's sum.  `hdr` is H of the lane's row (the
 //    message pass computes it for 64 rows at once).
 // Valid in lanes < 4U.
@@ -619,10 +619,9 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
       header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);
     else  // message tables (gvs_crypto.h head_aes)
       head_aes(c.rkh, lds_te(s_te), r0 + ((lane >> 2) % U), 0u, table, nullptr, hdr);
-    if (side)
-      wave_seal<U, 4>(c, s_te, table, r0, 0u, v, tags, true, st, hdr);
-    else  // message tables: 8 leaves of 128 B
-      wave_seal<U, 8>(c, s_te, table, r0, 0u, v, tags, false, st, hdr);
+    // the row hash (NH over 8 leaves of 128 B) for the message tables and,
+    // since round 6, the mailbox table
+    wave_seal<U, 8>(c, s_te, table, r0, 0u, v, tags, side != nullptr, st, hdr);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (side)  // the mailbox table: 16-row tiles (mtile_unit)

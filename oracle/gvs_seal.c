@@ -283,12 +283,14 @@ void gvo_row_hash(const uint32_t nh[268], const uint64_t l3k[16], const uint32_t
  *         for table 2 (side entry) AES-128_kh(that ^ side ct);
  *         mailbox table: BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
  *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
- *   G   = gvo_row_hash(ct) for the message tables (table & 1 = 0: a
- *         Carter-Wegman MAC, H the PRF of a nonce never sealed twice);
- *         for the mailbox table the XOR of its 4 leaf PRFs
+ *   G   = gvo_row_hash(ct) for every table but the map directory (a
+ *         Carter-Wegman MAC, H the PRF of a nonce never sealed twice; the
+ *         mailbox table since the end of round 6);
+ *         for the map directory (table 3) the XOR of its 4 leaf PRFs
  *         L_i = BLAKE2b-128(key = mac_key, person = "gvs-leaf" | le32(i) | le32(1), leaf i of 256 B)
  * table: 0 message rows, 1 mailbox rows, 2 pending final states (P, by
- * position, side = target row), 0x100 a message row whose final state is
+ * position, side = target row), 3 the key-value map's directory rows,
+ * 0x100 a message row whose final state is
  * pending in P (header only: its keystream and leaves are table 0's; the CTR
  * block carries the table's low byte). 
  * side_pt may be NULL (message rows); then side_ct is not written and 16 zero
@@ -336,7 +338,7 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   } else {
     gvo_blake2b(mk, 32, head_person, hdr, sizeof hdr, tag, 16);
   }
-  if (!(table & 1)) { /* message tables: the row hash */
+  if (table != 3) { /* every table but the map directory: the row hash */
     uint32_t nh[268], l3p[4];
     uint64_t l3k[16];
     uint8_t g[16];
@@ -345,7 +347,7 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
     for (int k = 0; k < 16; ++k) tag[k] ^= g[k];
     return;
   }
-  /* mailbox table: 4 leaves of 256 B */
+  /* map directory: 4 leaves of 256 B */
   const uint32_t nl = 4, lb = 1024 / nl;
   for (uint32_t i = 0; i < nl; ++i) {
     uint8_t person[16] = {'g', 'v', 's', '-', 'l', 'e', 'a', 'f'}, l[16];

@@ -103,12 +103,12 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
             if sct is not None:
                 h = openssl_ecb(kh, bytes(a ^ b for a, b in zip(h, sct)))
             tag = int.from_bytes(h, "little")
-        if table & 1:  # mailbox rows: 4 leaf PRFs of 256 B
+        if table == 3:  # map directory rows: 4 leaf PRFs of 256 B
             for i in range(4):
                 person = b"gvs-leaf" + i.to_bytes(4, "little") + (1).to_bytes(4, "little")
                 tag ^= int.from_bytes(hashlib.blake2b(ct[256 * i:256 * i + 256], key=mk, digest_size=16,
                                                       person=person).digest(), "little")
-        else:  # message tables: the row hash
+        else:  # every other table: the row hash
             tag ^= int.from_bytes(py_row_hash(py_uhash_keys(secret), ct), "little")
         out.append((ct, sct, tag.to_bytes(16, "little")))
     return out
