@@ -9,11 +9,12 @@
 //   keystream block j = AES_k(le64(row) | le32(e) | table | 0 | be16(j))
 //                       (standard CTR, counter in the last two bytes)
 //   ct_j = pt_j ^ keystream_j          (j = 0..63 row, j = 64 side entry)
-//   H    = message tables: AES-128_kh(le64(row) | le32(e) | le32(table)),
-//          then AES-128_kh of that ^ side_ct for table 2 (head_aes;
-//          kh = BLAKE2b-128(key = secret, "gvs storage head"));
-//          mailbox and map directory (1, 3): BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
-//                      le64(row) | le32(e) | le32(table) | side_ct or 0^16)
+//   H    = every table but the map directory: AES-128_kh(le64(row) | le32(e) |
+//          le32(table)), then AES-128_kh of that ^ side_ct for the tables with a
+//          side entry, 1 and 2 (head_aes; kh = BLAKE2b-128(key = secret,
+//          "gvs storage head"));
+//          map directory (3): BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+//                      le64(row) | le32(e) | le32(table) | 0^16)
 //   tag  = H ^ G(ct)
 //   G    = every table but the map directory (tables 0, 1, 2 and 0x100): the
 //          row hash (round 6): the layers of UMAC's UHASH-128 (RFC 4418 §5) for
@@ -82,7 +83,7 @@ __host__ __device__ inline uint32_t te_at(const uint32_t* tab, uint32_t s, int k
 }
 
 template <typename Tab>
-__host__ __device__ inline void aes128_encrypt_words(const AesRk& rk, const Tab& te0, uint32_t s0,
+__host__ __device__ __attribute__((always_inline)) inline void aes128_encrypt_words(const AesRk& rk, const Tab& te0, uint32_t s0,
                                                      uint32_t s1, uint32_t s2, uint32_t s3,
                                                      uint32_t out[4]) {
   s0 ^= rk.w[0];
@@ -126,21 +127,30 @@ __host__ __device__ inline uint4 ctr_keystream(const AesRk& rk, const Tab& te0, 
   return make_uint4(bswap32(o[0]), bswap32(o[1]), bswap32(o[2]), bswap32(o[3]));
 }
 
-// H of a message-table row (table & 1 = 0): AES-128 under kh of the nonce
-// le64(row) | le32(epoch) | le32(table), and for the tables with a side entry
-// (P, table 2) AES again of that XOR the side ciphertext: a PRF of a fixed-
+// H of a row of every table but the map directory: AES-128 under kh of the
+// nonce le64(row) | le32(epoch) | le32(table), and for the tables with a side
+// entry (mailboxes 1, P 2) AES again of that XOR the side ciphertext: a PRF of a fixed-
 // length input per table.  out = H as two little-endian 64-bit words.
 template <typename Tab>
-__host__ __device__ inline void head_aes(const AesRk& rkh, const Tab& te0, uint64_t row, uint32_t epoch,
-                                         uint32_t table, const uint64_t* side, uint64_t out[2]) {
+__host__ __device__ __attribute__((always_inline)) inline void head_aes_w(const AesRk& rkh, const Tab& te0,
+                                                                         uint64_t row, uint32_t epoch,
+                                                                         uint32_t table, bool with_side,
+                                                                         uint64_t s0, uint64_t s1,
+                                                                         uint64_t out[2]) {
   uint32_t o[4];
   aes128_encrypt_words(rkh, te0, bswap32((uint32_t)row), bswap32((uint32_t)(row >> 32)), bswap32(epoch),
                        bswap32(table), o);
-  if (side)
-    aes128_encrypt_words(rkh, te0, o[0] ^ bswap32((uint32_t)side[0]), o[1] ^ bswap32((uint32_t)(side[0] >> 32)),
-                         o[2] ^ bswap32((uint32_t)side[1]), o[3] ^ bswap32((uint32_t)(side[1] >> 32)), o);
+  if (with_side)
+    aes128_encrypt_words(rkh, te0, o[0] ^ bswap32((uint32_t)s0), o[1] ^ bswap32((uint32_t)(s0 >> 32)),
+                         o[2] ^ bswap32((uint32_t)s1), o[3] ^ bswap32((uint32_t)(s1 >> 32)), o);
   out[0] = (uint64_t)bswap32(o[0]) | ((uint64_t)bswap32(o[1]) << 32);
   out[1] = (uint64_t)bswap32(o[2]) | ((uint64_t)bswap32(o[3]) << 32);
+}
+template <typename Tab>
+__host__ __device__ __attribute__((always_inline)) inline void head_aes(const AesRk& rkh, const Tab& te0, uint64_t row,
+                                                                       uint32_t epoch, uint32_t table,
+                                                                       const uint64_t* side, uint64_t out[2]) {
+  head_aes_w(rkh, te0, row, epoch, table, side != nullptr, side ? side[0] : 0ull, side ? side[1] : 0ull, out);
 }
 
 // --------------------------------------------------------------- BLAKE2b
@@ -303,18 +313,6 @@ __host__ __device__ inline void header_block(uint64_t row, uint32_t epoch, uint3
   m[3] = side[1];
 #pragma unroll
   for (int k = 4; k < 16; ++k) m[k] = 0;
-}
-
-// H of one row
-__host__ __device__ __attribute__((always_inline)) inline void header_prf(
-    const B2State& k, uint64_t row, uint32_t epoch, uint32_t table, const uint64_t side[2],
-    uint64_t out[2]) {
-  uint64_t m[16];
-  header_block(row, epoch, table, side, m);
-  B2State s = k;
-  b2_compress(s, m, 128 + 32, true);
-  out[0] = s.h[0];
-  out[1] = s.h[1];
 }
 
 // ------------------------------------------------------- message row hash

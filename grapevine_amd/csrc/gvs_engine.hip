@@ -2551,10 +2551,7 @@ int gvs_storage_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row,
     sd[1] = ld64(side_ct + 8);
   }
   uint64_t t[2];
-  if (table & 1)
-    header_prf(sc.headk, row, epoch, table, sd, t);
-  else
-    head_aes(sc.rkh, te0, row, epoch, table, side_pt ? sd : nullptr, t);
+  head_aes(sc.rkh, te0, row, epoch, table, side_pt ? sd : nullptr, t);
   {  // the row hash (every table this function seals), leaf by leaf as the kernels do
     uint64_t sum[4] = {0, 0, 0, 0}, g[2];
     for (uint32_t i = 0; i < 8; ++i) {

@@ -48,9 +48,25 @@ static_assert(kHoLsum + kSrAuth <= 2048, "the holes hold 2048 slots");
 // kept at s_nk + 76 l.  A stride of 76 words puts the four windows' 16-B reads
 // of one instruction in different banks (64 words would put them all in one).
 constexpr uint32_t kMNkWin = 76;
-__device__ inline void load_nk(uint32_t* s_nk, const uint32_t* nhk) {
+// the key windows, then the L3 keys and pads (kept in LDS rather than in
+// scalar registers: the passes' round keys already fill those)
+struct MNk {
+  uint32_t w[4 * kMNkWin];
+  uint64_t l3k[16];
+  uint32_t l3p[4];
+  AesRk rkh;  // the header PRF's round keys (read by the per-row header loops)
+};
+__device__ inline void load_nk(MNk* s, const SealCtx& c) {
   for (uint32_t i = threadIdx.x; i < 4u * kMNkWin; i += blockDim.x)
-    s_nk[i] = nhk[64u * (i / kMNkWin) + i % kMNkWin];
+    s->w[i] = c.nhk[64u * (i / kMNkWin) + i % kMNkWin];
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s->l3k[i] = c.l3k[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s->l3p[i] = c.l3p[i];
+#pragma unroll
+    for (int i = 0; i < 44; ++i) s->rkh.w[i] = c.rkh.w[i];
+  }
 }
 
 // G of the lane's row (the row hash, gvs_crypto.h) in every lane of the row:
@@ -59,8 +75,8 @@ __device__ inline void load_nk(uint32_t* s_nk, const uint32_t* nhk) {
 // the row's four lanes, then L3.  Word pairs (4i, 4i + 1) and (4i + 2, 4i + 3)
 // meet key words 4(i + t) .. 4(i + t) + 3 of the window in iteration t: a
 // sliding window of four 16-B key reads.
-__device__ inline void mrow_hash(const uint32_t* s_nk, const SealCtx& c, const uint4 (&v)[kMA], uint64_t r[2]) {
-  const uint4* kp = reinterpret_cast<const uint4*>(s_nk + kMNkWin * (lane_id() & 3u));
+__device__ inline void mrow_hash(const MNk* s_nk, const uint4 (&v)[kMA], uint64_t r[2]) {
+  const uint4* kp = reinterpret_cast<const uint4*>(s_nk->w + kMNkWin * (lane_id() & 3u));
   uint64_t s[4] = {0, 0, 0, 0};
   uint4 k0 = kp[0], k1 = kp[1], k2 = kp[2];
 #pragma unroll
@@ -83,7 +99,7 @@ __device__ inline void mrow_hash(const uint32_t* s_nk, const SealCtx& c, const u
     s[t] += shfl_u64(s[t], (int)(lane_id() ^ 1u));
     s[t] += shfl_u64(s[t], (int)(lane_id() ^ 2u));
   }
-  row_hash_fin(s, c.l3k, c.l3p, r);
+  row_hash_fin(s, s_nk->l3k, s_nk->l3p, r);
 }
 
 // XOR the keystream of (mailbox table, row, epoch) blocks 16 (L & 3) .. + 15
@@ -168,12 +184,26 @@ __device__ inline void ma_load(uint4 (&v)[kMA], const uint4* mbox, uint64_t t) {
 // side keystream at the write epoch.  One row per thread.
 template <bool WR>
 __device__ inline void ma_prepass(const MArgs& a, uint32_t q, GroupM* g, uint32_t ng, int16_t* s_sg,
-                                  uint8_t* s_occb, uint32_t* s_occ, uint32_t* s_te) {
+                                  uint8_t* s_occb, uint32_t* s_occ, uint32_t* s_te, const MNk* s_nk) {
   const LdsTe te = lds_te(s_te);
   for (uint32_t j = threadIdx.x; j < a.Sr; j += 256) {
     const uint64_t row = (uint64_t)q * a.Sr + j;
     const uint4 sct = a.side[row];
-    const uint4 sd = xor4(sct, ctr_keystream(a.sc.rk, te, 1u, row, a.sc.epoch, 64u));
+    // the side entry's keystream at the read epoch (and, writing, at epoch + 1:
+    // through one copy of the AES code, which keeps k_m2a's code well inside
+    // the instruction cache)
+    uint4 ksr = make_uint4(0, 0, 0, 0), ksw = ksr;
+    if constexpr (WR) {
+#pragma unroll 1
+      for (uint32_t w = 0; w < 2u; ++w) {
+        const uint4 k = ctr_keystream(a.sc.rk, te, 1u, row, a.sc.epoch + w, 64u);
+        ksr = sel4(w == 0u, k, ksr);
+        ksw = k;
+      }
+    } else {
+      ksr = ctr_keystream(a.sc.rk, te, 1u, row, a.sc.epoch, 64u);
+    }
+    const uint4 sd = xor4(sct, ksr);
     const uint64_t hi = u4lo(sd), w1 = u4hi(sd);
     const bool occ = (w1 & 1u) != 0;
     const int kf = find_group_m(g, ng, a.cm, hi, w1 >> 23);
@@ -184,25 +214,24 @@ __device__ inline void ma_prepass(const MArgs& a, uint32_t q, GroupM* g, uint32_
     g[kk].len = (uint32_t)(w1 >> 1) & 63u;
     s_sg[j] = (int16_t)k;
     s_occb[j] = occ ? 1 : 0;
-    const uint64_t sv[2] = {u4lo(sct), u4hi(sct)};
     uint64_t h[2];
-    header_prf(a.sc.headk, row, a.sc.epoch, 1u, sv, h);
+    head_aes_w(s_nk->rkh, te, row, a.sc.epoch, 1u, true, u4lo(sct), u4hi(sct), h);
     *hole(s_te, kHoHr + j) = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
     if (WR) {
       *hole(s_te, kHoSide + j) = sd;
-      *hole(s_te, kHoKsw + j) = ctr_keystream(a.sc.rk, te, 1u, row, a.sc.epoch + 1u, 64u);
+      *hole(s_te, kHoKsw + j) = ksw;
     }
   }
 }
 
 // Verify and decrypt the chunk at the read epoch (rows j0 .. j0 + 15 of
 // partition q): a tag mismatch fails the batch and the handle for good.
-__device__ inline void ma_unseal(const MArgs& a, uint32_t* s_te, const uint32_t* s_nk, uint32_t q, uint32_t j0,
+__device__ inline void ma_unseal(const MArgs& a, uint32_t* s_te, const MNk* s_nk, uint32_t q, uint32_t j0,
                                  uint4 (&v)[kMA]) {
   const uint32_t lane = lane_id(), u = lane >> 2;
   const uint64_t row = (uint64_t)q * a.Sr + j0 + u;
   uint64_t ls[2];
-  mrow_hash(s_nk, a.sc, v, ls);
+  mrow_hash(s_nk, v, ls);
   const uint4 hr = *hole(s_te, kHoHr + j0 + u);
   const uint4 want = a.btag[row];  // 16 rows' tags: two whole lines
   const bool bad = (u4lo(want) != (ls[0] ^ u4lo(hr))) | (u4hi(want) != (ls[1] ^ u4hi(hr)));
@@ -223,20 +252,20 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   __shared__ uint8_t s_tf[kGroupMax];
   __shared__ uint16_t s_tp[kGroupMax + 1];
   __shared__ int16_t s_tl[kGroupMax];
-  __shared__ __attribute__((aligned(16))) uint32_t s_nk[4 * kMNkWin];
+  __shared__ __attribute__((aligned(16))) MNk s_nk;
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   load_te(s_te, a.te);
-  load_nk(s_nk, a.sc.nhk);
+  load_nk(&s_nk, a.sc);
   const uint32_t ng = load_groups(a, q, g, &s_ng, false);
   if (tid == 0) {
     s_occ = 0;
     s_empt = 0;
   }
   __syncthreads();
-  ma_prepass<false>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  ma_prepass<false>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te, &s_nk);
   __syncthreads();
   // admission (grapevine.proto:74), as k_m1x
   count_empty(g, ng, a.cm, &s_empt);
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(256, 2) void k_m1a(MArgs a) {
   for (uint32_t j0 = wave * kMA; j0 < a.Sr; j0 += kRowWaves * kMA, ++ci) {
     uint4 v[kMA];
     ma_load(v, a.mbox, ((uint64_t)q * a.Sr + j0) / kMA);
-    ma_unseal(a, s_te, s_nk, q, j0, v);
+    ma_unseal(a, s_te, &s_nk, q, j0, v);
     uint32_t mm = 0;
 #pragma unroll
     for (int u = 0; u < kMA; ++u) mm |= (s_sg[j0 + u] >= 0) ? (1u << u) : 0u;
@@ -321,13 +350,13 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   __shared__ int16_t s_pend[kGroupMax + 1];
   __shared__ uint8_t s_ld[kGroupMax + 1];
   __shared__ uint32_t s_w[4], s_ng, s_occ, s_delta, s_tw[kRowWaves];
-  __shared__ __attribute__((aligned(16))) uint32_t s_nk[4 * kMNkWin];
+  __shared__ __attribute__((aligned(16))) MNk s_nk;
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t q = blockIdx.x;
   if (a.scal->error) return;
   load_te(s_te, a.te);
-  load_nk(s_nk, a.sc.nhk);
+  load_nk(&s_nk, a.sc);
   uint4* side = a.side + (uint64_t)q * a.Sr;
   const uint32_t ng = load_groups(a, q, g, &s_ng, true);
   if (tid == 0) {
@@ -335,7 +364,7 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
     s_delta = 0;
   }
   __syncthreads();
-  ma_prepass<true>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te);
+  ma_prepass<true>(a, q, g, ng, s_sg, s_occb, &s_occ, s_te, &s_nk);
   __syncthreads();
   // final lengths, placement of new recipients, the slot each touched row
   // takes: as k_m2x
@@ -447,7 +476,7 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
       if (job == 0u) ma_load(v, a.mbox, t);
       if (job == 0u || job == 3u) {
         uint64_t ls[2];
-        mrow_hash(s_nk, a.sc, v, ls);
+        mrow_hash(&s_nk, v, ls);
         if (job == 0u) {  // the read tag: H at the read epoch (prepass) over the old side ciphertext
           const uint4 hr = *hole(s_te, kHoHr + j0 + u);
           const uint4 want = a.btag[row];  // 16 rows' tags: two whole lines
@@ -500,9 +529,8 @@ __global__ __launch_bounds__(256, GVS_M2A_WGS) void k_m2a(MArgs a) {
   for (uint32_t j = tid; j < a.Sr; j += 256) {
     const uint64_t row = (uint64_t)q * a.Sr + j;
     const uint4 sct = *hole(s_te, kHoKsw + j), ls = *hole(s_te, kHoLsum + j);
-    const uint64_t sv[2] = {u4lo(sct), u4hi(sct)};
     uint64_t h[2];
-    header_prf(a.sc.headk, row, ep, 1u, sv, h);
+    head_aes_w(s_nk.rkh, lds_te(s_te), row, ep, 1u, true, u4lo(sct), u4hi(sct), h);
     const uint64_t t0 = h[0] ^ u4lo(ls), t1 = h[1] ^ u4hi(ls);
     a.btag[row] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
   }

@@ -615,9 +615,10 @@ __global__ __launch_bounds__(256) void k_seal_init(SealCtx c, const uint32_t* g_
       sd[0] = u4lo(x);
       sd[1] = u4hi(x);
     }
-    if (side)  // one-time: no amortising
-      header_prf(c.headk, r0 + ((lane >> 2) % U), 0u, table, sd, hdr);
-    else  // message tables (gvs_crypto.h head_aes)
+    // (two call sites rather than a pointer select, which would put sd in scratch)
+    if (side)
+      head_aes(c.rkh, lds_te(s_te), r0 + ((lane >> 2) % U), 0u, table, sd, hdr);
+    else
       head_aes(c.rkh, lds_te(s_te), r0 + ((lane >> 2) % U), 0u, table, nullptr, hdr);
     // the row hash (NH over 8 leaves of 128 B) for the message tables and,
     // since round 6, the mailbox table

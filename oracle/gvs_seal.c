@@ -279,10 +279,10 @@ void gvo_row_hash(const uint32_t nh[268], const uint64_t l3k[16], const uint32_t
 }
 
 /* Seal one row: ct = pt ^ AES-CTR keystream; tag = H ^ G, with
- *   H   = message tables (table & 1 = 0): AES-128_kh(le64(row) | le32(epoch) | le32(table)),
- *         for table 2 (side entry) AES-128_kh(that ^ side ct);
- *         mailbox table: BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
- *                     le64(row) | le32(epoch) | le32(table) | side ct or 0^16)
+ *   H   = every table but the map directory: AES-128_kh(le64(row) | le32(epoch) | le32(table)),
+ *         for the tables with a side entry (1, 2) AES-128_kh(that ^ side ct);
+ *         map directory (3): BLAKE2b-128(key = mac_key, person = "gvs-head" | 0^8,
+ *                     le64(row) | le32(epoch) | le32(table) | 0^16)
  *   G   = gvo_row_hash(ct) for every table but the map directory (a
  *         Carter-Wegman MAC, H the PRF of a nonce never sealed twice; the
  *         mailbox table since the end of round 6);
@@ -321,10 +321,10 @@ void gvo_seal_row(const uint8_t secret[32], uint32_t table, uint64_t row, uint32
   put_le(hdr + 8, epoch, 4);
   put_le(hdr + 12, table, 4);
   if (side_pt) memcpy(hdr + 16, side_ct, 16);
-  if (!(table & 1)) {
-    /* message tables: H = AES_kh(nonce), or AES_kh(AES_kh(nonce) ^ side ct)
-     * for the tables with a side entry (P, table 2): a PRF of a fixed-length
-     * input per table, kh = BLAKE2b-128(key = secret, "gvs storage head") */
+  if (table != 3) {
+    /* H = AES_kh(nonce), or AES_kh(AES_kh(nonce) ^ side ct) for the tables
+     * with a side entry (mailboxes, table 1; P, table 2): a PRF of a
+     * fixed-length input per table, kh = BLAKE2b-128(key = secret, "gvs storage head") */
     static const char hk[] = "gvs storage head";
     uint8_t kh[16], rkh[176];
     gvo_blake2b(secret, 32, NULL, (const uint8_t *)hk, sizeof hk - 1, kh, 16);

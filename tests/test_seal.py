@@ -93,11 +93,11 @@ def py_seal_rows(secret, table, rows, epoch, pts, side_pts=None):
         ct = bytes(np.frombuffer(pts[k], np.uint8) ^ ks[k, :1024])
         sct = bytes(np.frombuffer(side_pts[k], np.uint8) ^ ks[k, 1024:]) if side_pts is not None else None
         hdr = r.to_bytes(8, "little") + epoch.to_bytes(4, "little") + table.to_bytes(4, "little")
-        if table & 1:
+        if table == 3:  # map directory rows
             hdr += sct if sct is not None else bytes(16)
             tag = int.from_bytes(hashlib.blake2b(hdr, key=mk, digest_size=16,
                                                  person=b"gvs-head" + bytes(8)).digest(), "little")
-        else:  # message tables: AES-128 under kh of the nonce (then of it ^ side ct)
+        else:  # AES-128 under kh of the nonce (then of it ^ side ct)
             kh = hashlib.blake2b(b"gvs storage head", key=secret, digest_size=16).digest()
             h = openssl_ecb(kh, hdr)
             if sct is not None:
