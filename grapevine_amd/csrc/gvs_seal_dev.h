@@ -346,6 +346,59 @@ __device__ inline void ctr_keystream_jn2(const AesRk& rk, const LdsTe& te, const
   for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
 }
 
+// Round 2 cached as well (the two-table window): after round 1 only word 0
+// of the state differs between a lane's blocks, and each round-2 column reads
+// exactly one byte of word 0 (column 0: T0[w0.b3]; 1: T1[w0.b0] in the ror16
+// pair; 2: T0[w0.b1] in the ror16 pair; 3: T1[w0.b2]).  The other twelve
+// lookups and the round key are folded once per row into f[]; per block,
+// round 2 costs four lookups instead of sixteen (the sealed message pass is
+// bound by its LDS lookups).
+struct CtrRound2J {
+  uint32_t f[4];  // round-2 columns without their word-0 terms
+  uint32_t t0;    // round-1 word 0 without its block term (CtrRound1J::t[0])
+  uint32_t x3b0;  // as CtrRound1J
+};
+
+__device__ inline CtrRound2J ctr_round2_row(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1) {
+  const uint32_t s1 = c1.t[1], s2 = c1.t[2], s3 = c1.t[3];
+  CtrRound2J c;
+  c.f[0] = te1_at(te, s1, 2) ^ ror32(te_at(te, s2, 1) ^ te1_at(te, s3, 0), 16) ^ rk.w[8];
+  c.f[1] = te_at(te, s1, 3) ^ te1_at(te, s2, 2) ^ ror32(te_at(te, s3, 1), 16) ^ rk.w[9];
+  c.f[2] = te_at(te, s2, 3) ^ te1_at(te, s3, 2) ^ ror32(te1_at(te, s1, 0), 16) ^ rk.w[10];
+  c.f[3] = te_at(te, s3, 3) ^ ror32(te_at(te, s1, 1) ^ te1_at(te, s2, 0), 16) ^ rk.w[11];
+  c.t0 = c1.t[0];
+  c.x3b0 = c1.x3b0;
+  return c;
+}
+
+// keystream blocks j0 + i0 .. j0 + i0 + NB - 1 of the row from round 3 on
+template <int NB>
+__device__ inline void ctr_keystream_jn3(const AesRk& rk, const LdsTe& te, const CtrRound2J& c2, uint32_t i0,
+                                         uint4 (&ks)[NB]) {
+  uint32_t w0[NB], l[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) w0[b] = c2.t0 ^ ror32(te_at(te, c2.x3b0 ^ (i0 + (uint32_t)b), 0), 24);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    l[b][0] = te_at(te, w0[b], 3);
+    l[b][1] = te1_at(te, w0[b], 0);
+    l[b][2] = te_at(te, w0[b], 1);
+    l[b][3] = te1_at(te, w0[b], 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    s[b][0] = c2.f[0] ^ l[b][0];
+    s[b][1] = c2.f[1] ^ ror32(l[b][1], 16);
+    s[b][2] = c2.f[2] ^ ror32(l[b][2], 16);
+    s[b][3] = c2.f[3] ^ l[b][3];
+  }
+  aes128_rounds_n2<3, NB>(rk, te, s);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
+}
+
 // The tile layout of a sealed message (or block) table: rows in tiles of 8
 // (8 KiB); inside a tile, 16-B unit i * 64 + L holds block 8 (L & 7) + i of
 // row L >> 3.  A wave's coalesced load of unit i into lane L (8 whole-KiB

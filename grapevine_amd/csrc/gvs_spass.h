@@ -175,6 +175,9 @@ __device__ inline B2State opaque(const B2State& k) {
 #ifndef GVS_SP_NB
 #define GVS_SP_NB 2
 #endif
+#ifndef GVS_SP_R2
+#define GVS_SP_R2 1  // round 2 cached per row (ctr_round2_row); 0 in A/B builds only
+#endif
 __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[8]) {
   constexpr int NB = GVS_SP_NB;
   // the row's high word and the lane's block offset are the same for every
@@ -183,10 +186,14 @@ __device__ inline void lm_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, u
   // (a scratch reload in front of every keystream)
   const uint64_t r = ((uint64_t)opaque((uint32_t)(row >> 32)) << 32) | opaque((uint32_t)row);
   const CtrRound1J c1 = ctr_round1_row(c.rk, te, 0u, r, epoch, opaque((lane_id() & 7u) * 8u));
+  CtrRound2J c2{};
+  if (GVS_SP_DUAL && GVS_SP_R2) c2 = ctr_round2_row(c.rk, te, c1);
 #pragma unroll
   for (uint32_t i = 0; i < 8; i += NB) {
     uint4 ks[NB];
-    if (GVS_SP_DUAL)
+    if (GVS_SP_DUAL && GVS_SP_R2)
+      ctr_keystream_jn3<NB>(c.rk, te, c2, i, ks);
+    else if (GVS_SP_DUAL)
       ctr_keystream_jn2<NB>(c.rk, te, c1, i, ks);
     else
       ctr_keystream_jn<NB>(c.rk, te, c1, i, ks);
