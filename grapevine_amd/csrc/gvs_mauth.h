@@ -107,10 +107,11 @@ __device__ inline void mrow_hash(const MNk* s_nk, const uint4 (&v)[kMA], uint64_
 __device__ inline void ma_ctr(const SealCtx& c, const LdsTe& te, uint64_t row, uint32_t epoch, uint4 (&v)[kMA]) {
   constexpr int NB = 2;
   const CtrRound1J c1 = ctr_round1_row(c.rk, te, 1u, row, epoch, (lane_id() & 3u) * 16u);
+  const CtrRound2J c2 = ctr_round2_row1(c.rk, te, c1);  // round 2 cached too
 #pragma unroll
   for (uint32_t i = 0; i < kMA; i += NB) {
     uint4 ks[NB];
-    ctr_keystream_jn<NB, true>(c.rk, te, c1, i, ks);  // rounds rolled: code size (gvs_seal_dev.h)
+    ctr_keystream_jn3_1<NB, true>(c.rk, te, c2, i, ks);  // rounds rolled: code size (gvs_seal_dev.h)
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       v[i + b] = xor4(v[i + b], ks[b]);

@@ -399,6 +399,48 @@ __device__ inline void ctr_keystream_jn3(const AesRk& rk, const LdsTe& te, const
   for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
 }
 
+// The same for the one-table window (the sealed mailbox passes, gvs_mauth.h):
+// a column is T0[a] ^ ror8(T0[b]) ^ ror16(T0[c]) ^ ror24(T0[d]), word 0's
+// byte entering column 0 direct, column 1 as d, column 2 as c, column 3 as b.
+__device__ inline CtrRound2J ctr_round2_row1(const AesRk& rk, const LdsTe& te, const CtrRound1J& c1) {
+  const uint32_t s1 = c1.t[1], s2 = c1.t[2], s3 = c1.t[3];
+  CtrRound2J c;
+  c.f[0] = xor3(ror32(te_at(te, s1, 2), 8), ror32(te_at(te, s2, 1), 16), ror32(te_at(te, s3, 0), 24)) ^ rk.w[8];
+  c.f[1] = xor3(te_at(te, s1, 3), ror32(te_at(te, s2, 2), 8), ror32(te_at(te, s3, 1), 16)) ^ rk.w[9];
+  c.f[2] = xor3(te_at(te, s2, 3), ror32(te_at(te, s3, 2), 8), ror32(te_at(te, s1, 0), 24)) ^ rk.w[10];
+  c.f[3] = xor3(te_at(te, s3, 3), ror32(te_at(te, s1, 1), 16), ror32(te_at(te, s2, 0), 24)) ^ rk.w[11];
+  c.t0 = c1.t[0];
+  c.x3b0 = c1.x3b0;
+  return c;
+}
+
+template <int NB, bool ROLL = false>
+__device__ inline void ctr_keystream_jn3_1(const AesRk& rk, const LdsTe& te, const CtrRound2J& c2, uint32_t i0,
+                                           uint4 (&ks)[NB]) {
+  uint32_t w0[NB], l[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) w0[b] = c2.t0 ^ ror32(te_at(te, c2.x3b0 ^ (i0 + (uint32_t)b), 0), 24);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    l[b][0] = te_at(te, w0[b], 3);
+    l[b][1] = te_at(te, w0[b], 0);
+    l[b][2] = te_at(te, w0[b], 1);
+    l[b][3] = te_at(te, w0[b], 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    s[b][0] = c2.f[0] ^ l[b][0];
+    s[b][1] = c2.f[1] ^ ror32(l[b][1], 24);
+    s[b][2] = c2.f[2] ^ ror32(l[b][2], 16);
+    s[b][3] = c2.f[3] ^ ror32(l[b][3], 8);
+  }
+  aes128_rounds_n<3, NB, ROLL>(rk, te, s);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ks[b] = make_uint4(bswap32(s[b][0]), bswap32(s[b][1]), bswap32(s[b][2]), bswap32(s[b][3]));
+}
+
 // The tile layout of a sealed message (or block) table: rows in tiles of 8
 // (8 KiB); inside a tile, 16-B unit i * 64 + L holds block 8 (L & 7) + i of
 // row L >> 3.  A wave's coalesced load of unit i into lane L (8 whole-KiB
