@@ -185,6 +185,14 @@ case "$2" in
       step pmc_mix 400 bash tools/gpu_pmc_mix.sh ;;
   all) tests && bench && timing ;;
   full) tests && timing && step oblivious_all 1150 $PT tests/test_oblivious.py ;;
+  ktraffic)  # HBM traffic per launch of the headline path's larger kernels (two PMC passes, device batches only)
+    BA="python3 bench.py --no-cpu --steps 5 --warmup 1 --host-steps 0 --wire-steps 0"
+    step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- $BA && \
+    step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- $BA && \
+    for k in k_rpass2s k_m21x k_m1r_c k_rr2_c "k_vscan_a<gvs::Rr2Op>" k_copy k_out k_meta k_alloc_ring; do
+      python3 tools/traffic_from_pmc.py "$O/pmc_fetch" "$O/pmc_write" 24 65536 "$k" > "$O/traffic_$(echo $k | tr -c 'a-zA-Z0-9_\n' '_').json"
+    done
+    rm -rf "$O/pmc_fetch" "$O/pmc_write" ;;
   prof)  # HBM traffic of k_rpass2 (two PMC passes), kernel stats, auth and expiry lines
     step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --warmup 1
